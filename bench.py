@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the reference's per-pixel path on MI355X.
+
+Workload (BASELINE.json configs):
+  * restir (default): Renderer_TEST's live pipeline -- PT_01 G-buffer -> PT_1 initial
+    RIS candidates -> PT_4 final shading -- 1920x1080, 1 spp per frame, DUMMY_SCENE_1
+    (Cornell-style room, 22 294 triangles, 3 lights).  Temporal/spatial reuse are not
+    in the reference code and are not run here.
+  * mcpt: TEST_MCPT brute-force path tracer, same frame (configs[1]).
+A step = one frame (all passes) over the whole band; inputs (scene, uniform) are resident
+in HBM before the timed region.  Multi-GPU (torchrun): weak scaling, rank r renders rows
+[r*H, (r+1)*H) of a W x (H*N) frame with global pixel coordinates (no collective on the
+data path; only the timing barrier and a max-reduce of the elapsed time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
+# algorithmic bytes: 32 per slab test, 36 per triangle test, 48 per
+# instance transform, 48 per hit reconstruction; per-pixel pass IO below.
+B_AABB, B_TRI, B_INST, B_HIT = 32, 36, 48, 48
+PASS_IO = {"gbuffer": 16, "init": 16 + 128, "final": 16 + 128 + 16 + 16, "mcpt": 16 + 16}
+
+
+def ray_bytes(c: dict) -> int:
+    return B_AABB * c["aabb_tests"] + B_TRI * c["tri_tests"] + B_INST * c["instance_xforms"] + B_HIT * c["hits"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["restir", "mcpt"], default="restir")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--scene", default="dummy_scene_1")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend="nccl")
+
+    from pathtracerdemo_amd.renderer import Renderer
+    from pathtracerdemo_amd.scene.world import compile_scene
+    from pathtracerdemo_amd.scene.camera import Camera
+
+    W, Hb = args.width, args.height
+    H = Hb * world
+    cs = compile_scene(args.scene)
+    row_begin, row_end = rank * Hb, (rank + 1) * Hb
+    pipeline = args.workload
+    r = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end)
+    r.Initialize(cs)
+
+    # work census of the exact frame (counting build, untimed): algorithmic bytes
+    rc = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
+                  count_work=True)
+    rc.Initialize(cs)
+    rc.Update()
+    passes = ["gbuffer", "init", "final"] if pipeline == "restir" else ["mcpt"]
+    counts = {}
+    from pathtracerdemo_amd import _native as N
+    pid = {"gbuffer": N.PTX_PASS_GBUFFER, "init": N.PTX_PASS_INIT, "final": N.PTX_PASS_FINAL,
+           "mcpt": N.PTX_PASS_MCPT}
+    for p in passes:
+        rc.reset_stats()
+        rc.run_pass(pid[p])
+        rc.synchronize()
+        counts[p] = rc.read_counters()
+    rc.close()
+    px = W * Hb
+    alg_bytes = {p: ray_bytes(counts[p]) + PASS_IO[p] * px for p in passes}
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        r.Update()
+        r.Render()
+    r.synchronize()
+    r.reset_stats()
+    barrier()
+    r.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r.Update()
+        r.Render()
+    r.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = r.stats()
+    img = r.read_image()
+    nonfinite = int((~np.isfinite(img[..., :3])).sum())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    samples = W * H * args.steps  # all ranks, 1 spp
+    value = samples / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+    kms = {p: st["kernel_ms_total"][pid[p]] / max(1, st["kernel_launches"][pid[p]]) for p in passes}
+    dom = max(passes, key=lambda p: kms[p])
+    achieved = alg_bytes[dom] / (kms[dom] * 1e-3) / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    if os.path.exists(prof):
+        try:
+            traffic = json.load(open(prof)).get(f"{pipeline}:{dom}:{W}x{Hb}")
+        except Exception:
+            traffic = None
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads)
+    line = {
+        "metric": "Msamples/sec at 1920x1080, 1 spp ReSTIR DI; per-pixel L2 vs WebGPU ref",
+        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{args.scene} {pipeline} {W}x{Hb} per GPU, 1 spp/frame",
+                   "pipeline": "PT_01 gbuffer -> PT_1 init -> PT_4 final" if pipeline == "restir"
+                   else "TEST_MCPT brute force", "frame": f"{W}x{H}", "band_rows_per_gpu": Hb,
+                   "parallelism": f"row-bands x{world}"},
+        "kernel_ms": {p: round(kms[p], 4) for p in passes},
+        "nonfinite_px": nonfinite,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "alg_bytes_per_launch": alg_bytes[dom], "alg_bytes_per_sample": round(alg_bytes[dom] / px, 1),
+                     "work": counts[dom]},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cs, W, H, pipeline, threads):
+    """The C oracle (a port of the WGSL) on the host cores: one full frame, timed."""
+    from oracle import oracle as O
+    from pathtracerdemo_amd.scene.camera import Camera
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    cam = Camera(W, H)
+    cam.set_location(0, 0, 6)
+    u = cs.uniform(W, H, cam.view_projection_inverse(), cam.location, 1)
+    fr = O.Frame(u, cs.scene, cs.geometry, cs.accel)
+    t0 = time.perf_counter()
+    fr.run(O.PASS_RESTIR if pipeline == "restir" else O.PASS_MCPT, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(W * H / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"one full {W}x{H} frame ({pipeline}, FrameIndex 1), C oracle, {threads} pthreads",
+            "seconds": round(dt, 2)}
+
+
+if __name__ == "__main__":
+    main()

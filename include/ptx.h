@@ -1,0 +1,108 @@
+/*
+ * ptx.h -- C-ABI drop-in boundary of the MI355X path tracer (libptx.so).
+ *
+ * Replaces the WebGPU compute path behind the reference's Renderer class
+ * (apps/frontend/src/graphics-core/Renderer_TEST.ts; GC/ below = graphics-core/):
+ *
+ *   ptx_create           <- new Renderer(adapter, device, canvas)          GC/Renderer_TEST.ts:83-126
+ *   ptx_upload_scene     <- Initialize(world) -> CreateGPUResources         GC/Renderer_TEST.ts:141-163,445-460
+ *                           (takes exactly SerializeWorldData's three u32 arrays, :267-420)
+ *   ptx_set_frame        <- Update(): the 33-word uniform block             GC/Renderer_TEST.ts:165-206
+ *   ptx_render           <- Render(): G-buffer -> Init -> Final dispatches  GC/Renderer_TEST.ts:208-261
+ *                           (+ copyTextureToTexture Result->Scene, :223-231) or the
+ *                           legacy brute-force TEST_MCPT dispatch            GC/Renderer.ts:580-647
+ *   ptx_reset_accumulation <- texture re-creation on Initialize             GC/Renderer_TEST.ts:445-476
+ *   ptx_destroy          <- DestroyGPUResources                             GC/Renderer_TEST.ts:462-476
+ *   ptx_run_pass         <- ComputePass.Dispatch of one pass                GC/ComputePass.ts:66-78
+ *
+ * Conventions: every function returns 0 (PTX_OK) or a negative PTX_E* code and never
+ * throws; ptx_last_error() holds the handle's last message.  Input arrays are borrowed
+ * for the duration of the call only.  A handle is single-threaded and owns one HIP
+ * stream on one device.  Multi-GPU: one handle per rank, each rendering the row band
+ * [row_begin, row_end) of the full image with global pixel coordinates (RNG seeds and
+ * camera rays use global (x, y), so output is independent of the band split).
+ */
+#ifndef PTX_H
+#define PTX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTX_ABI_VERSION 1
+
+#define PTX_OK 0
+#define PTX_E_INVALID (-1)  /* bad argument / state                  */
+#define PTX_E_HIP (-2)      /* HIP runtime error                     */
+#define PTX_E_SCENE (-3)    /* scene arrays inconsistent/unsupported */
+#define PTX_E_NOMEM (-4)    /* allocation failure                    */
+
+#define PTX_UNIFORM_WORDS 33
+#define PTX_GBUFFER_WORDS 4     /* rgba32 texel: flags|inst|mat, prim, bary.x, bary.y */
+#define PTX_RESERVOIR_WORDS 32  /* 128-byte Reservoir, SH/PT_1_InitPass.wgsl:145-185 */
+
+/* pipelines */
+#define PTX_PIPELINE_RESTIR 0  /* PT_01 G-buffer -> PT_1 Init -> PT_4 Final (Renderer_TEST) */
+#define PTX_PIPELINE_MCPT 1    /* TEST_MCPT brute force (legacy Renderer)                 */
+
+/* passes for ptx_run_pass */
+#define PTX_PASS_GBUFFER 0
+#define PTX_PASS_INIT 1
+#define PTX_PASS_FINAL 2
+#define PTX_PASS_MCPT 3
+
+/* buffers for ptx_read_buffer / ptx_write_buffer / ptx_device_pointer */
+#define PTX_BUF_GBUFFER 0    /* band_h * W * 4 u32   */
+#define PTX_BUF_RESERVOIR 1  /* band_h * W * 32 u32  */
+#define PTX_BUF_ACCUM 2      /* band_h * W * 4 f32 (Scene texture: accumulated radiance) */
+#define PTX_BUF_COUNTERS 3   /* 8 u64 work counters (PTX_FLAG_COUNT builds) */
+
+#define PTX_FLAG_COUNT_WORK 1u  /* count rays / AABB / triangle tests on device (slower) */
+
+typedef struct ptx_config {
+    uint32_t width, height;       /* full image size (uniform words 0,1 must match) */
+    uint32_t row_begin, row_end;  /* band rendered by this handle; 0,0 = all rows    */
+    int32_t device;               /* HIP device ordinal; -1 = current device        */
+    uint32_t pipeline;            /* PTX_PIPELINE_*                                  */
+    uint32_t flags;               /* PTX_FLAG_*                                      */
+    uint32_t reserved[5];
+} ptx_config;
+
+typedef struct ptx_stats {
+    uint64_t frames;              /* ptx_render calls since the last stats reset    */
+    double kernel_ms_total[4];    /* summed device time per pass (HIP events)       */
+    uint64_t kernel_launches[4];  /* launches per pass                              */
+    uint32_t triangles, bvh_nodes, instances, max_bvh_depth;
+    uint64_t device_bytes;        /* device memory held by the handle               */
+} ptx_stats;
+
+typedef struct ptx_handle ptx_handle;
+
+int ptx_abi_version(void);
+int ptx_create(const ptx_config *cfg, ptx_handle **out);
+int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const uint32_t *geometry,
+                     size_t n_geometry, const uint32_t *accel, size_t n_accel);
+int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]);
+/* Run the configured pipeline for the current frame; if rgba_out != NULL copy the band's
+ * accumulated RGBA f32 image (band_h * W * 4) into it (blocking). Otherwise asynchronous. */
+int ptx_render(ptx_handle *h, float *rgba_out);
+int ptx_run_pass(ptx_handle *h, int pass);
+int ptx_reset_accumulation(ptx_handle *h);
+int ptx_synchronize(ptx_handle *h);
+int ptx_get_stats(ptx_handle *h, ptx_stats *out);
+int ptx_reset_stats(ptx_handle *h);
+int ptx_read_buffer(ptx_handle *h, int which, void *host_dst, size_t bytes);
+int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t bytes);
+int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the own stream. */
+int ptx_set_stream(ptx_handle *h, void *hip_stream);
+int ptx_destroy(ptx_handle *h);
+const char *ptx_last_error(const ptx_handle *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

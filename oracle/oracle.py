@@ -1,0 +1,127 @@
+"""ctypes binding of the C oracle (TEST INFRASTRUCTURE -- the parity checker).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module.  It runs the CPU restatement of the reference WGSL (see pt_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+PASS_GBUFFER, PASS_INIT, PASS_FINAL, PASS_MCPT, PASS_RESTIR = 0, 1, 2, 3, 4
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [("rays", ctypes.c_uint64), ("instance_xforms", ctypes.c_uint64),
+                ("aabb_tests", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64), ("hits", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class Inputs(ctypes.Structure):
+    _fields_ = [("uniform", ctypes.c_void_p), ("scene", ctypes.c_void_p),
+                ("geometry", ctypes.c_void_p), ("accel", ctypes.c_void_p)]
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "pt_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", HERE, "liboracle.so"], check=True, capture_output=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(build())
+        P = ctypes.c_void_p
+        _lib.pto_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Inputs), ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, P, P, P, ctypes.POINTER(Counters)]
+        _lib.pto_run.restype = ctypes.c_int
+        _lib.pto_pcg.argtypes = [ctypes.c_uint32]
+        _lib.pto_pcg.restype = ctypes.c_uint32
+        _lib.pto_random.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+        _lib.pto_random.restype = ctypes.c_float
+        _lib.pto_bsdf.argtypes = [P, P, P, P, P]
+        _lib.pto_pdf_bsdf.argtypes = [P, P, P, P]
+        _lib.pto_pdf_bsdf.restype = ctypes.c_float
+        _lib.pto_sample_bsdf.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_uint32), P,
+                                         ctypes.POINTER(ctypes.c_uint32)]
+        _lib.pto_ray_triangle.argtypes = [P, P, P, P, P, ctypes.c_float]
+        _lib.pto_ray_triangle.restype = ctypes.c_float
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Frame:
+    """Full-frame oracle buffers for one W x H uniform block."""
+
+    def __init__(self, uniform: np.ndarray, scene: np.ndarray, geometry: np.ndarray, accel: np.ndarray):
+        self.uniform = np.ascontiguousarray(uniform, dtype=np.uint32)
+        self.scene = np.ascontiguousarray(scene, dtype=np.uint32)
+        self.geometry = np.ascontiguousarray(geometry, dtype=np.uint32)
+        self.accel = np.ascontiguousarray(accel, dtype=np.uint32) if len(accel) else np.zeros(1, np.uint32)
+        self.W, self.H = int(self.uniform[0]), int(self.uniform[1])
+        self.gbuffer = np.zeros((self.H, self.W, 4), dtype=np.uint32)
+        self.reservoir = np.zeros((self.H, self.W, 32), dtype=np.uint32)
+        self.accum = np.zeros((self.H, self.W, 4), dtype=np.float32)
+        self.counters = {}
+
+    def set_frame_index(self, f: int):
+        self.uniform[23] = f
+
+    def run(self, pass_id: int, threads: int = 0, rect=None) -> dict:
+        threads = threads or os.cpu_count() or 1
+        x0, y0, x1, y1 = rect if rect is not None else (0, 0, self.W, self.H)
+        inp = Inputs(self.uniform.ctypes.data, self.scene.ctypes.data, self.geometry.ctypes.data,
+                     self.accel.ctypes.data)
+        cnt = Counters()
+        rc = lib().pto_run(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
+                           _ptr(self.reservoir), _ptr(self.accum), ctypes.byref(cnt))
+        if rc != 0:
+            raise RuntimeError(f"oracle pass {pass_id} failed ({rc})")
+        self.counters[pass_id] = cnt.as_dict()
+        return self.counters[pass_id]
+
+
+def pcg(seed: int) -> int:
+    return int(lib().pto_pcg(seed & 0xFFFFFFFF))
+
+
+def bsdf(n, mat, v, l) -> np.ndarray:
+    args = [np.asarray(a, dtype=np.float32) for a in (n, mat, v, l)]
+    out = np.zeros(3, dtype=np.float32)
+    lib().pto_bsdf(*[_ptr(a) for a in args], _ptr(out))
+    return out
+
+
+def pdf_bsdf(n, mat, v, l) -> float:
+    args = [np.asarray(a, dtype=np.float32) for a in (n, mat, v, l)]
+    return float(lib().pto_pdf_bsdf(*[_ptr(a) for a in args]))
+
+
+def sample_bsdf(n, mat, v, seed: int):
+    args = [np.asarray(a, dtype=np.float32) for a in (n, mat, v)]
+    s = ctypes.c_uint32(seed)
+    lobe = ctypes.c_uint32(0)
+    out = np.zeros(3, dtype=np.float32)
+    lib().pto_sample_bsdf(*[_ptr(a) for a in args], ctypes.byref(s), _ptr(out), ctypes.byref(lobe))
+    return out, int(lobe.value), int(s.value)
+
+
+def ray_triangle(o, d, p0, p1, p2, det_eps: float) -> float:
+    args = [np.asarray(a, dtype=np.float32) for a in (o, d, p0, p1, p2)]
+    return float(lib().pto_ray_triangle(*[_ptr(a) for a in args], det_eps))

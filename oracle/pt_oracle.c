@@ -1,0 +1,1119 @@
+/*
+ * pt_oracle.c -- scalar-f32 CPU restatement of the reference WGSL (TEST INFRASTRUCTURE).
+ * See pt_oracle.h for scope.  Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
+ * Every function cites the WGSL it restates (SH/ = apps/frontend/src/graphics-core/shaders/).
+ */
+#include "pt_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ constants
+ * SH/PT_1_InitPass.wgsl:193-221 */
+#define STRIDE_INSTANCE 33u
+#define STRIDE_LIGHT 18u
+#define STRIDE_DESCRIPTOR 6u
+#define STRIDE_MATERIAL 15u
+#define STRIDE_VERTEX 8u
+#define STRIDE_BLAS 8u
+#define RECONNECTION_DISTANCE 0.1f
+#define RECONNECTION_ROUGHNESS 0.5f
+#define INF_F 1e11f
+#define EPS_F 1e-4f
+#define PI_F 3.141592f
+#define ENV_C 0.5f
+#define LIGHT_DIRECTION 0u
+#define LIGHT_POINT 1u
+#define LIGHT_RECT 2u
+#define LIGHT_ENV 3u
+#define LOBE_LAMBERT 0u
+#define LOBE_GGX 1u
+#define LOBE_LIGHT 3u
+#define STACK_MAX 96
+
+/* uniform word indices (SH/PT_1_InitPass.wgsl:5-27) */
+enum { U_W = 0, U_H = 1, U_VPINV = 4, U_FRAME = 23, U_OFF_DESC = 24, U_OFF_MAT = 25, U_OFF_LIGHT = 26,
+       U_OFF_CDF = 27, U_OFF_INDEX = 28, U_OFF_SUBROOT = 29, U_OFF_BLAS = 30, U_INST_COUNT = 31,
+       U_LIGHT_COUNT = 32 };
+
+/* pass-specific epsilons (SURVEY.md §7 "Per-pass epsilon quirks") */
+typedef struct pass_eps {
+    float det_eps;   /* GetRayTriangleHitDistance |det| threshold */
+    float bary_eps;  /* GetBaryCentricWeights |denom| threshold    */
+    int final_pass;  /* PT_4 variants of PDF_LIGHT / L_emit (no EPS guard) */
+} pass_eps;
+static const pass_eps EPS_GBUFFER = {1e-8f, 1e-6f, 0};  /* SH/PT_01_GBufferPass.wgsl:409,468 */
+static const pass_eps EPS_INIT = {1e-4f, 1e-8f, 0};     /* SH/PT_1_InitPass.wgsl:528,567 */
+static const pass_eps EPS_FINAL = {1e-4f, 1e-8f, 1};    /* SH/PT_4_FinalShadingPass.wgsl:1249,1265 */
+static const pass_eps EPS_MCPT = {1e-4f, 1e-8f, 0};     /* SH/TEST_MCPT.wgsl */
+
+/* ------------------------------------------------------------------ f32 vector algebra */
+typedef struct { float x, y, z; } v3;
+static inline v3 V3(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 vadd(v3 a, v3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vsub(v3 a, v3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vmul(v3 a, v3 b) { return V3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 vscale(v3 a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
+static inline v3 vdivs(v3 a, float s) { return V3(a.x / s, a.y / s, a.z / s); }
+static inline v3 vneg(v3 a) { return V3(-a.x, -a.y, -a.z); }
+static inline float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 vcross(v3 a, v3 b) {
+    return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline float vlength(v3 a) { return sqrtf(vdot(a, a)); }
+static inline v3 vnormalize(v3 a) { return vdivs(a, vlength(a)); }
+static inline float fmin_(float a, float b) { return fminf(a, b); }
+static inline float fmax_(float a, float b) { return fmaxf(a, b); }
+static inline float saturate_(float a) { return fminf(fmaxf(a, 0.0f), 1.0f); }
+static inline float mixf(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+static inline v3 vmix(v3 a, v3 b, float t) { return V3(mixf(a.x, b.x, t), mixf(a.y, b.y, t), mixf(a.z, b.z, t)); }
+static inline float luminance(v3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
+static inline float f32_of(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline uint32_t u32_of(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+/* mat4 (column-major, m[4*col+row]) * vec4, SH/PT_1_InitPass.wgsl:480-484 */
+static inline v3 xform_point(const float *m, v3 p) {
+    float x = ((m[0] * p.x + m[4] * p.y) + m[8] * p.z) + m[12] * 1.0f;
+    float y = ((m[1] * p.x + m[5] * p.y) + m[9] * p.z) + m[13] * 1.0f;
+    float z = ((m[2] * p.x + m[6] * p.y) + m[10] * p.z) + m[14] * 1.0f;
+    float w = ((m[3] * p.x + m[7] * p.y) + m[11] * p.z) + m[15] * 1.0f;
+    return V3(x / w, y / w, z / w);
+}
+/* transpose(m) * vec4(p,1), then /w (normal transform, SH/PT_1_InitPass.wgsl:395) */
+static inline v3 xform_point_transposed(const float *m, v3 p) {
+    float x = ((m[0] * p.x + m[1] * p.y) + m[2] * p.z) + m[3] * 1.0f;
+    float y = ((m[4] * p.x + m[5] * p.y) + m[6] * p.z) + m[7] * 1.0f;
+    float z = ((m[8] * p.x + m[9] * p.y) + m[10] * p.z) + m[11] * 1.0f;
+    float w = ((m[12] * p.x + m[13] * p.y) + m[14] * p.z) + m[15] * 1.0f;
+    return V3(x / w, y / w, z / w);
+}
+
+/* ------------------------------------------------------------------ RNG (PT_1:810-826) */
+uint32_t pto_pcg(uint32_t seed) {
+    uint32_t state = seed * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+float pto_random(uint32_t *seed) {
+    uint32_t h = pto_pcg(*seed);
+    *seed += 1u;
+    return (float)h / 4294967295.0f; /* literal rounds to 2^32 in f32 */
+}
+
+/* ------------------------------------------------------------------ scene access */
+typedef struct ctx {
+    const uint32_t *U, *S, *G, *A;
+    pass_eps eps;
+    pto_counters *cnt;
+} ctx;
+
+typedef struct material {
+    v3 albedo;
+    float alpha;
+    float metalness, roughness, transmission, ior;
+} material;
+
+typedef struct surface {
+    v3 pos, nrm;
+    material mat;
+} surface;
+
+typedef struct compact {
+    uint32_t valid, inst, mat, prim;
+    float bu, bv;
+} compact;
+
+typedef struct hit {
+    int valid;
+    float t;
+    compact s;
+} hit;
+
+typedef struct ray { v3 o, d; } ray;
+
+typedef struct desc { uint32_t off_vertex, off_index, off_material, off_subroot, off_blas, count_sub; } desc;
+
+static inline const float *inst_model(const ctx *c, uint32_t i) { return (const float *)(c->S + STRIDE_INSTANCE * i); }
+static inline const float *inst_inv(const ctx *c, uint32_t i) { return (const float *)(c->S + STRIDE_INSTANCE * i + 16u); }
+static inline uint32_t inst_mesh(const ctx *c, uint32_t i) { return c->S[STRIDE_INSTANCE * i + 32u]; }
+
+static inline desc get_desc(const ctx *c, uint32_t mesh) {
+    const uint32_t *p = c->S + c->U[U_OFF_DESC] + STRIDE_DESCRIPTOR * mesh;
+    desc d = {p[0], p[1], p[2], p[3], p[4], p[5]};
+    return d;
+}
+
+/* GetMaterial, SH/PT_1_InitPass.wgsl:285-314 (transmissive -> yellow, roughness >= 0.01) */
+static material get_material(const ctx *c, const desc *d, uint32_t mid) {
+    const uint32_t *p = c->S + c->U[U_OFF_MAT] + d->off_material + STRIDE_MATERIAL * mid;
+    material m;
+    m.albedo = V3(f32_of(p[0]), f32_of(p[1]), f32_of(p[2]));
+    m.alpha = f32_of(p[3]);
+    m.metalness = f32_of(p[8]);
+    m.roughness = f32_of(p[9]);
+    m.transmission = f32_of(p[10]);
+    m.ior = f32_of(p[11]);
+    if (m.transmission > 0.0f) m.albedo = V3(1.0f, 1.0f, 0.0f);
+    m.roughness = fmax_(m.roughness, 0.01f);
+    return m;
+}
+
+static inline v3 vertex_pos(const ctx *c, const desc *d, uint32_t vid) {
+    const uint32_t *p = c->G + d->off_vertex + STRIDE_VERTEX * vid;
+    return V3(f32_of(p[0]), f32_of(p[1]), f32_of(p[2]));
+}
+static inline v3 vertex_nrm(const ctx *c, const desc *d, uint32_t vid) {
+    const uint32_t *p = c->G + d->off_vertex + STRIDE_VERTEX * vid;
+    return V3(f32_of(p[3]), f32_of(p[4]), f32_of(p[5]));
+}
+static inline void tri_ids(const ctx *c, const desc *d, uint32_t prim, uint32_t id[3]) {
+    const uint32_t *p = c->G + c->U[U_OFF_INDEX] + d->off_index + 3u * prim;
+    id[0] = p[0]; id[1] = p[1]; id[2] = p[2];
+}
+
+/* GetBlasNode, SH/PT_01_GBufferPass.wgsl:310-322 */
+static inline const uint32_t *blas_node(const ctx *c, const desc *d, uint32_t sub, uint32_t node) {
+    uint32_t root = c->G[c->U[U_OFF_SUBROOT] + d->off_subroot + sub];
+    return c->A + c->U[U_OFF_BLAS] + d->off_blas + root + STRIDE_BLAS * node;
+}
+
+/* GetSurface, SH/PT_1_InitPass.wgsl:438-467 (and GetTriangleWorldSpace :390-407) */
+static surface get_surface(const ctx *c, compact x) {
+    surface s;
+    uint32_t mesh = inst_mesh(c, x.inst);
+    desc d = get_desc(c, mesh);
+    const float *M = inst_model(c, x.inst);
+    const float *Mi = inst_inv(c, x.inst);
+    uint32_t id[3];
+    s.mat = get_material(c, &d, x.mat);
+    tri_ids(c, &d, x.prim, id);
+    v3 p0 = xform_point(M, vertex_pos(c, &d, id[0]));
+    v3 n0 = xform_point_transposed(Mi, vertex_nrm(c, &d, id[0]));
+    v3 p1 = xform_point(M, vertex_pos(c, &d, id[1]));
+    v3 n1 = xform_point_transposed(Mi, vertex_nrm(c, &d, id[1]));
+    v3 p2 = xform_point(M, vertex_pos(c, &d, id[2]));
+    v3 n2 = xform_point_transposed(Mi, vertex_nrm(c, &d, id[2]));
+    float U = x.bu, V = x.bv, W = 1.0f - U - V;
+    s.nrm = vnormalize(vadd(vadd(vscale(n0, U), vscale(n1, V)), vscale(n2, W)));
+    s.pos = vadd(vadd(vscale(p0, U), vscale(p1, V)), vscale(p2, W));
+    return s;
+}
+
+/* ------------------------------------------------------------------ geometry tests */
+/* TransformRayWithMat4x4, SH/PT_1_InitPass.wgsl:486-496 */
+static ray transform_ray(const float *m, ray r, int normalize_dir) {
+    v3 start = xform_point(m, r.o);
+    v3 end = xform_point(m, vadd(r.o, r.d));
+    v3 dir = vsub(end, start);
+    ray out = {start, normalize_dir ? vnormalize(dir) : dir};
+    return out;
+}
+
+/* GetRayAABBIntersectionRange, SH/PT_1_InitPass.wgsl:498-514; returns 1 and range on hit */
+static inline void aabb_range(ray r, const uint32_t *node, float *tmin_out, float *tmax_out) {
+    v3 inv = V3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    v3 bmin = V3(f32_of(node[0]), f32_of(node[1]), f32_of(node[2]));
+    v3 bmax = V3(f32_of(node[3]), f32_of(node[4]), f32_of(node[5]));
+    v3 t1 = vmul(vsub(bmin, r.o), inv);
+    v3 t2 = vmul(vsub(bmax, r.o), inv);
+    v3 tn = V3(fmin_(t1.x, t2.x), fmin_(t1.y, t2.y), fmin_(t1.z, t2.z));
+    v3 tf = V3(fmax_(t1.x, t2.x), fmax_(t1.y, t2.y), fmax_(t1.z, t2.z));
+    float t_min = fmax_(tn.x, fmax_(tn.y, tn.z));
+    float t_max = fmin_(tf.x, fmin_(tf.y, tf.z));
+    if (t_min > t_max) { *tmin_out = 1.0f; *tmax_out = 0.0f; return; }
+    *tmin_out = t_min;
+    *tmax_out = t_max;
+}
+/* DoRangesOverlap, SH/PT_1_InitPass.wgsl:475-478 */
+static inline int ranges_overlap(float r1x, float r1y, float r2x, float r2y) { return (r1x <= r2y) && (r2x <= r1y); }
+
+/* GetRayTriangleHitDistance, SH/PT_1_InitPass.wgsl:516-547 (det EPS per pass) */
+static float ray_triangle(ray r, v3 P0, v3 P1, v3 P2, float det_eps) {
+    v3 e1 = vsub(P1, P0);
+    v3 e2 = vsub(P2, P0);
+    v3 pvec = vcross(r.d, e2);
+    float det = vdot(e1, pvec);
+    if (fabsf(det) < det_eps) return 1e11f;
+    float inv_det = 1.0f / det;
+    v3 tvec = vsub(r.o, P0);
+    float u = vdot(tvec, pvec) * inv_det;
+    if (u < 0.0f || u > 1.0f) return 1e11f;
+    v3 qvec = vcross(tvec, e1);
+    float v = vdot(r.d, qvec) * inv_det;
+    if (v < 0.0f || (u + v) > 1.0f) return 1e11f;
+    float t = vdot(e2, qvec) * inv_det;
+    if (t <= 1e-4f) return 1e11f;
+    return t;
+}
+
+/* GetBaryCentricWeights, SH/PT_1_InitPass.wgsl:549-575 -> (w,u,v) */
+static void barycentric(v3 P, v3 A, v3 B, v3 C, float eps, float out[3]) {
+    v3 v0 = vsub(B, A), v1 = vsub(C, A), v2 = vsub(P, A);
+    float d00 = vdot(v0, v0), d01 = vdot(v0, v1), d11 = vdot(v1, v1);
+    float d20 = vdot(v2, v0), d21 = vdot(v2, v1);
+    float denom = d00 * d11 - d01 * d01;
+    if (fabsf(denom) < eps) { out[0] = 1.0f; out[1] = 0.0f; out[2] = 0.0f; return; }
+    float inv = 1.0f / denom;
+    float u = (d11 * d20 - d01 * d21) * inv;
+    float v = (d00 * d21 - d01 * d20) * inv;
+    out[0] = 1.0f - u - v;
+    out[1] = u;
+    out[2] = v;
+}
+
+/* TraceRay, SH/PT_1_InitPass.wgsl:605-715 (PT_01:509-621 identical up to epsilons) */
+static hit trace_ray(const ctx *c, ray in) {
+    hit best;
+    memset(&best, 0, sizeof best);
+    float vx = 1e-4f, vy = 1e10f; /* RayValidRange */
+    uint32_t stack[STACK_MAX];
+    const uint32_t ninst = c->U[U_INST_COUNT];
+    if (c->cnt) c->cnt->rays++;
+    for (uint32_t inst = 0; inst < ninst; ++inst) {
+        const uint32_t mesh = inst_mesh(c, inst);
+        desc d = get_desc(c, mesh);
+        ray local = transform_ray(inst_inv(c, inst), in, 0);
+        if (c->cnt) c->cnt->instance_xforms++;
+        for (uint32_t sub = 0; sub < d.count_sub; ++sub) {
+            float rx, ry;
+            aabb_range(local, blas_node(c, &d, sub, 0), &rx, &ry);
+            if (c->cnt) c->cnt->aabb_tests++;
+            if (!ranges_overlap(vx, vy, rx, ry)) continue;
+            int sp = -1;
+            stack[++sp] = 0;
+            while (sp > -1) {
+                uint32_t id = stack[sp--];
+                const uint32_t *node = blas_node(c, &d, sub, id);
+                int leaf = (node[7] & 0xffff0000u) != 0u;
+                if (!leaf) {
+                    uint32_t lid = id + 1u, rid = node[6] / 8u;
+                    float lx, ly, rrx, rry;
+                    aabb_range(local, blas_node(c, &d, sub, lid), &lx, &ly);
+                    aabb_range(local, blas_node(c, &d, sub, rid), &rrx, &rry);
+                    if (c->cnt) c->cnt->aabb_tests += 2;
+                    int lh = ranges_overlap(vx, vy, lx, ly);
+                    int rh = ranges_overlap(vx, vy, rrx, rry);
+                    if (lh && rh) {
+                        if (lx < rrx) { stack[++sp] = rid; stack[++sp] = lid; }
+                        else { stack[++sp] = lid; stack[++sp] = rid; }
+                    } else if (lh) {
+                        stack[++sp] = lid;
+                    } else if (rh) {
+                        stack[++sp] = rid;
+                    }
+                    if (sp >= STACK_MAX - 2) abort(); /* reference stack is 96/64 entries */
+                    continue;
+                }
+                uint32_t first = node[6], last = first + (node[7] & 0xffffu);
+                for (uint32_t prim = first; prim < last; ++prim) {
+                    uint32_t ids[3];
+                    tri_ids(c, &d, prim, ids);
+                    float t = ray_triangle(local, vertex_pos(c, &d, ids[0]), vertex_pos(c, &d, ids[1]),
+                                           vertex_pos(c, &d, ids[2]), c->eps.det_eps);
+                    if (c->cnt) c->cnt->tri_tests++;
+                    if (vy < t) continue;
+                    vy = t;
+                    best.valid = 1;
+                    best.s.valid = 1;
+                    best.s.inst = inst;
+                    best.s.mat = sub;
+                    best.s.prim = prim;
+                }
+            }
+        }
+    }
+    if (best.valid) {
+        best.t = vy;
+        const uint32_t mesh = inst_mesh(c, best.s.inst);
+        desc d = get_desc(c, mesh);
+        const float *M = inst_model(c, best.s.inst);
+        uint32_t ids[3];
+        tri_ids(c, &d, best.s.prim, ids);
+        v3 A = xform_point(M, vertex_pos(c, &d, ids[0]));
+        v3 B = xform_point(M, vertex_pos(c, &d, ids[1]));
+        v3 C = xform_point(M, vertex_pos(c, &d, ids[2]));
+        v3 P = vadd(in.o, vscale(in.d, best.t));
+        float w[3];
+        barycentric(P, A, B, C, c->eps.bary_eps, w);
+        best.s.bu = w[0];
+        best.s.bv = w[1];
+        if (c->cnt) c->cnt->hits++;
+    }
+    return best;
+}
+
+/* ------------------------------------------------------------------ lights */
+typedef struct light {
+    v3 pos, dir, color, U, V;
+    uint32_t type;
+    float intensity, area;
+} light;
+
+typedef struct light_sample {
+    v3 dir;
+    uint32_t type;
+    v3 pos;
+    int32_t id;
+    v3 Le;
+    float pdf;
+} light_sample;
+
+static light get_light(const ctx *c, uint32_t id) {
+    const uint32_t *p = c->S + c->U[U_OFF_LIGHT] + STRIDE_LIGHT * id;
+    light l;
+    l.pos = V3(f32_of(p[0]), f32_of(p[1]), f32_of(p[2]));
+    l.dir = V3(f32_of(p[3]), f32_of(p[4]), f32_of(p[5]));
+    l.color = V3(f32_of(p[6]), f32_of(p[7]), f32_of(p[8]));
+    l.U = V3(f32_of(p[9]), f32_of(p[10]), f32_of(p[11]));
+    l.V = V3(f32_of(p[12]), f32_of(p[13]), f32_of(p[14]));
+    l.type = p[15];
+    l.intensity = f32_of(p[16]);
+    l.area = f32_of(p[17]);
+    return l;
+}
+static inline float light_cdf(const ctx *c, uint32_t i) { return f32_of(c->S[c->U[U_OFF_CDF] + i]); }
+
+/* ------------------------------------------------------------------ BSDF (PT_1:834-929) */
+static float ggx_d(float NdotH, float R) {
+    float a = R * R, a2 = a * a;
+    float X = NdotH * NdotH * (a2 - 1.0f) + 1.0f;
+    float denom = PI_F * X * X;
+    return a2 / fmax_(denom, EPS_F);
+}
+static float geom_shadow(float NdotV, float NdotL, float R) {
+    float r = R + 1.0f;
+    float K = r * r / 8.0f;
+    return 1.0f / ((NdotV * (1.0f - K) + K) * (NdotL * (1.0f - K) + K));
+}
+static v3 fresnel(float d, v3 F0) {
+    float p = powf(1.0f - saturate_(d), 5.0f);
+    return V3(F0.x + (1.0f - F0.x) * p, F0.y + (1.0f - F0.y) * p, F0.z + (1.0f - F0.z) * p);
+}
+static v3 brdf(const surface *X, v3 V, v3 L) {
+    v3 N = X->nrm;
+    v3 H = vnormalize(vadd(L, V));
+    float NdotV = fmax_(vdot(N, V), 0.0f), NdotL = fmax_(vdot(N, L), 0.0f);
+    float NdotH = fmax_(vdot(N, H), 0.0f), VdotH = fmax_(vdot(V, H), 0.0f);
+    v3 base = X->mat.albedo;
+    float metal = X->mat.metalness, R = X->mat.roughness;
+    v3 F0 = vmix(V3(0.04f, 0.04f, 0.04f), base, metal);
+    float D = ggx_d(NdotH, R);
+    float G0 = geom_shadow(NdotV, NdotL, R);
+    v3 F = fresnel(VdotH, F0);
+    v3 kD = vscale(V3(1.0f - F.x, 1.0f - F.y, 1.0f - F.z), 1.0f - metal);
+    v3 diffuse = vmul(vdivs(kD, PI_F), base);
+    v3 spec = vscale(vscale(vscale(F, D), G0), 0.25f);
+    return vadd(diffuse, spec);
+}
+static v3 btdf(const surface *X, v3 V, v3 L) {
+    v3 albedo = X->mat.albedo;
+    float R = X->mat.roughness;
+    int same = vdot(V, X->nrm) > 0.0f;
+    float n_in = same ? X->mat.ior : 1.0f;
+    float n_out = same ? 1.0f : X->mat.ior;
+    v3 hv = vadd(vscale(L, n_in), vscale(V, n_out));
+    float H_norm = vlength(hv);
+    v3 N = same ? X->nrm : vneg(X->nrm);
+    v3 H = vnormalize(hv);
+    float NdotL = fabsf(vdot(N, L)), NdotV = fabsf(vdot(N, V)), NdotH = fabsf(vdot(N, H));
+    float LdotH = fabsf(vdot(L, H)), VdotH = fabsf(vdot(V, H));
+    float G0 = geom_shadow(NdotL, NdotV, R);
+    float D = ggx_d(NdotH, R);
+    float nr = (n_out - n_in) / (n_out + n_in);
+    v3 F = fresnel(LdotH, V3(nr * nr, nr * nr, nr * nr));
+    float s = n_out * n_out;
+    v3 num = vscale(V3(1.0f - F.x, 1.0f - F.y, 1.0f - F.z), s);
+    num = vscale(num, LdotH);
+    num = vscale(num, VdotH);
+    num = vscale(num, G0);
+    num = vscale(num, D);
+    num = vmul(num, albedo);
+    return vdivs(num, fmax_(H_norm * H_norm, EPS_F));
+}
+static v3 bsdf(const surface *X, v3 V, v3 L) {
+    float T = X->mat.transmission;
+    v3 N = X->nrm;
+    if (vdot(L, N) * vdot(V, N) > 0.0f) return vscale(brdf(X, V, L), 1.0f - T);
+    return vscale(btdf(X, V, L), T);
+}
+
+/* ------------------------------------------------------------------ sampling (PT_1:577-589,937-1106) */
+typedef struct mat3 { v3 T, B, N; } mat3;
+static mat3 tbn(v3 N) {
+    int same = fabsf(vdot(N, V3(0.0f, 1.0f, 0.0f))) > 0.9999f;
+    v3 cv = same ? V3(1.0f, 0.0f, 0.0f) : V3(0.0f, 1.0f, 0.0f);
+    mat3 m;
+    m.T = vnormalize(vcross(cv, N));
+    m.B = vcross(N, m.T);
+    m.N = N;
+    return m;
+}
+static inline v3 mat3_mul(mat3 m, v3 v) { return vadd(vadd(vscale(m.T, v.x), vscale(m.B, v.y)), vscale(m.N, v.z)); }
+static inline v3 reflect_(v3 I, v3 N) { return vsub(I, vscale(N, 2.0f * vdot(N, I))); }
+static inline v3 refract_(v3 I, v3 N, float eta) {
+    float d = vdot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return V3(0.0f, 0.0f, 0.0f);
+    return vsub(vscale(I, eta), vscale(N, eta * d + sqrtf(k)));
+}
+static v3 sample_cosine(uint32_t *seed) {
+    float r1 = pto_random(seed), r2 = pto_random(seed);
+    float R = sqrtf(r1);
+    float phi = 2.0f * PI_F * r2;
+    return V3(R * cosf(phi), R * sinf(phi), sqrtf(1.0f - r1));
+}
+static v3 sample_ggx(uint32_t *seed, float R) {
+    float r1 = pto_random(seed), r2 = pto_random(seed);
+    float a = R * R;
+    float phi = 2.0f * PI_F * r1;
+    float ct = sqrtf((1.0f - r2) / (1.0f + (a * a - 1.0f) * r2));
+    float st = sqrtf(1.0f - ct * ct);
+    return vnormalize(V3(st * cosf(phi), st * sinf(phi), ct));
+}
+static v3 sample_brdf(uint32_t *seed, const surface *X, v3 V, uint32_t *lobe) {
+    float metal = X->mat.metalness;
+    v3 F0 = vmix(V3(0.04f, 0.04f, 0.04f), X->mat.albedo, metal);
+    float p_spec = mixf(luminance(F0), 1.0f, metal);
+    mat3 m = tbn(X->nrm);
+    int spec = pto_random(seed) < p_spec;
+    v3 L;
+    if (spec) {
+        v3 H = mat3_mul(m, sample_ggx(seed, X->mat.roughness));
+        L = reflect_(vneg(V), H);
+    } else {
+        L = mat3_mul(m, sample_cosine(seed));
+    }
+    *lobe = spec ? LOBE_GGX : LOBE_LAMBERT;
+    return L;
+}
+static v3 sample_btdf(uint32_t *seed, const surface *X, v3 V, uint32_t *lobe) {
+    int same = vdot(V, X->nrm) > 0.0f;
+    float n_in = same ? 1.0f : X->mat.ior;
+    float n_out = same ? X->mat.ior : 1.0f;
+    v3 N = same ? X->nrm : vneg(X->nrm);
+    float ratio = n_in / n_out;
+    float r = (1.0f - ratio) / (1.0f + ratio);
+    float R2 = ratio * ratio;
+    float cos_t = fabsf(vdot(V, N));
+    float p_refl = fresnel(cos_t, V3(r * r, r * r, r * r)).x;
+    if (cos_t * cos_t < (R2 - 1.0f) / R2) p_refl = 1.0f;
+    int refl = pto_random(seed) < p_refl;
+    mat3 m = tbn(N);
+    v3 H = mat3_mul(m, sample_ggx(seed, X->mat.roughness));
+    v3 Lr = refract_(vneg(V), H, ratio);
+    v3 Ll = reflect_(vneg(V), H);
+    *lobe = LOBE_GGX;
+    return vnormalize(refl ? Ll : Lr);
+}
+static v3 sample_bsdf(uint32_t *seed, const surface *X, v3 V, uint32_t *lobe) {
+    int transparent = pto_random(seed) < X->mat.transmission;
+    if (transparent) return sample_btdf(seed, X, V, lobe);
+    return sample_brdf(seed, X, V, lobe);
+}
+
+/* ------------------------------------------------------------------ pdfs (PT_1:1114-1245) */
+static float pdf_brdf(const surface *X, v3 V, v3 L) {
+    float metal = X->mat.metalness, R = X->mat.roughness;
+    v3 F0 = vmix(V3(0.04f, 0.04f, 0.04f), X->mat.albedo, metal);
+    float p_spec = mixf(luminance(F0), 1.0f, metal);
+    v3 N = X->nrm;
+    v3 H = vnormalize(vadd(L, V));
+    float LdotN = fmax_(vdot(L, N), 0.0f);
+    float NdotH = fmax_(vdot(N, H), 0.0f);
+    float VdotH = fmax_(vdot(V, H), 0.0f);
+    float pdf_s = ggx_d(NdotH, R) / fmax_(4.0f * VdotH, EPS_F);
+    float pdf_d = LdotN / PI_F;
+    return mixf(pdf_d, pdf_s, p_spec);
+}
+static float pdf_btdf(const surface *X, v3 V, v3 L) {
+    float R = X->mat.roughness;
+    int same = vdot(V, X->nrm) > 0.0f;
+    float n_in = same ? 1.0f : X->mat.ior;
+    float n_out = same ? X->mat.ior : 1.0f;
+    float ratio = n_in / n_out;
+    v3 N = same ? X->nrm : vneg(X->nrm);
+    float r0 = (1.0f - ratio) / (1.0f + ratio);
+    float R0 = r0 * r0;
+    float cos_t = fabsf(vdot(V, N));
+    float p_refl = fresnel(cos_t, V3(R0, R0, R0)).x;
+    float sin2 = 1.0f - cos_t * cos_t;
+    float R2 = ratio * ratio;
+    if (sin2 * R2 > 1.0f) p_refl = 1.0f;
+    float p_trans = 1.0f - p_refl;
+    float pdf_r = 0.0f;
+    if (p_refl > 0.0f) {
+        v3 Hr = vnormalize(vadd(V, L));
+        float NdotHr = fmax_(0.0f, vdot(N, Hr));
+        float VdotHr = fmax_(0.0f, vdot(V, Hr));
+        if (VdotHr > 0.0f) pdf_r = ggx_d(NdotHr, R) / (4.0f * VdotHr);
+    }
+    float pdf_t = 0.0f;
+    if (p_trans > 0.0f) {
+        v3 Ht = vnormalize(vadd(vscale(V, n_out), vscale(L, n_in)));
+        float NdotHt = fmax_(0.0f, vdot(N, Ht));
+        float VdotHt = fmax_(0.0f, vdot(V, Ht));
+        float LdotHt = fmax_(0.0f, vdot(L, Ht));
+        float denom = n_in * LdotHt + n_out * VdotHt;
+        if (denom > 0.0f) {
+            float J = (n_out * n_out * VdotHt) / (denom * denom);
+            pdf_t = ggx_d(NdotHt, R) * fabsf(J);
+        }
+    }
+    return p_refl * pdf_r + p_trans * pdf_t;
+}
+static float pdf_bsdf(const surface *X, v3 V, v3 L) {
+    v3 N = X->nrm;
+    if (vdot(L, N) * vdot(V, N) > 0.0f) return pdf_brdf(X, V, L);
+    return pdf_btdf(X, V, L);
+}
+
+/* DirectionToLight, SH/PT_1_InitPass.wgsl:746-772 */
+static v3 direction_to_light(const surface *X, const light_sample *XL) {
+    switch (XL->type) {
+    case LIGHT_DIRECTION: return vneg(XL->dir);
+    case LIGHT_POINT:
+    case LIGHT_RECT: return vnormalize(vsub(XL->pos, X->pos));
+    case LIGHT_ENV: return vneg(XL->dir);
+    default: return V3(0.0f, 0.0f, 0.0f);
+    }
+}
+
+/* PDF_LIGHT, SH/PT_1_InitPass.wgsl:1220-1245 (PT_4:1249 drops the EPS guard) */
+static float pdf_light(const ctx *c, const surface *X, v3 V, const light_sample *XL) {
+    if (XL->type == LIGHT_ENV) {
+        v3 L = direction_to_light(X, XL);
+        return pdf_bsdf(X, V, L);
+    }
+    light ls = get_light(c, (uint32_t)XL->id);
+    float before = (XL->id == 0) ? 0.0f : light_cdf(c, (uint32_t)XL->id - 1u);
+    float choose = light_cdf(c, (uint32_t)XL->id) - before;
+    float pdf_point = 1.0f;
+    if (XL->type == LIGHT_RECT) {
+        v3 r = vsub(XL->pos, X->pos);
+        v3 L = vnormalize(r);
+        float denom = ls.area * fabsf(vdot(ls.dir, L));
+        pdf_point = vdot(r, r) / (c->eps.final_pass ? denom : fmax_(denom, EPS_F));
+    }
+    return choose * pdf_point;
+}
+
+/* SampleNEE, SH/PT_1_InitPass.wgsl:970-1025 */
+static light_sample sample_nee(const ctx *c, uint32_t *seed, const surface *X, v3 V) {
+    light_sample s;
+    memset(&s, 0, sizeof s);
+    float P = pto_random(seed);
+    uint32_t L = 0, R = c->U[U_LIGHT_COUNT] - 1u, M = (L + R) >> 1;
+    while (L < R) {
+        if (P < light_cdf(c, M)) R = M;
+        else L = M + 1u;
+        M = (L + R) >> 1;
+    }
+    s.id = (int32_t)M;
+    light ls = get_light(c, M);
+    s.type = ls.type;
+    s.Le = vscale(ls.color, ls.intensity);
+    switch (ls.type) {
+    case LIGHT_DIRECTION:
+        s.pos = vsub(X->pos, vscale(ls.dir, INF_F));
+        s.dir = ls.dir;
+        break;
+    case LIGHT_POINT:
+        s.pos = ls.pos;
+        s.dir = vnormalize(vsub(X->pos, ls.pos));
+        break;
+    case LIGHT_RECT: {
+        float ru = pto_random(seed) * 2.0f - 1.0f;
+        float rv = pto_random(seed) * 2.0f - 1.0f;
+        v3 off = vadd(vscale(ls.U, ru), vscale(ls.V, rv));
+        s.pos = vadd(ls.pos, off);
+        s.dir = vnormalize(vsub(X->pos, s.pos));
+        break;
+    }
+    default: break;
+    }
+    s.pdf = pdf_light(c, X, V, &s);
+    return s;
+}
+
+/* L_emit, SH/PT_1_InitPass.wgsl:1253-1260 (PT_4:1265: no EPS guard) */
+static v3 l_emit(const ctx *c, const light_sample *XL, const surface *X) {
+    v3 r = vsub(XL->pos, X->pos);
+    float rr = vdot(r, r);
+    float att = (XL->type == LIGHT_POINT) ? 1.0f / (c->eps.final_pass ? rr : fmax_(rr, EPS_F)) : 1.0f;
+    return vscale(XL->Le, att);
+}
+
+/* GetMaterialFromHit + Visibility, SH/PT_1_InitPass.wgsl:316-322,774-802 */
+static float visibility(const ctx *c, v3 start, v3 end) {
+    float T = 1.0f;
+    float dist = vlength(vsub(end, start));
+    v3 dir = vdivs(vsub(end, start), dist);
+    ray r = {start, dir};
+    float remain = dist;
+    for (int it = 0; it < 5; ++it) {
+        hit h = trace_ray(c, r);
+        if (!h.valid || h.t > remain) return T;
+        desc d = get_desc(c, inst_mesh(c, h.s.inst));
+        material m = get_material(c, &d, h.s.mat);
+        if (m.transmission == 0.0f) return 0.0f;
+        T *= m.transmission;
+        remain -= h.t;
+        surface s = get_surface(c, h.s);
+        r.o = s.pos;
+    }
+    return 0.0f;
+}
+
+/* CreateEnvLight, SH/PT_1_InitPass.wgsl:717-730 */
+static light_sample create_env_light(const surface *X, v3 V, v3 L) {
+    light_sample s;
+    memset(&s, 0, sizeof s);
+    s.pos = vadd(X->pos, vscale(L, INF_F));
+    s.type = LIGHT_ENV;
+    s.dir = vneg(L);
+    s.id = -1;
+    s.Le = V3(ENV_C, ENV_C, ENV_C);
+    s.pdf = pdf_bsdf(X, V, L);
+    return s;
+}
+
+/* ------------------------------------------------------------------ camera */
+static ray camera_ray(const ctx *c, uint32_t x, uint32_t y) { /* GenerateRayFromThreadID, PT_01:496-507 */
+    const float *vpinv = (const float *)(c->U + U_VPINV);
+    float u = ((float)x + 0.5f) / (float)c->U[U_W];
+    float v = ((float)y + 0.5f) / (float)c->U[U_H];
+    ray clip = {V3(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f), V3(0.0f, 0.0f, 1.0f)};
+    return transform_ray(vpinv, clip, 1);
+}
+static v3 get_x0(const ctx *c, uint32_t x, uint32_t y) { /* Get_X0, PT_1:732-738 */
+    const float *vpinv = (const float *)(c->U + U_VPINV);
+    float u = ((float)x + 0.5f) / (float)c->U[U_W];
+    float v = ((float)y + 0.5f) / (float)c->U[U_H];
+    return xform_point(vpinv, V3(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
+}
+static inline uint32_t init_seed(const ctx *c, uint32_t x, uint32_t y) { /* PT_1:823-826 */
+    return pto_pcg(x * 1973u + y * 9277u + c->U[U_FRAME] * 26699u);
+}
+
+/* G-buffer texel encode / decode, PT_01:643-653, PT_1:409-436 */
+static inline void encode_compact(compact s, uint32_t *out4) {
+    out4[0] = (s.valid << 31) | (s.inst << 16) | s.mat;
+    out4[1] = s.prim;
+    out4[2] = u32_of(s.bu);
+    out4[3] = u32_of(s.bv);
+}
+static inline compact decode_compact(const uint32_t *in4) {
+    compact s;
+    s.valid = (in4[0] & 0x80000000u) != 0u;
+    s.inst = (in4[0] & 0x7fff0000u) >> 16;
+    s.mat = in4[0] & 0x0000ffffu;
+    s.prim = in4[1];
+    s.bu = f32_of(in4[2]);
+    s.bv = f32_of(in4[3]);
+    return s;
+}
+
+static void ctx_init(ctx *c, const pto_inputs *in, pass_eps eps, pto_counters *cnt) {
+    c->U = in->uniform;
+    c->S = in->scene;
+    c->G = in->geometry;
+    c->A = in->accel;
+    c->eps = eps;
+    c->cnt = cnt;
+}
+
+/* ================================================================== PT_01 G-buffer */
+void pto_gbuffer(const pto_inputs *in, int x0, int y0, int x1, int y1, uint32_t *gbuffer, pto_counters *cnt) {
+    ctx c;
+    ctx_init(&c, in, EPS_GBUFFER, cnt);
+    const uint32_t W = c.U[U_W];
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            ray r = camera_ray(&c, (uint32_t)x, (uint32_t)y);
+            hit h = trace_ray(&c, r);
+            compact s = h.s;
+            s.valid = (uint32_t)h.valid;
+            encode_compact(s, gbuffer + 4u * ((uint32_t)y * W + (uint32_t)x));
+        }
+}
+
+/* ================================================================== PT_1 init pass */
+typedef struct path_state {
+    v3 pos[4];          /* Path.Surface[k].Position, k = 0..3                 */
+    float rough[4];     /* Path.Surface[k].Material.Roughness (k >= 1)        */
+    uint32_t lobe[4];   /* Path.Lobe[k] as set after SampleBSDF at vertex k   */
+    uint32_t nee_seed[4], bsdf_seed[4]; /* Path.rSeed[k+1] before NEE / BSDF at k */
+    compact cs[4];      /* CSurface[k]                                        */
+} path_state;
+
+/* CompressPath + SafeReconnectionIndex, PT_1:1262-1353, on the candidate chosen by
+ * UpdateReservoir. Candidate = (vertex i, NEE or env).  The snapshot Path it stands for
+ * has Surface[0..i] = the chain's, Lobe[1..i-1] set (and Lobe[i] for env),
+ * rSeed[2..i] = BSDF seeds of vertices 1..i-1, rSeed[i+1] = NEE seed (NEE) or BSDF seed
+ * (env) of vertex i, zero elsewhere. */
+static void compress_path(const path_state *ps, int i, int is_env, const light_sample *XL, uint32_t *out) {
+    uint32_t lobe[8] = {0}, seed[8] = {0};
+    for (int k = 1; k < i; ++k) { lobe[k] = ps->lobe[k]; seed[k + 1] = ps->bsdf_seed[k]; }
+    if (is_env) { lobe[i] = ps->lobe[i]; seed[i + 1] = ps->bsdf_seed[i]; }
+    else seed[i + 1] = ps->nee_seed[i];
+    const uint32_t length = (uint32_t)i + 1u;
+    uint32_t k = 0;
+    for (uint32_t kk = 2; kk < length; ++kk) {
+        float ra = lobe[kk - 1] == LOBE_LAMBERT ? 1.0f : ps->rough[kk - 1];
+        float rb = lobe[kk] == LOBE_LAMBERT ? 1.0f : ps->rough[kk];
+        int rough = fmin_(ra, rb) >= RECONNECTION_ROUGHNESS;
+        int far = vlength(vsub(ps->pos[kk - 1], ps->pos[kk])) >= RECONNECTION_DISTANCE;
+        if (far && rough) { k = kk; break; }
+    }
+    if (k == 0) {
+        int rough = ps->rough[length - 1] >= RECONNECTION_ROUGHNESS;
+        int dirl = XL->type == LIGHT_DIRECTION || XL->type == LIGHT_ENV;
+        int far = dirl || vlength(vsub(ps->pos[length - 1], XL->pos)) >= RECONNECTION_DISTANCE;
+        if (far && rough) k = length;
+    }
+    memset(out, 0, 4u * PTO_RESERVOIR_WORDS);
+    out[0] = seed[2]; out[1] = seed[3]; out[2] = seed[4]; out[3] = seed[5];
+    out[4] = u32_of(XL->dir.x); out[5] = u32_of(XL->dir.y); out[6] = u32_of(XL->dir.z);
+    out[7] = XL->type;
+    out[8] = u32_of(XL->pos.x); out[9] = u32_of(XL->pos.y); out[10] = u32_of(XL->pos.z);
+    out[11] = (uint32_t)XL->id;
+    out[12] = u32_of(XL->Le.x); out[13] = u32_of(XL->Le.y); out[14] = u32_of(XL->Le.z);
+    out[15] = u32_of(XL->pdf);
+    out[20] = k;
+    out[23] = length;
+    if (k != 0) {
+        int is_light = (k == length);
+        out[22] = is_light ? LOBE_LIGHT : lobe[k];
+        out[21] = lobe[k - 1];
+        if (!is_light) encode_compact(ps->cs[k], out + 16);
+    }
+}
+
+static void init_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t x, uint32_t y, uint32_t *res) {
+    const uint32_t W = c->U[U_W];
+    compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
+    if (!x1.valid) { /* reservoir unobservable: PT_4 returns before LoadReservoir (:1404-1408) */
+        memset(res, 0, 4u * PTO_RESERVOIR_WORDS);
+        return;
+    }
+    uint32_t seed = init_seed(c, x, y);
+    v3 f = V3(1.0f, 1.0f, 1.0f);
+    float p = 1.0f;
+    path_state ps;
+    memset(&ps, 0, sizeof ps);
+    surface X[4];
+    memset(X, 0, sizeof X);
+    ps.cs[1] = x1;
+    X[0].pos = get_x0(c, x, y);
+    X[1] = get_surface(c, x1);
+    ps.pos[0] = X[0].pos;
+    ps.pos[1] = X[1].pos;
+    ps.rough[1] = X[1].mat.roughness;
+    /* PathReservoir */
+    uint32_t C = 0;
+    float w_sum = 0.0f, p_hat_sel = 0.0f;
+    int sel_i = -1, sel_env = 0;
+    light_sample sel_XL;
+    memset(&sel_XL, 0, sizeof sel_XL);
+
+    for (int i = 1; i < 4; ++i) {
+        const surface *S = &X[i];
+        v3 V = vnormalize(vsub(X[i - 1].pos, S->pos));
+        /* Submit NEE path, PT_1:1407-1422 */
+        ps.nee_seed[i] = seed;
+        light_sample XL = sample_nee(c, &seed, S, V);
+        v3 L = direction_to_light(S, &XL);
+        v3 contrib = vmul(f, l_emit(c, &XL, S));
+        contrib = vmul(contrib, bsdf(S, V, L));
+        contrib = vscale(contrib, fabsf(vdot(S->nrm, L)));
+        contrib = vscale(contrib, visibility(c, S->pos, XL.pos));
+        float p_hat = luminance(contrib);
+        float ris = p_hat / (p * XL.pdf);
+        C += 1u; /* UpdateReservoir, PT_1:1298-1320 */
+        w_sum += ris;
+        if (pto_random(&seed) < ris / w_sum) { sel_i = i; sel_env = 0; sel_XL = XL; p_hat_sel = p_hat; }
+        if (i == 3) break;
+        /* Sample BSDF, PT_1:1427-1433 */
+        ps.bsdf_seed[i] = seed;
+        uint32_t lobe;
+        L = sample_bsdf(&seed, S, V, &lobe);
+        ps.lobe[i] = lobe;
+        /* path throughput + Russian roulette, PT_1:1436-1442 */
+        v3 b = vscale(bsdf(S, V, L), fabsf(vdot(S->nrm, L)));
+        f = vmul(f, b);
+        p *= pdf_bsdf(S, V, L);
+        float p_survive = luminance(f) / p;
+        if (pto_random(&seed) < p_survive) p *= p_survive;
+        else break;
+        ray r = {S->pos, L};
+        hit h = trace_ray(c, r);
+        if (!h.valid) { /* Submit env path, PT_1:1447-1461 */
+            light_sample env = create_env_light(S, V, L);
+            float ph = luminance(vscale(f, ENV_C));
+            float ris_e = ph / p;
+            C += 1u;
+            w_sum += ris_e;
+            if (pto_random(&seed) < ris_e / w_sum) { sel_i = i; sel_env = 1; sel_XL = env; p_hat_sel = ph; }
+            break;
+        }
+        ps.cs[i + 1] = h.s;
+        X[i + 1] = get_surface(c, h.s);
+        ps.pos[i + 1] = X[i + 1].pos;
+        ps.rough[i + 1] = X[i + 1].mat.roughness;
+    }
+    /* StoreReservoir, PT_1:1475-1483 */
+    if (sel_i < 0) memset(res, 0, 4u * PTO_RESERVOIR_WORDS); /* zero Path(): length 0, k 0 */
+    else compress_path(&ps, sel_i, sel_env, &sel_XL, res);
+    res[28] = u32_of(w_sum / p_hat_sel);
+    res[29] = C;
+}
+
+void pto_init(const pto_inputs *in, const uint32_t *gbuffer, int x0, int y0, int x1, int y1, uint32_t *reservoir,
+              pto_counters *cnt) {
+    ctx c;
+    ctx_init(&c, in, EPS_INIT, cnt);
+    const uint32_t W = c.U[U_W];
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x)
+            init_pixel(&c, gbuffer, (uint32_t)x, (uint32_t)y,
+                       reservoir + PTO_RESERVOIR_WORDS * ((uint32_t)y * W + (uint32_t)x));
+}
+
+/* ================================================================== PT_4 final shading */
+static void write_color(const ctx *c, float *px, v3 col) { /* WriteColor, PT_4:599-606 */
+    float t = 1.0f / (float)(c->U[U_FRAME] + 1u);
+    px[0] = mixf(px[0], col.x, t);
+    px[1] = mixf(px[1], col.y, t);
+    px[2] = mixf(px[2], col.z, t);
+    px[3] = 1.0f;
+}
+
+static void final_pixel(const ctx *c, const uint32_t *gbuffer, const uint32_t *res, uint32_t x, uint32_t y,
+                        float *px) {
+    const uint32_t W = c->U[U_W];
+    compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
+    if (!x1.valid) { px[0] = px[1] = px[2] = ENV_C; px[3] = 1.0f; return; }
+    const uint32_t C = res[29], length = res[23];
+    if (C == 0u || length < 2u) { write_color(c, px, V3(0.0f, 0.0f, 0.0f)); return; }
+    light_sample XL;
+    XL.dir = V3(f32_of(res[4]), f32_of(res[5]), f32_of(res[6]));
+    XL.type = res[7];
+    XL.pos = V3(f32_of(res[8]), f32_of(res[9]), f32_of(res[10]));
+    XL.id = (int32_t)res[11];
+    XL.Le = V3(f32_of(res[12]), f32_of(res[13]), f32_of(res[14]));
+    XL.pdf = f32_of(res[15]);
+    /* RegeneratePath, PT_4:1357-1384 */
+    surface S[8];
+    memset(S, 0, sizeof S);
+    S[0].pos = get_x0(c, x, y);
+    S[1] = get_surface(c, x1);
+    for (uint32_t i = 1; i + 1u < length; ++i) {
+        v3 V = vnormalize(vsub(S[i - 1].pos, S[i].pos));
+        uint32_t seed = res[i - 1u];
+        uint32_t lobe;
+        v3 dir = sample_bsdf(&seed, &S[i], V, &lobe);
+        ray r = {S[i].pos, dir};
+        hit h = trace_ray(c, r);
+        S[i + 1] = get_surface(c, h.s); /* a miss decodes the zero CompactSurface, as the WGSL does */
+    }
+    /* PathContribution, PT_4:1306-1336 */
+    v3 f = V3(1.0f, 1.0f, 1.0f);
+    for (uint32_t i = 1; i + 1u < length; ++i) {
+        v3 V = vnormalize(vsub(S[i - 1].pos, S[i].pos));
+        v3 L = vnormalize(vsub(S[i + 1].pos, S[i].pos));
+        f = vmul(f, vscale(bsdf(&S[i], L, V), fabsf(vdot(S[i].nrm, L))));
+    }
+    {
+        const surface *P = &S[length - 2u], *Xc = &S[length - 1u];
+        v3 V = vnormalize(vsub(P->pos, Xc->pos));
+        v3 L = direction_to_light(Xc, &XL);
+        f = vmul(f, vscale(bsdf(Xc, L, V), fabsf(vdot(Xc->nrm, L))));
+        f = vmul(f, vscale(l_emit(c, &XL, Xc), visibility(c, Xc->pos, XL.pos)));
+    }
+    write_color(c, px, vscale(f, f32_of(res[28])));
+}
+
+void pto_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *reservoir, int x0, int y0, int x1,
+               int y1, float *accum, pto_counters *cnt) {
+    ctx c;
+    ctx_init(&c, in, EPS_FINAL, cnt);
+    const uint32_t W = c.U[U_W];
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            uint32_t p = (uint32_t)y * W + (uint32_t)x;
+            final_pixel(&c, gbuffer, reservoir + PTO_RESERVOIR_WORDS * p, (uint32_t)x, (uint32_t)y, accum + 4u * p);
+        }
+}
+
+/* ================================================================== TEST_MCPT */
+/* GetLightColor, SH/TEST_MCPT.wgsl:1261-1309 */
+static v3 light_color(const ctx *c, uint32_t *seed, const surface *X, v3 V, uint32_t id) {
+    light_sample XL;
+    memset(&XL, 0, sizeof XL);
+    light ls = get_light(c, id);
+    XL.type = ls.type;
+    XL.Le = vscale(ls.color, ls.intensity);
+    switch (ls.type) {
+    case LIGHT_DIRECTION:
+        XL.pos = vsub(X->pos, vscale(ls.dir, INF_F));
+        XL.dir = ls.dir;
+        XL.pdf = 1.0f;
+        break;
+    case LIGHT_POINT:
+        XL.pos = ls.pos;
+        XL.dir = vnormalize(vsub(X->pos, ls.pos));
+        XL.pdf = 1.0f;
+        break;
+    case LIGHT_RECT: {
+        float ru = pto_random(seed) * 2.0f - 1.0f;
+        float rv = pto_random(seed) * 2.0f - 1.0f;
+        v3 off = vadd(vscale(ls.U, ru), vscale(ls.V, rv));
+        XL.pos = vadd(ls.pos, off);
+        XL.dir = vnormalize(vsub(X->pos, XL.pos));
+        v3 r = vsub(XL.pos, X->pos);
+        v3 L = vnormalize(r);
+        XL.pdf = vdot(r, r) / fmax_(ls.area * fabsf(vdot(ls.dir, L)), EPS_F);
+        break;
+    }
+    default: break;
+    }
+    v3 L = direction_to_light(X, &XL);
+    v3 out = vmul(l_emit(c, &XL, X), bsdf(X, V, L));
+    out = vscale(out, fabsf(vdot(X->nrm, L)));
+    out = vscale(out, visibility(c, X->pos, XL.pos));
+    return vdivs(out, XL.pdf);
+}
+
+static void mcpt_pixel(const ctx *c, uint32_t x, uint32_t y, float *px) { /* TEST_MCPT.wgsl:1315-1372 */
+    uint32_t seed = init_seed(c, x, y);
+    ray r = camera_ray(c, x, y);
+    v3 color = V3(0.0f, 0.0f, 0.0f), f = V3(1.0f, 1.0f, 1.0f);
+    float p = 1.0f;
+    const uint32_t nl = c->U[U_LIGHT_COUNT];
+    for (int bounce = 0; bounce < 3; ++bounce) {
+        hit h = trace_ray(c, r);
+        if (!h.valid) {
+            color = vadd(color, vscale(vdivs(f, p), ENV_C));
+            break;
+        }
+        surface X = get_surface(c, h.s);
+        v3 V = vnormalize(vsub(r.o, X.pos));
+        for (uint32_t id = 0; id < nl; ++id)
+            color = vadd(color, vmul(vdivs(f, p), light_color(c, &seed, &X, V, id)));
+        uint32_t lobe;
+        v3 L = sample_bsdf(&seed, &X, V, &lobe);
+        f = vmul(f, vscale(bsdf(&X, V, L), fabsf(vdot(X.nrm, L))));
+        p *= pdf_bsdf(&X, V, L);
+        r.o = X.pos;
+        r.d = L;
+        float ps = luminance(f) / p;
+        if (pto_random(&seed) < ps) p *= ps;
+        else break;
+    }
+    write_color(c, px, color);
+}
+
+void pto_mcpt(const pto_inputs *in, int x0, int y0, int x1, int y1, float *accum, pto_counters *cnt) {
+    ctx c;
+    ctx_init(&c, in, EPS_MCPT, cnt);
+    const uint32_t W = c.U[U_W];
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x)
+            mcpt_pixel(&c, (uint32_t)x, (uint32_t)y, accum + 4u * ((uint32_t)y * W + (uint32_t)x));
+}
+
+/* ================================================================== KAT helpers */
+static surface kat_surface(const float *n, const float *mat) {
+    surface s;
+    memset(&s, 0, sizeof s);
+    s.nrm = V3(n[0], n[1], n[2]);
+    s.mat.albedo = V3(mat[0], mat[1], mat[2]);
+    s.mat.metalness = mat[3];
+    s.mat.roughness = mat[4];
+    s.mat.transmission = mat[5];
+    s.mat.ior = mat[6];
+    return s;
+}
+void pto_bsdf(const float n[3], const float mat[7], const float v[3], const float l[3], float out[3]) {
+    surface s = kat_surface(n, mat);
+    v3 r = bsdf(&s, V3(v[0], v[1], v[2]), V3(l[0], l[1], l[2]));
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+float pto_pdf_bsdf(const float n[3], const float mat[7], const float v[3], const float l[3]) {
+    surface s = kat_surface(n, mat);
+    return pdf_bsdf(&s, V3(v[0], v[1], v[2]), V3(l[0], l[1], l[2]));
+}
+void pto_sample_bsdf(const float n[3], const float mat[7], const float v[3], uint32_t *seed, float out_dir[3],
+                     uint32_t *out_lobe) {
+    surface s = kat_surface(n, mat);
+    v3 d = sample_bsdf(seed, &s, V3(v[0], v[1], v[2]), out_lobe);
+    out_dir[0] = d.x; out_dir[1] = d.y; out_dir[2] = d.z;
+}
+float pto_ray_triangle(const float o[3], const float d[3], const float p0[3], const float p1[3], const float p2[3],
+                       float det_eps) {
+    ray r = {V3(o[0], o[1], o[2]), V3(d[0], d[1], d[2])};
+    return ray_triangle(r, V3(p0[0], p0[1], p0[2]), V3(p1[0], p1[1], p1[2]), V3(p2[0], p2[1], p2[2]), det_eps);
+}
+
+/* ================================================================== threaded driver */
+typedef struct job {
+    int pass, tid, nthreads, x0, y0, x1, y1;
+    const pto_inputs *in;
+    uint32_t *gbuffer, *reservoir;
+    float *accum;
+    pto_counters cnt;
+} job;
+
+static void *worker(void *arg) {
+    job *j = (job *)arg;
+    for (int y = j->y0 + j->tid; y < j->y1; y += j->nthreads) {
+        switch (j->pass) {
+        case 0: pto_gbuffer(j->in, j->x0, y, j->x1, y + 1, j->gbuffer, &j->cnt); break;
+        case 1: pto_init(j->in, j->gbuffer, j->x0, y, j->x1, y + 1, j->reservoir, &j->cnt); break;
+        case 2: pto_final(j->in, j->gbuffer, j->reservoir, j->x0, y, j->x1, y + 1, j->accum, &j->cnt); break;
+        case 3: pto_mcpt(j->in, j->x0, y, j->x1, y + 1, j->accum, &j->cnt); break;
+        default: break;
+        }
+    }
+    return NULL;
+}
+
+static int run_pass(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                    uint32_t *gbuffer, uint32_t *reservoir, float *accum, pto_counters *cnt) {
+    if (nthreads < 1) nthreads = 1;
+    job *jobs = (job *)calloc((size_t)nthreads, sizeof(job));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    if (!jobs || !th) { free(jobs); free(th); return -1; }
+    for (int t = 0; t < nthreads; ++t) {
+        job j = {pass, t, nthreads, x0, y0, x1, y1, in, gbuffer, reservoir, accum, {0, 0, 0, 0, 0}};
+        jobs[t] = j;
+        if (nthreads > 1) pthread_create(&th[t], NULL, worker, &jobs[t]);
+    }
+    if (nthreads == 1) worker(&jobs[0]);
+    for (int t = 0; t < nthreads; ++t) {
+        if (nthreads > 1) pthread_join(th[t], NULL);
+        if (cnt) {
+            cnt->rays += jobs[t].cnt.rays;
+            cnt->instance_xforms += jobs[t].cnt.instance_xforms;
+            cnt->aabb_tests += jobs[t].cnt.aabb_tests;
+            cnt->tri_tests += jobs[t].cnt.tri_tests;
+            cnt->hits += jobs[t].cnt.hits;
+        }
+    }
+    free(jobs);
+    free(th);
+    return 0;
+}
+
+int pto_run(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, uint32_t *gbuffer,
+            uint32_t *reservoir, float *accum, pto_counters *cnt) {
+    if (pass == 4) {
+        int rc = run_pass(0, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, accum, cnt);
+        if (!rc) rc = run_pass(1, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, accum, cnt);
+        if (!rc) rc = run_pass(2, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, accum, cnt);
+        return rc;
+    }
+    return run_pass(pass, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, accum, cnt);
+}

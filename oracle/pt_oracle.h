@@ -1,0 +1,83 @@
+/*
+ * pt_oracle.h -- CPU restatement of the reference's per-pixel path (TEST INFRASTRUCTURE).
+ *
+ * This is the parity CHECKER for the HIP path, never the product: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * It restates, function for function and in the same f32 operation order, the WGSL of
+ * hdm0922/PathTracerDemo (SH/ = apps/frontend/src/graphics-core/shaders/):
+ *   pto_gbuffer  <- SH/PT_01_GBufferPass.wgsl:496-659
+ *   pto_init     <- SH/PT_1_InitPass.wgsl:1361-1486
+ *   pto_final    <- SH/PT_4_FinalShadingPass.wgsl:1392-1428
+ *   pto_mcpt     <- SH/TEST_MCPT.wgsl:1315-1372
+ * over the reference's own device inputs (uniform block, SceneBuffer, GeometryBuffer,
+ * AccelBuffer; Renderer_TEST.ts:165-206,267-420).  Implementation-defined WGSL details
+ * are fixed as documented in DESIGN.md §Numerics (left-to-right dot/mat-vec sums, no
+ * FMA contraction, normalize(v) = v / length(v), IEEE minNum/maxNum for min/max).
+ *
+ * Parity pinning: the reference ships no tests, golden images or runnable WGSL
+ * runtime.  The restatement is pinned by the known-answer tests in
+ * tests/golden (PCG hash values published with the algorithm, analytic BSDF values)
+ * and by an independent numpy spot-checker (tests/numpy_ref.py).
+ */
+#ifndef PT_ORACLE_H
+#define PT_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTO_UNIFORM_WORDS 33
+#define PTO_RESERVOIR_WORDS 32
+
+typedef struct pto_inputs {
+    const uint32_t *uniform;   /* 33 words, Renderer_TEST.ts:174-202 */
+    const uint32_t *scene;     /* SceneBuffer    */
+    const uint32_t *geometry;  /* GeometryBuffer */
+    const uint32_t *accel;     /* AccelBuffer    */
+} pto_inputs;
+
+/* Work counters for the algorithmic-bytes model of SURVEY.md §8(d). */
+typedef struct pto_counters {
+    uint64_t rays;            /* TraceRay calls                          */
+    uint64_t instance_xforms; /* instance ray transforms (48 B each)     */
+    uint64_t aabb_tests;      /* slab tests (32 B each)                  */
+    uint64_t tri_tests;       /* Moller-Trumbore tests (36 B each)       */
+    uint64_t hits;            /* hit reconstructions (48 B each)         */
+} pto_counters;
+
+/* One pass over pixels [x0,x1) x [y0,y1). Buffers are full-frame (W*H). */
+void pto_gbuffer(const pto_inputs *in, int x0, int y0, int x1, int y1, uint32_t *gbuffer /* W*H*4 */,
+                 pto_counters *cnt);
+void pto_init(const pto_inputs *in, const uint32_t *gbuffer, int x0, int y0, int x1, int y1,
+              uint32_t *reservoir /* W*H*32 */, pto_counters *cnt);
+void pto_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *reservoir, int x0, int y0,
+               int x1, int y1, float *accum /* W*H*4 in/out */, pto_counters *cnt);
+void pto_mcpt(const pto_inputs *in, int x0, int y0, int x1, int y1, float *accum /* W*H*4 in/out */,
+              pto_counters *cnt);
+
+/* Multithreaded driver: pass = 0 gbuffer, 1 init, 2 final, 3 mcpt, 4 restir frame (0,1,2).
+ * Rows [y0,y1) are interleaved over nthreads pthreads.  Returns 0 on success. */
+int pto_run(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, uint32_t *gbuffer,
+            uint32_t *reservoir, float *accum, pto_counters *cnt);
+
+/* Known-answer helpers (SH/PT_1_InitPass.wgsl:810-826). */
+uint32_t pto_pcg(uint32_t seed);
+float pto_random(uint32_t *seed);
+
+/* BSDF / PDF known-answer helpers on an explicit surface (SH/PT_1_InitPass.wgsl:834-1245).
+ * mat = {albedo r,g,b, metalness, roughness, transmission, ior} AFTER GetMaterial's tweaks. */
+void pto_bsdf(const float n[3], const float mat[7], const float v[3], const float l[3], float out[3]);
+float pto_pdf_bsdf(const float n[3], const float mat[7], const float v[3], const float l[3]);
+void pto_sample_bsdf(const float n[3], const float mat[7], const float v[3], uint32_t *seed, float out_dir[3],
+                     uint32_t *out_lobe);
+float pto_ray_triangle(const float o[3], const float d[3], const float p0[3], const float p1[3],
+                       const float p2[3], float det_eps);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,83 @@
+"""ctypes binding of libptx.so (the C ABI of include/ptx.h).
+
+The product path: if the HIP library is missing or fails to load, importing the
+renderer raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libptx.so")
+
+PTX_OK = 0
+PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT = 0, 1
+PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT = 0, 1, 2, 3
+PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS = 0, 1, 2, 3
+PTX_FLAG_COUNT_WORK = 1
+
+# every symbol include/ptx.h declares (checked by tests/test_abi.py)
+EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame", "ptx_render", "ptx_run_pass",
+            "ptx_reset_accumulation", "ptx_synchronize", "ptx_get_stats", "ptx_reset_stats", "ptx_read_buffer",
+            "ptx_write_buffer", "ptx_device_pointer", "ptx_set_stream", "ptx_destroy", "ptx_last_error"]
+
+
+class PtxConfig(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("row_begin", ctypes.c_uint32),
+                ("row_end", ctypes.c_uint32), ("device", ctypes.c_int32), ("pipeline", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 5)]
+
+
+class PtxStats(ctypes.Structure):
+    _fields_ = [("frames", ctypes.c_uint64), ("kernel_ms_total", ctypes.c_double * 4),
+                ("kernel_launches", ctypes.c_uint64 * 4), ("triangles", ctypes.c_uint32),
+                ("bvh_nodes", ctypes.c_uint32), ("instances", ctypes.c_uint32), ("max_bvh_depth", ctypes.c_uint32),
+                ("device_bytes", ctypes.c_uint64)]
+
+
+class PtxError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libptx.so; raises PtxError when the HIP extension is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise PtxError(f"{path} is missing: build it with `make -C pathtracerdemo_amd/csrc` "
+                       "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    P, H = ctypes.c_void_p, ctypes.c_void_p
+    lib.ptx_abi_version.restype = ctypes.c_int
+    lib.ptx_create.argtypes = [ctypes.POINTER(PtxConfig), ctypes.POINTER(H)]
+    lib.ptx_upload_scene.argtypes = [H, P, ctypes.c_size_t, P, ctypes.c_size_t, P, ctypes.c_size_t]
+    lib.ptx_set_frame.argtypes = [H, P]
+    lib.ptx_render.argtypes = [H, P]
+    lib.ptx_run_pass.argtypes = [H, ctypes.c_int]
+    lib.ptx_reset_accumulation.argtypes = [H]
+    lib.ptx_synchronize.argtypes = [H]
+    lib.ptx_get_stats.argtypes = [H, ctypes.POINTER(PtxStats)]
+    lib.ptx_reset_stats.argtypes = [H]
+    lib.ptx_read_buffer.argtypes = [H, ctypes.c_int, P, ctypes.c_size_t]
+    lib.ptx_write_buffer.argtypes = [H, ctypes.c_int, P, ctypes.c_size_t]
+    lib.ptx_device_pointer.argtypes = [H, ctypes.c_int, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.ptx_set_stream.argtypes = [H, P]
+    lib.ptx_destroy.argtypes = [H]
+    lib.ptx_last_error.argtypes = [H]
+    lib.ptx_last_error.restype = ctypes.c_char_p
+    for name in EXPORTED:
+        if name not in ("ptx_last_error", "ptx_abi_version"):
+            getattr(lib, name).restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def check(lib, handle, rc: int, what: str):
+    if rc != PTX_OK:
+        msg = lib.ptx_last_error(handle) if handle else b""
+        raise PtxError(f"{what} failed ({rc}): {msg.decode(errors='replace') if msg else ''}")

@@ -1,0 +1,507 @@
+// ptx_api.cpp -- C-ABI boundary (include/ptx.h) of the MI355X path tracer.
+//
+// Mirrors the WebGPU host of the reference (apps/frontend/src/graphics-core/
+// Renderer_TEST.ts; GC/ below): buffers of CreateGPUResources (:445-460), the uniform
+// block of Update (:165-206), the three dispatches of Render (:208-261).  On top of the
+// reference arrays it derives the MI355X traversal layout described in ptx_device.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ptx.h"
+#include "ptx_launch.h"
+
+using namespace ptx;
+
+namespace {
+
+constexpr int kPasses = 4;
+constexpr int kEventRing = 64;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct TimedLaunch {
+    hipEvent_t start = nullptr, stop = nullptr;
+    int pass = -1;
+    bool pending = false;
+};
+
+}  // namespace
+
+struct ptx_handle {
+    ptx_config cfg{};
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // reference arrays (host copies: the derived layout is rebuilt when offsets change)
+    std::vector<uint32_t> scene, geometry, accel;
+    DevBuf d_scene, d_geometry;
+    // derived MI355X layout
+    DevBuf d_tris, d_nodes, d_subs, d_insts;
+    uint32_t n_tris = 0, n_nodes = 0, n_inst = 0, max_depth = 0, stack_depth = 0;
+    uint32_t layout_key[8] = {0};
+    bool layout_valid = false;
+    bool scene_loaded = false;
+    // frame
+    uint32_t uniform[PTX_UNIFORM_WORDS] = {0};
+    bool frame_set = false;
+    // band buffers
+    uint32_t band_h = 0;
+    DevBuf d_gbuf, d_res, d_accum, d_counters;
+    // stats
+    TimedLaunch ring[kEventRing];
+    int ring_pos = 0;
+    double ms_total[kPasses] = {0, 0, 0, 0};
+    uint64_t launches[kPasses] = {0, 0, 0, 0};
+    uint64_t frames = 0;
+};
+
+static int fail(ptx_handle *h, int code, const char *fmt, ...) {
+    if (h) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        h->err = buf;
+    }
+    return code;
+}
+#define HIP_CHECK(h, expr)                                                                                   \
+    do {                                                                                                     \
+        hipError_t e_ = (expr);                                                                              \
+        if (e_ != hipSuccess) return fail((h), PTX_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                                          __FILE__, __LINE__);                                               \
+    } while (0)
+
+static void free_buf(DevBuf &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+static int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
+    if (b.bytes == bytes && b.p) return PTX_OK;
+    free_buf(b);
+    if (bytes == 0) return PTX_OK;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) return fail(h, PTX_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    b.bytes = bytes;
+    return PTX_OK;
+}
+static int upload(ptx_handle *h, DevBuf &b, const void *src, size_t bytes) {
+    int rc = alloc_buf(h, b, std::max<size_t>(bytes, 16));
+    if (rc) return rc;
+    if (bytes) HIP_CHECK(h, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    return PTX_OK;
+}
+
+static inline float as_f32(uint32_t u) {
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+// ---------------------------------------------------------------- layout derivation
+// Walks the reference's per-sub-mesh BLAS (three-mesh-bvh node format, GC/Structs.ts:73-80;
+// read by GetBlasNode, SH/PT_01_GBufferPass.wgsl:310-322) and emits the child-pair node
+// records, the edge-form triangle table and the instance table of ptx_device.h.
+static int build_layout(ptx_handle *h) {
+    const uint32_t *U = h->uniform;
+    const auto &S = h->scene, &G = h->geometry, &A = h->accel;
+    const uint32_t off_desc = U[U_OFF_DESC], off_mat = U[U_OFF_MAT], off_index = U[U_OFF_INDEX];
+    const uint32_t off_subroot = U[U_OFF_SUBROOT], off_blas = U[U_OFF_BLAS], n_inst = U[U_INST_COUNT];
+    if (off_mat < off_desc || (off_mat - off_desc) % STRIDE_DESCRIPTOR)
+        return fail(h, PTX_E_SCENE, "uniform offsets: descriptor block [%u,%u) is not a multiple of 6", off_desc, off_mat);
+    const uint32_t n_mesh = (off_mat - off_desc) / STRIDE_DESCRIPTOR;
+    if ((size_t)n_inst * STRIDE_INSTANCE > off_desc)
+        return fail(h, PTX_E_SCENE, "instance count %u overlaps the descriptor block", n_inst);
+    if (off_desc + (size_t)n_mesh * STRIDE_DESCRIPTOR > S.size()) return fail(h, PTX_E_SCENE, "scene buffer too short");
+
+    std::vector<SubRoot> subs;
+    std::vector<NodePair> nodes;
+    std::vector<float> tris;  // 12 floats per triangle
+    std::vector<uint32_t> mesh_sub_base(n_mesh), mesh_nsub(n_mesh), mesh_tri_base(n_mesh);
+    uint32_t max_depth = 0;
+
+    for (uint32_t m = 0; m < n_mesh; ++m) {
+        const uint32_t *d = S.data() + off_desc + STRIDE_DESCRIPTOR * m;
+        const uint32_t off_vertex = d[0], off_idx = d[1], off_root = d[3], off_b = d[4], nsub = d[5];
+        mesh_sub_base[m] = (uint32_t)subs.size();
+        mesh_nsub[m] = nsub;
+        mesh_tri_base[m] = (uint32_t)(tris.size() / 12);
+        uint32_t mesh_tris = 0;
+        struct Pending { uint32_t base; std::vector<uint32_t> order; };
+        std::vector<Pending> per_sub;
+        for (uint32_t s = 0; s < nsub; ++s) {
+            size_t ri = (size_t)off_subroot + off_root + s;
+            if (ri >= G.size()) return fail(h, PTX_E_SCENE, "sub-BLAS root index out of range");
+            const uint32_t base = off_blas + off_b + G[ri];
+            // DFS over the sub-BVH to number interior nodes
+            std::unordered_map<uint32_t, uint32_t> gidx;
+            std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 0u}};
+            std::vector<uint32_t> interior;
+            while (!st.empty()) {
+                auto [n, depth] = st.back();
+                st.pop_back();
+                size_t w = (size_t)base + 8u * n;
+                if (w + 8 > A.size()) return fail(h, PTX_E_SCENE, "BLAS node %u out of range", n);
+                max_depth = std::max(max_depth, depth);
+                if (A[w + 7] & 0xffff0000u) {
+                    uint32_t first = A[w + 6], count = A[w + 7] & 0xffffu;
+                    mesh_tris = std::max(mesh_tris, first + count);
+                    continue;
+                }
+                gidx[n] = (uint32_t)(nodes.size() + interior.size());
+                interior.push_back(n);
+                st.push_back({n + 1u, depth + 1});
+                st.push_back({A[w + 6] / 8u, depth + 1});
+                if (depth > 1000) return fail(h, PTX_E_SCENE, "BLAS too deep / cyclic");
+            }
+            auto ref_of = [&](uint32_t n, uint32_t &ref) -> int {
+                size_t w = (size_t)base + 8u * n;
+                if (A[w + 7] & 0xffff0000u) {
+                    uint32_t first = A[w + 6], count = A[w + 7] & 0xffffu;
+                    if (count >= 128u || first > LEAF_FIRST_MASK)
+                        return fail(h, PTX_E_SCENE, "leaf (first %u, count %u) exceeds the packed ref", first, count);
+                    ref = LEAF_BIT | (count << 24) | first;
+                } else {
+                    ref = gidx.at(n);
+                }
+                return PTX_OK;
+            };
+            SubRoot r{};
+            for (int k = 0; k < 3; ++k) { r.bmin[k] = as_f32(A[base + k]); r.bmax[k] = as_f32(A[base + 3 + k]); }
+            if (int rc = ref_of(0u, r.ref)) return rc;
+            subs.push_back(r);
+            for (uint32_t n : interior) {
+                size_t w = (size_t)base + 8u * n;
+                uint32_t L = n + 1u, R = A[w + 6] / 8u;
+                size_t wl = (size_t)base + 8u * L, wr = (size_t)base + 8u * R;
+                NodePair np{};
+                for (int k = 0; k < 3; ++k) {
+                    np.lmin[k] = as_f32(A[wl + k]); np.lmax[k] = as_f32(A[wl + 3 + k]);
+                    np.rmin[k] = as_f32(A[wr + k]); np.rmax[k] = as_f32(A[wr + 3 + k]);
+                }
+                if (int rc = ref_of(L, np.lref)) return rc;
+                if (int rc = ref_of(R, np.rref)) return rc;
+                nodes.push_back(np);
+            }
+        }
+        // edge-form triangles in index (leaf) order, local space
+        for (uint32_t prim = 0; prim < mesh_tris; ++prim) {
+            size_t ii = (size_t)off_index + off_idx + 3u * prim;
+            if (ii + 3 > G.size()) return fail(h, PTX_E_SCENE, "index buffer out of range");
+            float P[3][3];
+            for (int v = 0; v < 3; ++v) {
+                size_t vi = (size_t)off_vertex + STRIDE_VERTEX * G[ii + v];
+                if (vi + 3 > G.size()) return fail(h, PTX_E_SCENE, "vertex out of range");
+                for (int k = 0; k < 3; ++k) P[v][k] = as_f32(G[vi + k]);
+            }
+            const float e1[3] = {P[1][0] - P[0][0], P[1][1] - P[0][1], P[1][2] - P[0][2]};
+            const float e2[3] = {P[2][0] - P[0][0], P[2][1] - P[0][1], P[2][2] - P[0][2]};
+            const float rec[12] = {P[0][0], P[0][1], P[0][2], e1[0], e1[1], e1[2], e2[0], e2[1], e2[2], 0, 0, 0};
+            tris.insert(tris.end(), rec, rec + 12);
+        }
+    }
+    std::vector<Inst> insts(n_inst);
+    for (uint32_t i = 0; i < n_inst; ++i) {
+        const uint32_t *p = S.data() + STRIDE_INSTANCE * i;
+        Inst &I = insts[i];
+        std::memcpy(I.m, p, 64);
+        std::memcpy(I.minv, p + 16, 64);
+        I.mesh = p[32];
+        if (I.mesh >= n_mesh) return fail(h, PTX_E_SCENE, "instance %u references mesh %u of %u", i, I.mesh, n_mesh);
+        I.sub_base = mesh_sub_base[I.mesh];
+        I.nsub = mesh_nsub[I.mesh];
+        I.tri_base = mesh_tri_base[I.mesh];
+    }
+    if (tris.empty()) tris.resize(12, 0.0f);
+    if (nodes.empty()) nodes.resize(1);
+    if (subs.empty()) subs.resize(1);
+    if (int rc = upload(h, h->d_tris, tris.data(), tris.size() * sizeof(float))) return rc;
+    if (int rc = upload(h, h->d_nodes, nodes.data(), nodes.size() * sizeof(NodePair))) return rc;
+    if (int rc = upload(h, h->d_subs, subs.data(), subs.size() * sizeof(SubRoot))) return rc;
+    if (int rc = upload(h, h->d_insts, insts.data(), std::max<size_t>(1, insts.size()) * sizeof(Inst))) return rc;
+    (void)off_mat;
+    h->n_tris = (uint32_t)(tris.size() / 12);
+    h->n_nodes = (uint32_t)nodes.size();
+    h->n_inst = n_inst;
+    h->max_depth = max_depth;
+    h->stack_depth = max_depth + 2u;
+    if ((size_t)h->stack_depth * kBlock * 4u > 160u * 1024u)
+        return fail(h, PTX_E_SCENE, "BLAS depth %u needs more LDS than a CU has", max_depth);
+    h->layout_valid = true;
+    return PTX_OK;
+}
+
+static Scene make_scene(ptx_handle *h) {
+    Scene sc{};
+    std::memcpy(sc.U, h->uniform, sizeof sc.U);
+    sc.S = (const uint32_t *)h->d_scene.p;
+    sc.G = (const uint32_t *)h->d_geometry.p;
+    sc.tris = (const float4 *)h->d_tris.p;
+    sc.nodes = (const NodePair *)h->d_nodes.p;
+    sc.subs = (const SubRoot *)h->d_subs.p;
+    sc.insts = (const Inst *)h->d_insts.p;
+    sc.n_inst = h->n_inst;
+    sc.width = h->cfg.width;
+    sc.height = h->cfg.height;
+    sc.row_begin = h->cfg.row_begin;
+    sc.row_end = h->cfg.row_end;
+    sc.counters = (h->cfg.flags & PTX_FLAG_COUNT_WORK) ? (unsigned long long *)h->d_counters.p : nullptr;
+    return sc;
+}
+
+static void resolve_event(TimedLaunch &t, ptx_handle *h) {
+    if (!t.pending) return;
+    float ms = 0.0f;
+    if (hipEventSynchronize(t.stop) == hipSuccess && hipEventElapsedTime(&ms, t.start, t.stop) == hipSuccess) {
+        h->ms_total[t.pass] += ms;
+        h->launches[t.pass] += 1;
+    }
+    t.pending = false;
+}
+
+static int timed_launch(ptx_handle *h, int pass) {
+    if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before rendering");
+    if (!h->layout_valid) {
+        if (int rc = build_layout(h)) return rc;
+    }
+    TimedLaunch &t = h->ring[h->ring_pos];
+    h->ring_pos = (h->ring_pos + 1) % kEventRing;
+    resolve_event(t, h);
+    Scene sc = make_scene(h);
+    HIP_CHECK(h, hipEventRecord(t.start, h->stream));
+    hipError_t e = hipSuccess;
+    switch (pass) {
+    case PTX_PASS_GBUFFER: e = launch_gbuffer(sc, (uint4 *)h->d_gbuf.p, h->stack_depth, h->stream); break;
+    case PTX_PASS_INIT:
+        e = launch_init(sc, (const uint4 *)h->d_gbuf.p, (uint4 *)h->d_res.p, h->stack_depth, h->stream);
+        break;
+    case PTX_PASS_FINAL:
+        e = launch_final(sc, (const uint4 *)h->d_gbuf.p, (const uint4 *)h->d_res.p, (float4 *)h->d_accum.p,
+                         h->stack_depth, h->stream);
+        break;
+    case PTX_PASS_MCPT: e = launch_mcpt(sc, (float4 *)h->d_accum.p, h->stack_depth, h->stream); break;
+    default: return fail(h, PTX_E_INVALID, "unknown pass %d", pass);
+    }
+    if (e != hipSuccess) return fail(h, PTX_E_HIP, "kernel launch (pass %d): %s", pass, hipGetErrorString(e));
+    HIP_CHECK(h, hipEventRecord(t.stop, h->stream));
+    t.pass = pass;
+    t.pending = true;
+    return PTX_OK;
+}
+
+static DevBuf *buffer_of(ptx_handle *h, int which) {
+    switch (which) {
+    case PTX_BUF_GBUFFER: return &h->d_gbuf;
+    case PTX_BUF_RESERVOIR: return &h->d_res;
+    case PTX_BUF_ACCUM: return &h->d_accum;
+    case PTX_BUF_COUNTERS: return &h->d_counters;
+    default: return nullptr;
+    }
+}
+
+// ================================================================ exported C ABI
+extern "C" {
+
+int ptx_abi_version(void) { return PTX_ABI_VERSION; }
+
+int ptx_create(const ptx_config *cfg, ptx_handle **out) {
+    if (!cfg || !out) return PTX_E_INVALID;
+    *out = nullptr;
+    if (cfg->width == 0 || cfg->height == 0 || cfg->pipeline > PTX_PIPELINE_MCPT) return PTX_E_INVALID;
+    ptx_handle *h = new (std::nothrow) ptx_handle();
+    if (!h) return PTX_E_NOMEM;
+    h->cfg = *cfg;
+    if (h->cfg.row_begin == 0 && h->cfg.row_end == 0) h->cfg.row_end = h->cfg.height;
+    if (h->cfg.row_begin >= h->cfg.row_end || h->cfg.row_end > h->cfg.height) {
+        delete h;
+        return PTX_E_INVALID;
+    }
+    h->band_h = h->cfg.row_end - h->cfg.row_begin;
+    int rc = PTX_OK;
+    hipError_t e;
+    if (cfg->device >= 0) {
+        if ((e = hipSetDevice(cfg->device)) != hipSuccess) rc = PTX_E_HIP;
+    }
+    if (!rc && (e = hipGetDevice(&h->device)) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && (e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking)) != hipSuccess) rc = PTX_E_HIP;
+    for (int i = 0; !rc && i < kEventRing; ++i) {
+        if (hipEventCreate(&h->ring[i].start) != hipSuccess || hipEventCreate(&h->ring[i].stop) != hipSuccess)
+            rc = PTX_E_HIP;
+    }
+    h->stream = h->own_stream;
+    const size_t px = (size_t)h->band_h * h->cfg.width;
+    if (!rc) rc = alloc_buf(h, h->d_gbuf, px * 16u);
+    if (!rc) rc = alloc_buf(h, h->d_res, px * 128u);
+    if (!rc) rc = alloc_buf(h, h->d_accum, px * 16u);
+    if (!rc) rc = alloc_buf(h, h->d_counters, 64u);
+    if (!rc && hipMemset(h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && hipMemset(h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && hipMemset(h->d_gbuf.p, 0, h->d_gbuf.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && hipMemset(h->d_res.p, 0, h->d_res.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (rc) {
+        ptx_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return PTX_OK;
+}
+
+int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const uint32_t *geometry,
+                     size_t n_geometry, const uint32_t *accel, size_t n_accel) {
+    if (!h) return PTX_E_INVALID;
+    if (!scene || !geometry || (!accel && n_accel)) return fail(h, PTX_E_INVALID, "null scene array");
+    h->scene.assign(scene, scene + n_scene);
+    h->geometry.assign(geometry, geometry + n_geometry);
+    h->accel.assign(accel ? accel : scene, accel ? accel + n_accel : scene);
+    if (int rc = upload(h, h->d_scene, scene, n_scene * 4u)) return rc;
+    if (int rc = upload(h, h->d_geometry, geometry, n_geometry * 4u)) return rc;
+    h->layout_valid = false;
+    h->scene_loaded = true;
+    if (h->frame_set) return build_layout(h);
+    return PTX_OK;
+}
+
+int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]) {
+    if (!h || !uniform) return PTX_E_INVALID;
+    if (uniform[0] != h->cfg.width || uniform[1] != h->cfg.height)
+        return fail(h, PTX_E_INVALID, "uniform resolution %ux%u != handle %ux%u", uniform[0], uniform[1],
+                    h->cfg.width, h->cfg.height);
+    uint32_t key[8];
+    for (int k = 0; k < 8; ++k) key[k] = uniform[24 + k];
+    if (std::memcmp(key, h->layout_key, sizeof key) != 0) {
+        std::memcpy(h->layout_key, key, sizeof key);
+        h->layout_valid = false;
+    }
+    std::memcpy(h->uniform, uniform, sizeof h->uniform);
+    h->frame_set = true;
+    if (h->scene_loaded && !h->layout_valid) return build_layout(h);
+    return PTX_OK;
+}
+
+int ptx_run_pass(ptx_handle *h, int pass) {
+    if (!h) return PTX_E_INVALID;
+    return timed_launch(h, pass);
+}
+
+int ptx_render(ptx_handle *h, float *rgba_out) {
+    if (!h) return PTX_E_INVALID;
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR) {
+        for (int p : {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL})
+            if (int rc = timed_launch(h, p)) return rc;
+    } else {
+        if (int rc = timed_launch(h, PTX_PASS_MCPT)) return rc;
+    }
+    h->frames++;
+    if (rgba_out) {
+        HIP_CHECK(h, hipMemcpyAsync(rgba_out, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost, h->stream));
+        HIP_CHECK(h, hipStreamSynchronize(h->stream));
+    }
+    return PTX_OK;
+}
+
+int ptx_reset_accumulation(ptx_handle *h) {
+    if (!h) return PTX_E_INVALID;
+    HIP_CHECK(h, hipMemsetAsync(h->d_accum.p, 0, h->d_accum.bytes, h->stream));
+    return PTX_OK;
+}
+
+int ptx_synchronize(ptx_handle *h) {
+    if (!h) return PTX_E_INVALID;
+    HIP_CHECK(h, hipStreamSynchronize(h->stream));
+    return PTX_OK;
+}
+
+int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
+    if (!h || !out) return PTX_E_INVALID;
+    for (auto &t : h->ring) resolve_event(t, h);
+    std::memset(out, 0, sizeof *out);
+    out->frames = h->frames;
+    for (int p = 0; p < kPasses; ++p) {
+        out->kernel_ms_total[p] = h->ms_total[p];
+        out->kernel_launches[p] = h->launches[p];
+    }
+    out->triangles = h->n_tris;
+    out->bvh_nodes = h->n_nodes;
+    out->instances = h->n_inst;
+    out->max_bvh_depth = h->max_depth;
+    out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
+                        h->d_subs.bytes + h->d_insts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes;
+    return PTX_OK;
+}
+
+int ptx_reset_stats(ptx_handle *h) {
+    if (!h) return PTX_E_INVALID;
+    for (auto &t : h->ring) t.pending = false;
+    HIP_CHECK(h, hipStreamSynchronize(h->stream));
+    for (int p = 0; p < kPasses; ++p) { h->ms_total[p] = 0.0; h->launches[p] = 0; }
+    h->frames = 0;
+    HIP_CHECK(h, hipMemset(h->d_counters.p, 0, h->d_counters.bytes));
+    return PTX_OK;
+}
+
+int ptx_read_buffer(ptx_handle *h, int which, void *host_dst, size_t bytes) {
+    if (!h || !host_dst) return PTX_E_INVALID;
+    DevBuf *b = buffer_of(h, which);
+    if (!b || bytes > b->bytes) return fail(h, PTX_E_INVALID, "read of %zu bytes from buffer %d", bytes, which);
+    HIP_CHECK(h, hipStreamSynchronize(h->stream));
+    HIP_CHECK(h, hipMemcpy(host_dst, b->p, bytes, hipMemcpyDeviceToHost));
+    return PTX_OK;
+}
+
+int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t bytes) {
+    if (!h || !host_src) return PTX_E_INVALID;
+    DevBuf *b = buffer_of(h, which);
+    if (!b || bytes > b->bytes) return fail(h, PTX_E_INVALID, "write of %zu bytes to buffer %d", bytes, which);
+    HIP_CHECK(h, hipStreamSynchronize(h->stream));
+    HIP_CHECK(h, hipMemcpy(b->p, host_src, bytes, hipMemcpyHostToDevice));
+    return PTX_OK;
+}
+
+int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes) {
+    if (!h || !dev_ptr) return PTX_E_INVALID;
+    DevBuf *b = buffer_of(h, which);
+    if (!b) return fail(h, PTX_E_INVALID, "unknown buffer %d", which);
+    *dev_ptr = b->p;
+    if (bytes) *bytes = b->bytes;
+    return PTX_OK;
+}
+
+int ptx_set_stream(ptx_handle *h, void *hip_stream) {
+    if (!h) return PTX_E_INVALID;
+    h->stream = hip_stream ? (hipStream_t)hip_stream : h->own_stream;
+    return PTX_OK;
+}
+
+int ptx_destroy(ptx_handle *h) {
+    if (!h) return PTX_E_INVALID;
+    if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
+    for (auto &t : h->ring) {
+        if (t.start) (void)hipEventDestroy(t.start);
+        if (t.stop) (void)hipEventDestroy(t.stop);
+    }
+    for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_gbuf,
+                      &h->d_res, &h->d_accum, &h->d_counters})
+        free_buf(*b);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+    return PTX_OK;
+}
+
+const char *ptx_last_error(const ptx_handle *h) { return h ? h->err.c_str() : "null handle"; }
+
+}  // extern "C"

@@ -1,0 +1,299 @@
+// ptx_device.h -- device-side scene layout, f32 math and BVH traversal for gfx950.
+//
+// Semantics follow the reference WGSL (SH/ = apps/frontend/src/graphics-core/shaders/),
+// with every implementation-defined WGSL detail fixed as in DESIGN.md §Numerics and
+// compiled with -ffp-contract=off so that ray setup, slab tests, Moller-Trumbore and
+// barycentrics are bit-identical to the CPU oracle.
+//
+// MI355X layout (built once per scene by ptx_api.cpp from the reference arrays):
+//   * tris:  per triangle 3 x float4 = {v0.xyz, e1.x} {e1.yz, e2.xy} {e2.z, -, -, -}
+//            (local space, leaf order; e1 = v1 - v0, e2 = v2 - v0 exactly as
+//            GetRayTriangleHitDistance computes them, SH/PT_1_InitPass.wgsl:522-523)
+//   * nodes: one 64-byte record per interior BVH node holding BOTH children's boxes and
+//            refs, so a node visit is 4 x 16-byte loads instead of the reference's
+//            3 x 32-byte node fetches (GetBlasNode x3, SH/PT_1_InitPass.wgsl:633-642);
+//            the same binary tree, visited in the same order.
+//   * subs:  per (mesh, sub-mesh) root box + root ref.
+//   * insts: per instance M, M^-1, mesh, sub range, triangle base.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptx {
+
+// ------------------------------------------------------------------ constants
+// SH/PT_1_InitPass.wgsl:193-221
+constexpr uint32_t STRIDE_INSTANCE = 33u;
+constexpr uint32_t STRIDE_LIGHT = 18u;
+constexpr uint32_t STRIDE_DESCRIPTOR = 6u;
+constexpr uint32_t STRIDE_MATERIAL = 15u;
+constexpr uint32_t STRIDE_VERTEX = 8u;
+constexpr float RECONNECTION_DISTANCE = 0.1f;
+constexpr float RECONNECTION_ROUGHNESS = 0.5f;
+constexpr float INF_F = 1e11f;
+constexpr float EPS_F = 1e-4f;
+constexpr float PI_F = 3.141592f;
+constexpr float ENV_C = 0.5f;
+constexpr uint32_t LIGHT_DIRECTION = 0u, LIGHT_POINT = 1u, LIGHT_RECT = 2u, LIGHT_ENV = 3u;
+constexpr uint32_t LOBE_LAMBERT = 0u, LOBE_GGX = 1u, LOBE_LIGHT = 3u;
+
+enum : uint32_t {
+    U_W = 0, U_H = 1, U_VPINV = 4, U_CAMPOS = 20, U_FRAME = 23, U_OFF_DESC = 24, U_OFF_MAT = 25,
+    U_OFF_LIGHT = 26, U_OFF_CDF = 27, U_OFF_INDEX = 28, U_OFF_SUBROOT = 29, U_OFF_BLAS = 30,
+    U_INST_COUNT = 31, U_LIGHT_COUNT = 32
+};
+
+// child / stack reference encoding: interior node index, or LEAF_BIT | count<<24 | first tri
+constexpr uint32_t LEAF_BIT = 0x80000000u;
+constexpr uint32_t LEAF_FIRST_MASK = 0x00FFFFFFu;
+
+struct alignas(16) NodePair {   // 64 B
+    float lmin[3], lmax[3], rmin[3], rmax[3];
+    uint32_t lref, rref, pad0, pad1;
+};
+struct alignas(16) SubRoot {    // 32 B
+    float bmin[3], bmax[3];
+    uint32_t ref, pad;
+};
+struct alignas(16) Inst {       // 144 B
+    float m[16];
+    float minv[16];
+    uint32_t mesh, sub_base, nsub, tri_base;
+};
+
+// Everything a kernel reads, passed by value (lives in the kernarg segment).
+struct Scene {
+    uint32_t U[33];       // uniform block (33 words), by value: race-free per-frame update
+    const uint32_t *S;    // SceneBuffer
+    const uint32_t *G;    // GeometryBuffer
+    const float4 *tris;   // 3 float4 per triangle
+    const NodePair *nodes;
+    const SubRoot *subs;
+    const Inst *insts;
+    uint32_t n_inst;
+    uint32_t width, height, row_begin, row_end;
+    unsigned long long *counters;  // nullptr unless PTX_FLAG_COUNT_WORK
+};
+
+// ------------------------------------------------------------------ f32 vector algebra
+// Operation order is fixed (left-to-right sums, no contraction): DESIGN.md §Numerics.
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return f3{a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ float length(f3 a) { return __builtin_sqrtf(dot(a, a)); }
+__device__ __forceinline__ f3 normalize(f3 a) { return a / length(a); }
+__device__ __forceinline__ float length3(f3 a) { return length(a); }
+__device__ __forceinline__ float mixf(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+__device__ __forceinline__ f3 mix3(f3 a, f3 b, float t) { return f3{mixf(a.x, b.x, t), mixf(a.y, b.y, t), mixf(a.z, b.z, t)}; }
+__device__ __forceinline__ float saturate(float a) { return fminf(fmaxf(a, 0.0f), 1.0f); }
+__device__ __forceinline__ float luminance(f3 c) { return c.x * 0.2126f + c.y * 0.7152f + c.z * 0.0722f; }
+__device__ __forceinline__ float asf(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ uint32_t asu(float f) { return __float_as_uint(f); }
+
+// column-major mat4 * (p,1) then /w (TransformVec3WithMat4x4, SH/PT_1_InitPass.wgsl:480-484)
+__device__ __forceinline__ f3 xform_point(const float *m, f3 p) {
+    float x = ((m[0] * p.x + m[4] * p.y) + m[8] * p.z) + m[12] * 1.0f;
+    float y = ((m[1] * p.x + m[5] * p.y) + m[9] * p.z) + m[13] * 1.0f;
+    float z = ((m[2] * p.x + m[6] * p.y) + m[10] * p.z) + m[14] * 1.0f;
+    float w = ((m[3] * p.x + m[7] * p.y) + m[11] * p.z) + m[15] * 1.0f;
+    return f3{x / w, y / w, z / w};
+}
+// transpose(m) * (p,1) then /w (normal transform, SH/PT_1_InitPass.wgsl:395)
+__device__ __forceinline__ f3 xform_point_t(const float *m, f3 p) {
+    float x = ((m[0] * p.x + m[1] * p.y) + m[2] * p.z) + m[3] * 1.0f;
+    float y = ((m[4] * p.x + m[5] * p.y) + m[6] * p.z) + m[7] * 1.0f;
+    float z = ((m[8] * p.x + m[9] * p.y) + m[10] * p.z) + m[11] * 1.0f;
+    float w = ((m[12] * p.x + m[13] * p.y) + m[14] * p.z) + m[15] * 1.0f;
+    return f3{x / w, y / w, z / w};
+}
+
+// ------------------------------------------------------------------ RNG, SH/PT_1_InitPass.wgsl:810-826
+__device__ __forceinline__ uint32_t pcg(uint32_t seed) {
+    uint32_t state = seed * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+__device__ __forceinline__ float rnd(uint32_t &seed) {
+    uint32_t h = pcg(seed);
+    seed += 1u;
+    return (float)h / 4294967295.0f;
+}
+
+// ------------------------------------------------------------------ counters
+enum { CNT_RAYS = 0, CNT_INST = 1, CNT_AABB = 2, CNT_TRI = 3, CNT_HITS = 4 };
+
+// ------------------------------------------------------------------ ray / hit
+struct Ray { f3 o, d; };
+struct Compact { uint32_t valid, inst, mat, prim; float bu, bv; };
+struct Hit { bool valid; float t; Compact s; };
+
+struct PassEps { float det_eps, bary_eps; };
+
+// GetRayAABBIntersectionRange + DoRangesOverlap(RayValidRange, .) (SH/PT_1_InitPass.wgsl:475-514)
+// with InvDirection hoisted (it is the same 1/dir for every test of the ray).
+__device__ __forceinline__ bool box_overlap(f3 o, f3 inv, const float *bmin, const float *bmax, float vx,
+                                            float vy, float &tnear) {
+    float t1x = (bmin[0] - o.x) * inv.x, t1y = (bmin[1] - o.y) * inv.y, t1z = (bmin[2] - o.z) * inv.z;
+    float t2x = (bmax[0] - o.x) * inv.x, t2y = (bmax[1] - o.y) * inv.y, t2z = (bmax[2] - o.z) * inv.z;
+    float tmin = fmaxf(fminf(t1x, t2x), fmaxf(fminf(t1y, t2y), fminf(t1z, t2z)));
+    float tmax = fminf(fmaxf(t1x, t2x), fminf(fmaxf(t1y, t2y), fmaxf(t1z, t2z)));
+    if (tmin > tmax) { tmin = 1.0f; tmax = 0.0f; }
+    tnear = tmin;
+    return (vx <= tmax) && (tmin <= vy);
+}
+
+// GetRayTriangleHitDistance (SH/PT_1_InitPass.wgsl:516-547) on the precomputed edges.
+__device__ __forceinline__ float ray_tri(f3 o, f3 d, float4 a, float4 b, float4 c, float det_eps) {
+    f3 p0 = mk(a.x, a.y, a.z);
+    f3 e1 = mk(a.w, b.x, b.y);
+    f3 e2 = mk(b.z, b.w, c.x);
+    f3 pvec = cross(d, e2);
+    float det = dot(e1, pvec);
+    if (fabsf(det) < det_eps) return 1e11f;
+    float inv_det = 1.0f / det;
+    f3 tvec = o - p0;
+    float u = dot(tvec, pvec) * inv_det;
+    if (u < 0.0f || u > 1.0f) return 1e11f;
+    f3 qvec = cross(tvec, e1);
+    float v = dot(d, qvec) * inv_det;
+    if (v < 0.0f || (u + v) > 1.0f) return 1e11f;
+    float t = dot(e2, qvec) * inv_det;
+    if (t <= 1e-4f) return 1e11f;
+    return t;
+}
+
+// Reference-layout accessors (cold paths: hit reconstruction and shading).
+__device__ __forceinline__ const uint32_t *desc_ptr(const Scene &sc, uint32_t mesh) {
+    return sc.S + sc.U[U_OFF_DESC] + STRIDE_DESCRIPTOR * mesh;
+}
+__device__ __forceinline__ void tri_vertex_ids(const Scene &sc, const uint32_t *desc, uint32_t prim, uint32_t id[3]) {
+    const uint32_t *p = sc.G + sc.U[U_OFF_INDEX] + desc[1] + 3u * prim;
+    id[0] = p[0]; id[1] = p[1]; id[2] = p[2];
+}
+__device__ __forceinline__ f3 vtx_pos(const Scene &sc, const uint32_t *desc, uint32_t vid) {
+    const uint32_t *p = sc.G + desc[0] + STRIDE_VERTEX * vid;
+    return mk(asf(p[0]), asf(p[1]), asf(p[2]));
+}
+__device__ __forceinline__ f3 vtx_nrm(const Scene &sc, const uint32_t *desc, uint32_t vid) {
+    const uint32_t *p = sc.G + desc[0] + STRIDE_VERTEX * vid;
+    return mk(asf(p[3]), asf(p[4]), asf(p[5]));
+}
+
+// GetBaryCentricWeights (SH/PT_1_InitPass.wgsl:549-575): returns (w,u) = bary.xy
+__device__ __forceinline__ void barycentric(f3 P, f3 A, f3 B, f3 C, float eps, float &bx, float &by) {
+    f3 v0 = B - A, v1 = C - A, v2 = P - A;
+    float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1);
+    float d20 = dot(v2, v0), d21 = dot(v2, v1);
+    float denom = d00 * d11 - d01 * d01;
+    if (fabsf(denom) < eps) { bx = 1.0f; by = 0.0f; return; }
+    float inv = 1.0f / denom;
+    float u = (d11 * d20 - d01 * d21) * inv;
+    float v = (d00 * d21 - d01 * d20) * inv;
+    bx = 1.0f - u - v;
+    by = u;
+}
+
+// TraceRay (SH/PT_1_InitPass.wgsl:605-715; PT_01:509-621): closest hit over every
+// instance and sub-mesh root, ordered-stack BLAS traversal, ties replace (`if (best < t)
+// continue`).  `stack` is this thread's column of the workgroup's LDS stack
+// (entry k at stack[k * stride]).
+__device__ __attribute__((noinline)) Hit trace_ray(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack,
+                                                  uint32_t stride) {
+    Hit best;
+    best.valid = false;
+    best.t = 0.0f;
+    best.s = Compact{0u, 0u, 0u, 0u, 0.0f, 0.0f};
+    const float vx = 1e-4f;
+    float vy = 1e10f;
+    uint32_t n_aabb = 0, n_tri = 0;
+    for (uint32_t ii = 0; ii < sc.n_inst; ++ii) {
+        const Inst &I = sc.insts[ii];
+        // TransformRayWithMat4x4(InRay, M^-1, false), SH/PT_1_InitPass.wgsl:486-496
+        f3 lo = xform_point(I.minv, ray.o);
+        f3 le = xform_point(I.minv, ray.o + ray.d);
+        f3 ld = le - lo;
+        f3 inv = mk(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
+        const uint32_t nsub = I.nsub;
+        for (uint32_t s = 0; s < nsub; ++s) {
+            const SubRoot &R = sc.subs[I.sub_base + s];
+            float tn;
+            ++n_aabb;
+            if (!box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) continue;
+            int sp = 0;
+            stack[0] = R.ref;
+            while (sp >= 0) {
+                uint32_t ref = stack[(uint32_t)sp * stride];
+                --sp;
+                if (!(ref & LEAF_BIT)) {
+                    const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + ref);
+                    float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+                    float lmin[3] = {q0.x, q0.y, q0.z}, lmax[3] = {q0.w, q1.x, q1.y};
+                    float rmin[3] = {q1.z, q1.w, q2.x}, rmax[3] = {q2.y, q2.z, q2.w};
+                    uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
+                    float tl, tr;
+                    bool hl = box_overlap(lo, inv, lmin, lmax, vx, vy, tl);
+                    bool hr = box_overlap(lo, inv, rmin, rmax, vx, vy, tr);
+                    n_aabb += 2;
+                    if (hl && hr) {
+                        uint32_t first = tl < tr ? rref : lref;
+                        uint32_t second = tl < tr ? lref : rref;
+                        stack[(uint32_t)(sp + 1) * stride] = first;
+                        stack[(uint32_t)(sp + 2) * stride] = second;
+                        sp += 2;
+                    } else if (hl || hr) {
+                        stack[(uint32_t)(sp + 1) * stride] = hl ? lref : rref;
+                        sp += 1;
+                    }
+                    continue;
+                }
+                const uint32_t first = ref & LEAF_FIRST_MASK;
+                const uint32_t count = (ref >> 24) & 0x7Fu;
+                const float4 *tp = sc.tris + 3u * (I.tri_base + first);
+                for (uint32_t k = 0; k < count; ++k) {
+                    float4 a = tp[3u * k + 0u], b = tp[3u * k + 1u], c = tp[3u * k + 2u];
+                    float t = ray_tri(lo, ld, a, b, c, eps.det_eps);
+                    ++n_tri;
+                    if (vy < t) continue;
+                    vy = t;
+                    best.valid = true;
+                    best.s.inst = ii;
+                    best.s.mat = s;
+                    best.s.prim = first + k;
+                }
+            }
+        }
+    }
+    if (sc.counters) {
+        atomicAdd(&sc.counters[CNT_RAYS], 1ull);
+        atomicAdd(&sc.counters[CNT_INST], (unsigned long long)sc.n_inst);
+        atomicAdd(&sc.counters[CNT_AABB], (unsigned long long)n_aabb);
+        atomicAdd(&sc.counters[CNT_TRI], (unsigned long long)n_tri);
+        if (best.valid) atomicAdd(&sc.counters[CNT_HITS], 1ull);
+    }
+    if (best.valid) {
+        best.t = vy;
+        best.s.valid = 1u;
+        const Inst &I = sc.insts[best.s.inst];
+        const uint32_t *desc = desc_ptr(sc, I.mesh);
+        uint32_t id[3];
+        tri_vertex_ids(sc, desc, best.s.prim, id);
+        f3 A = xform_point(I.m, vtx_pos(sc, desc, id[0]));
+        f3 B = xform_point(I.m, vtx_pos(sc, desc, id[1]));
+        f3 C = xform_point(I.m, vtx_pos(sc, desc, id[2]));
+        f3 P = ray.o + ray.d * best.t;
+        barycentric(P, A, B, C, eps.bary_eps, best.s.bu, best.s.bv);
+    }
+    return best;
+}
+
+}  // namespace ptx

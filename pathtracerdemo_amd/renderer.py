@@ -1,0 +1,139 @@
+"""Host-side mirror of the reference renderer class over the HIP C ABI.
+
+Same surface and semantics as ``Renderer`` of apps/frontend/src/graphics-core/
+Renderer_TEST.ts (constructor :83-126, GetCamera :129-132, ResetFrameCount :134-137,
+Initialize :141-163, Update :165-206, Render :208-261), with the WebGPU device replaced
+by libptx.so on one MI355X.  ``pipeline="mcpt"`` mirrors the legacy Renderer.ts
+(TEST_MCPT.wgsl brute force, GC/Renderer.ts:536-647).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .scene.camera import Camera
+from .scene.world import CompiledScene, World, serialize_world
+
+
+class Renderer:
+    def __init__(self, width: int, height: int, device: int = -1, pipeline: str = "restir",
+                 row_begin: int = 0, row_end: int = 0, count_work: bool = False):
+        self._lib = N.load()
+        self.width, self.height = int(width), int(height)
+        self.pipeline = pipeline
+        cfg = N.PtxConfig(width=self.width, height=self.height, row_begin=row_begin, row_end=row_end,
+                          device=device,
+                          pipeline=N.PTX_PIPELINE_MCPT if pipeline == "mcpt" else N.PTX_PIPELINE_RESTIR,
+                          flags=N.PTX_FLAG_COUNT_WORK if count_work else 0)
+        self._h = ctypes.c_void_p()
+        rc = self._lib.ptx_create(ctypes.byref(cfg), ctypes.byref(self._h))
+        if rc != N.PTX_OK:
+            raise N.PtxError(f"ptx_create failed ({rc})")
+        self.row_begin = row_begin
+        self.row_end = row_end or self.height
+        self.compiled: CompiledScene | None = None
+        self.camera: Camera | None = None
+        self.frame_count = 0
+        self.uniform = None
+
+    # ------------------------------------------------------------------ reference surface
+    def GetCamera(self) -> Camera:
+        return self.camera
+
+    def ResetFrameCount(self) -> None:
+        self.frame_count = 0
+
+    def Initialize(self, world: World | CompiledScene) -> None:
+        """Renderer_TEST.Initialize: camera at (0,0,6), yaw/pitch 0, FrameCount 0, upload."""
+        self.camera = Camera(self.width, self.height)
+        self.camera.set_location(0, 0, 6)
+        self.camera.set_yaw(0)
+        self.camera.set_pitch(0)
+        self.ResetFrameCount()
+        self.compiled = world if isinstance(world, CompiledScene) else serialize_world(world)
+        cs = self.compiled
+        self._call("ptx_upload_scene", self._h, cs.scene.ctypes.data, len(cs.scene), cs.geometry.ctypes.data,
+                   len(cs.geometry), cs.accel.ctypes.data if len(cs.accel) else None, len(cs.accel))
+        self._call("ptx_reset_accumulation", self._h)
+
+    def Update(self) -> None:
+        """Renderer_TEST.Update: FrameCount++ and the 33-word uniform block."""
+        self.frame_count += 1
+        u = self.compiled.uniform(self.width, self.height, self.camera.view_projection_inverse(),
+                                  self.camera.location, self.frame_count)
+        self.set_uniform(u)
+
+    def Render(self) -> None:
+        """Renderer_TEST.Render: the configured passes, accumulated into the Scene texture."""
+        self._call("ptx_render", self._h, None)
+
+    # ------------------------------------------------------------------ extras
+    def set_uniform(self, u: np.ndarray) -> None:
+        self.uniform = np.ascontiguousarray(u, dtype=np.uint32)
+        self._call("ptx_set_frame", self._h, self.uniform.ctypes.data)
+
+    def run_pass(self, pass_id: int) -> None:
+        self._call("ptx_run_pass", self._h, pass_id)
+
+    def synchronize(self) -> None:
+        self._call("ptx_synchronize", self._h)
+
+    def reset_accumulation(self) -> None:
+        self._call("ptx_reset_accumulation", self._h)
+
+    @property
+    def band_rows(self) -> int:
+        return self.row_end - self.row_begin
+
+    def _read(self, which: int, dtype, comps: int) -> np.ndarray:
+        out = np.zeros((self.band_rows, self.width, comps), dtype=dtype)
+        self._call("ptx_read_buffer", self._h, which, out.ctypes.data, out.nbytes)
+        return out
+
+    def read_image(self) -> np.ndarray:
+        return self._read(N.PTX_BUF_ACCUM, np.float32, 4)
+
+    def read_gbuffer(self) -> np.ndarray:
+        return self._read(N.PTX_BUF_GBUFFER, np.uint32, 4)
+
+    def read_reservoir(self) -> np.ndarray:
+        return self._read(N.PTX_BUF_RESERVOIR, np.uint32, 32)
+
+    def write_buffer(self, which: int, arr: np.ndarray) -> None:
+        arr = np.ascontiguousarray(arr)
+        self._call("ptx_write_buffer", self._h, which, arr.ctypes.data, arr.nbytes)
+
+    def read_counters(self) -> dict:
+        c = np.zeros(8, dtype=np.uint64)
+        self._call("ptx_read_buffer", self._h, N.PTX_BUF_COUNTERS, c.ctypes.data, c.nbytes)
+        return {"rays": int(c[0]), "instance_xforms": int(c[1]), "aabb_tests": int(c[2]), "tri_tests": int(c[3]),
+                "hits": int(c[4])}
+
+    def stats(self) -> dict:
+        s = N.PtxStats()
+        self._call("ptx_get_stats", self._h, ctypes.byref(s))
+        return {"frames": s.frames, "kernel_ms_total": list(s.kernel_ms_total),
+                "kernel_launches": list(s.kernel_launches), "triangles": s.triangles, "bvh_nodes": s.bvh_nodes,
+                "instances": s.instances, "max_bvh_depth": s.max_bvh_depth, "device_bytes": s.device_bytes}
+
+    def reset_stats(self) -> None:
+        self._call("ptx_reset_stats", self._h)
+
+    def set_stream(self, stream_ptr: int | None) -> None:
+        self._call("ptx_set_stream", self._h, stream_ptr)
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.ptx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _call(self, name: str, *args):
+        N.check(self._lib, self._h, getattr(self._lib, name)(*args), name)
