@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--scene", default="dummy_scene_1")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--simple", action="store_true", help="one-thread-per-pixel kernels (A/B baseline)")
     return ap.parse_args()
 
 
@@ -71,7 +72,8 @@ def main():
     cs = compile_scene(args.scene)
     row_begin, row_end = rank * Hb, (rank + 1) * Hb
     pipeline = args.workload
-    r = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end)
+    r = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
+                 simple=args.simple)
     r.Initialize(cs)
 
     # work census of the exact frame (counting build, untimed): algorithmic bytes

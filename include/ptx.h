@@ -60,7 +60,8 @@ extern "C" {
 #define PTX_BUF_ACCUM 2      /* band_h * W * 4 f32 (Scene texture: accumulated radiance) */
 #define PTX_BUF_COUNTERS 3   /* 8 u64 work counters (PTX_FLAG_COUNT builds) */
 
-#define PTX_FLAG_COUNT_WORK 1u  /* count rays / AABB / triangle tests on device (slower) */
+#define PTX_FLAG_COUNT_WORK 1u     /* count rays / AABB / triangle tests on device (slower)   */
+#define PTX_FLAG_SIMPLE_KERNELS 2u /* one-thread-per-pixel kernels instead of persistent lanes */
 
 typedef struct ptx_config {
     uint32_t width, height;       /* full image size (uniform words 0,1 must match) */

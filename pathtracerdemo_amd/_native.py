@@ -16,6 +16,7 @@ PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT = 0, 1
 PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT = 0, 1, 2, 3
 PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS = 0, 1, 2, 3
 PTX_FLAG_COUNT_WORK = 1
+PTX_FLAG_SIMPLE_KERNELS = 2
 
 # every symbol include/ptx.h declares (checked by tests/test_abi.py)
 EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame", "ptx_render", "ptx_run_pass",

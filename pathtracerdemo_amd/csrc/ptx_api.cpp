@@ -59,7 +59,7 @@ struct ptx_handle {
     bool frame_set = false;
     // band buffers
     uint32_t band_h = 0;
-    DevBuf d_gbuf, d_res, d_accum, d_counters;
+    DevBuf d_gbuf, d_res, d_accum, d_counters, d_queue;
     // stats
     TimedLaunch ring[kEventRing];
     int ring_pos = 0;
@@ -283,18 +283,28 @@ static int timed_launch(ptx_handle *h, int pass) {
     h->ring_pos = (h->ring_pos + 1) % kEventRing;
     resolve_event(t, h);
     Scene sc = make_scene(h);
+    const bool simple = (h->cfg.flags & PTX_FLAG_SIMPLE_KERNELS) != 0;
+    unsigned int *ctr = (unsigned int *)h->d_queue.p + pass;
+    if (!simple && pass != PTX_PASS_GBUFFER) HIP_CHECK(h, hipMemsetAsync(ctr, 0, sizeof(unsigned int), h->stream));
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
     hipError_t e = hipSuccess;
+    const uint4 *gb = (const uint4 *)h->d_gbuf.p;
     switch (pass) {
     case PTX_PASS_GBUFFER: e = launch_gbuffer(sc, (uint4 *)h->d_gbuf.p, h->stack_depth, h->stream); break;
     case PTX_PASS_INIT:
-        e = launch_init(sc, (const uint4 *)h->d_gbuf.p, (uint4 *)h->d_res.p, h->stack_depth, h->stream);
+        e = simple ? launch_init(sc, gb, (uint4 *)h->d_res.p, h->stack_depth, h->stream)
+                   : launch_init_persistent(sc, gb, (uint4 *)h->d_res.p, ctr, h->stack_depth, h->stream);
         break;
     case PTX_PASS_FINAL:
-        e = launch_final(sc, (const uint4 *)h->d_gbuf.p, (const uint4 *)h->d_res.p, (float4 *)h->d_accum.p,
-                         h->stack_depth, h->stream);
+        e = simple ? launch_final(sc, gb, (const uint4 *)h->d_res.p, (float4 *)h->d_accum.p, h->stack_depth,
+                                  h->stream)
+                   : launch_final_persistent(sc, gb, (const uint4 *)h->d_res.p, (float4 *)h->d_accum.p, ctr,
+                                             h->stack_depth, h->stream);
         break;
-    case PTX_PASS_MCPT: e = launch_mcpt(sc, (float4 *)h->d_accum.p, h->stack_depth, h->stream); break;
+    case PTX_PASS_MCPT:
+        e = simple ? launch_mcpt(sc, (float4 *)h->d_accum.p, h->stack_depth, h->stream)
+                   : launch_mcpt_persistent(sc, (float4 *)h->d_accum.p, ctr, h->stack_depth, h->stream);
+        break;
     default: return fail(h, PTX_E_INVALID, "unknown pass %d", pass);
     }
     if (e != hipSuccess) return fail(h, PTX_E_HIP, "kernel launch (pass %d): %s", pass, hipGetErrorString(e));
@@ -349,6 +359,7 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!rc) rc = alloc_buf(h, h->d_res, px * 128u);
     if (!rc) rc = alloc_buf(h, h->d_accum, px * 16u);
     if (!rc) rc = alloc_buf(h, h->d_counters, 64u);
+    if (!rc) rc = alloc_buf(h, h->d_queue, 64u);
     if (!rc && hipMemset(h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (!rc && hipMemset(h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (!rc && hipMemset(h->d_gbuf.p, 0, h->d_gbuf.bytes) != hipSuccess) rc = PTX_E_HIP;
@@ -495,7 +506,7 @@ int ptx_destroy(ptx_handle *h) {
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
     for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_gbuf,
-                      &h->d_res, &h->d_accum, &h->d_counters})
+                      &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue})
         free_buf(*b);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;

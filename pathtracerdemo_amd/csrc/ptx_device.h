@@ -100,13 +100,21 @@ __device__ __forceinline__ float luminance(f3 c) { return c.x * 0.2126f + c.y * 
 __device__ __forceinline__ float asf(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t asu(float f) { return __float_as_uint(f); }
 
+// The perspective divide of TransformVec3WithMat4x4.  For affine matrices and finite
+// points w is exactly 1.0 and x / 1.0f == x bit for bit (IEEE), so the ~10-instruction
+// correctly rounded division is skipped; any other w (projective VP^-1, NaN/inf inputs)
+// takes the division, so results are identical to dividing unconditionally.
+__device__ __forceinline__ f3 wdivide(float x, float y, float z, float w) {
+    if (w == 1.0f) return f3{x, y, z};
+    return f3{x / w, y / w, z / w};
+}
 // column-major mat4 * (p,1) then /w (TransformVec3WithMat4x4, SH/PT_1_InitPass.wgsl:480-484)
 __device__ __forceinline__ f3 xform_point(const float *m, f3 p) {
     float x = ((m[0] * p.x + m[4] * p.y) + m[8] * p.z) + m[12] * 1.0f;
     float y = ((m[1] * p.x + m[5] * p.y) + m[9] * p.z) + m[13] * 1.0f;
     float z = ((m[2] * p.x + m[6] * p.y) + m[10] * p.z) + m[14] * 1.0f;
     float w = ((m[3] * p.x + m[7] * p.y) + m[11] * p.z) + m[15] * 1.0f;
-    return f3{x / w, y / w, z / w};
+    return wdivide(x, y, z, w);
 }
 // transpose(m) * (p,1) then /w (normal transform, SH/PT_1_InitPass.wgsl:395)
 __device__ __forceinline__ f3 xform_point_t(const float *m, f3 p) {
@@ -114,7 +122,7 @@ __device__ __forceinline__ f3 xform_point_t(const float *m, f3 p) {
     float y = ((m[4] * p.x + m[5] * p.y) + m[6] * p.z) + m[7] * 1.0f;
     float z = ((m[8] * p.x + m[9] * p.y) + m[10] * p.z) + m[11] * 1.0f;
     float w = ((m[12] * p.x + m[13] * p.y) + m[14] * p.z) + m[15] * 1.0f;
-    return f3{x / w, y / w, z / w};
+    return wdivide(x, y, z, w);
 }
 
 // ------------------------------------------------------------------ RNG, SH/PT_1_InitPass.wgsl:810-826
@@ -135,7 +143,7 @@ enum { CNT_RAYS = 0, CNT_INST = 1, CNT_AABB = 2, CNT_TRI = 3, CNT_HITS = 4 };
 // ------------------------------------------------------------------ ray / hit
 struct Ray { f3 o, d; };
 struct Compact { uint32_t valid, inst, mat, prim; float bu, bv; };
-struct Hit { bool valid; float t; Compact s; };
+struct Hit { bool valid; float t; Compact s; f3 pos; };
 
 struct PassEps { float det_eps, bary_eps; };
 
@@ -206,13 +214,15 @@ __device__ __forceinline__ void barycentric(f3 P, f3 A, f3 B, f3 C, float eps, f
 // TraceRay (SH/PT_1_InitPass.wgsl:605-715; PT_01:509-621): closest hit over every
 // instance and sub-mesh root, ordered-stack BLAS traversal, ties replace (`if (best < t)
 // continue`).  `stack` is this thread's column of the workgroup's LDS stack
-// (entry k at stack[k * stride]).
-__device__ __attribute__((noinline)) Hit trace_ray(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack,
-                                                  uint32_t stride) {
+// (entry k at stack[k * stride]).  Also returns the hit position exactly as
+// GetSurface(hit).Position computes it (same world-space vertices and barycentrics).
+template <bool COUNT>
+__device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack, uint32_t stride) {
     Hit best;
     best.valid = false;
     best.t = 0.0f;
     best.s = Compact{0u, 0u, 0u, 0u, 0.0f, 0.0f};
+    best.pos = mk(0.0f, 0.0f, 0.0f);
     const float vx = 1e-4f;
     float vy = 1e10f;
     uint32_t n_aabb = 0, n_tri = 0;
@@ -273,7 +283,7 @@ __device__ __attribute__((noinline)) Hit trace_ray(const Scene &sc, Ray ray, Pas
             }
         }
     }
-    if (sc.counters) {
+    if (COUNT) {
         atomicAdd(&sc.counters[CNT_RAYS], 1ull);
         atomicAdd(&sc.counters[CNT_INST], (unsigned long long)sc.n_inst);
         atomicAdd(&sc.counters[CNT_AABB], (unsigned long long)n_aabb);
@@ -292,8 +302,15 @@ __device__ __attribute__((noinline)) Hit trace_ray(const Scene &sc, Ray ray, Pas
         f3 C = xform_point(I.m, vtx_pos(sc, desc, id[2]));
         f3 P = ray.o + ray.d * best.t;
         barycentric(P, A, B, C, eps.bary_eps, best.s.bu, best.s.bv);
+        const float U = best.s.bu, V = best.s.bv, W = 1.0f - U - V;
+        best.pos = (A * U + B * V) + C * W;
     }
     return best;
+}
+template <bool COUNT>
+__device__ __attribute__((noinline)) Hit trace_ray(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack,
+                                                  uint32_t stride) {
+    return trace_core<COUNT>(sc, ray, eps, stack, stride);
 }
 
 }  // namespace ptx

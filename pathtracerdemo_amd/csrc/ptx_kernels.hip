@@ -70,11 +70,12 @@ __device__ __forceinline__ void write_color(const Scene &sc, float4 *accum, size
 }
 
 // =========================================================================== PT_01
+template <bool COUNT>
 __global__ __launch_bounds__(BLOCK) void gbuffer_kernel(Scene sc, uint4 *gbuf) {
     uint32_t x, y;
     if (!pixel_of(sc, x, y)) return;
     uint32_t *stack = lds_stack + threadIdx.x;
-    Hit h = trace_ray(sc, camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);
+    Hit h = trace_ray<COUNT>(sc, camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);
     Compact s = h.s;
     s.valid = h.valid ? 1u : 0u;
     gbuf[band_index(sc, x, y)] = encode(s);
@@ -137,6 +138,7 @@ __device__ void store_reservoir(uint4 *out, const Chain &ch, int sel_i, bool sel
     for (int q = 0; q < 8; ++q) out[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
+template <bool COUNT>
 __global__ __launch_bounds__(BLOCK) void init_kernel(Scene sc, const uint4 *gbuf, uint4 *reservoir) {
     uint32_t x, y;
     if (!pixel_of(sc, x, y)) return;
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(Scene sc, const uint4 *gbuf
         f3 contrib = f * l_emit<false>(XL, X);
         contrib = contrib * bsdf(X, V, L);
         contrib = contrib * fabsf(dot(X.nrm, L));
-        contrib = contrib * visibility(sc, X.pos, XL.pos, eps, stack, BLOCK);
+        contrib = contrib * visibility<COUNT>(sc, X.pos, XL.pos, eps, stack, BLOCK);
         float p_hat = luminance(contrib);
         float ris = p_hat / (p * XL.pdf);
         C += 1u;  // UpdateReservoir (SH/PT_1_InitPass.wgsl:1298-1320)
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(Scene sc, const uint4 *gbuf
         float p_survive = luminance(f) / p;
         if (rnd(seed) < p_survive) p *= p_survive;
         else break;
-        Hit h = trace_ray(sc, Ray{X.pos, L}, eps, stack, BLOCK);
+        Hit h = trace_ray<COUNT>(sc, Ray{X.pos, L}, eps, stack, BLOCK);
         if (!h.valid) {  // Submit env path (SH/PT_1_InitPass.wgsl:1447-1461)
             LightSample env;
             env.pos = X.pos + L * INF_F;
@@ -224,6 +226,7 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(Scene sc, const uint4 *gbuf
 }
 
 // =========================================================================== PT_4
+template <bool COUNT>
 __global__ __launch_bounds__(BLOCK) void final_kernel(Scene sc, const uint4 *gbuf, const uint4 *reservoir,
                                                       float4 *accum) {
     uint32_t x, y;
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(BLOCK) void final_kernel(Scene sc, const uint4 *gbu
         uint32_t seed = seeds[i - 1u];
         uint32_t lobe;
         f3 dir = sample_bsdf(seed, cur, V, lobe);
-        Hit h = trace_ray(sc, Ray{cur.pos, dir}, eps, stack, BLOCK);
+        Hit h = trace_ray<COUNT>(sc, Ray{cur.pos, dir}, eps, stack, BLOCK);
         Surface next = get_surface(sc, h.s);  // a miss decodes the zero CompactSurface (WGSL behaviour)
         f3 L = normalize(next.pos - cur.pos);
         f = f * (bsdf(cur, L, V) * fabsf(dot(cur.nrm, L)));
@@ -265,11 +268,12 @@ __global__ __launch_bounds__(BLOCK) void final_kernel(Scene sc, const uint4 *gbu
     f3 V = normalize(prev - cur.pos);
     f3 L = direction_to_light(cur, XL);
     f = f * (bsdf(cur, L, V) * fabsf(dot(cur.nrm, L)));
-    f = f * (l_emit<true>(XL, cur) * visibility(sc, cur.pos, XL.pos, eps, stack, BLOCK));
+    f = f * (l_emit<true>(XL, cur) * visibility<COUNT>(sc, cur.pos, XL.pos, eps, stack, BLOCK));
     write_color(sc, accum, pi, f * asf(r7.x));
 }
 
 // =========================================================================== TEST_MCPT
+template <bool COUNT>
 __global__ __launch_bounds__(BLOCK) void mcpt_kernel(Scene sc, float4 *accum) {
     uint32_t x, y;
     if (!pixel_of(sc, x, y)) return;
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(BLOCK) void mcpt_kernel(Scene sc, float4 *accum) {
     float p = 1.0f;
     const uint32_t nl = sc.U[U_LIGHT_COUNT];
     for (int bounce = 0; bounce < 3; ++bounce) {
-        Hit h = trace_ray(sc, r, eps, stack, BLOCK);
+        Hit h = trace_ray<COUNT>(sc, r, eps, stack, BLOCK);
         if (!h.valid) { color = color + (f / p) * ENV_C; break; }
         Surface X = get_surface(sc, h.s);
         f3 V = normalize(r.o - X.pos);
@@ -310,7 +314,7 @@ __global__ __launch_bounds__(BLOCK) void mcpt_kernel(Scene sc, float4 *accum) {
             f3 L = direction_to_light(X, XL);
             f3 c = l_emit<false>(XL, X) * bsdf(X, V, L);
             c = c * fabsf(dot(X.nrm, L));
-            c = c * visibility(sc, X.pos, XL.pos, eps, stack, BLOCK);
+            c = c * visibility<COUNT>(sc, X.pos, XL.pos, eps, stack, BLOCK);
             color = color + (f / p) * (c / XL.pdf);
         }
         uint32_t lobe;
@@ -330,21 +334,25 @@ static dim3 grid_of(const Scene &sc) {
     return dim3((sc.width + TILE - 1) / TILE, (sc.row_end - sc.row_begin + TILE - 1) / TILE, 1);
 }
 hipError_t launch_gbuffer(const Scene &sc, uint4 *gbuf, uint32_t depth, hipStream_t s) {
-    hipLaunchKernelGGL(gbuffer_kernel, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
+    if (sc.counters) hipLaunchKernelGGL(gbuffer_kernel<true>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
+    else hipLaunchKernelGGL(gbuffer_kernel<false>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
     return hipGetLastError();
 }
 hipError_t launch_init(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, uint32_t depth, hipStream_t s) {
-    hipLaunchKernelGGL(init_kernel, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf, reservoir);
+    if (sc.counters) hipLaunchKernelGGL(init_kernel<true>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf, reservoir);
+    else hipLaunchKernelGGL(init_kernel<false>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf, reservoir);
     return hipGetLastError();
 }
 hipError_t launch_final(const Scene &sc, const uint4 *gbuf, const uint4 *reservoir, float4 *accum, uint32_t depth,
                         hipStream_t s) {
-    hipLaunchKernelGGL(final_kernel, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf, reservoir,
+    if (sc.counters) hipLaunchKernelGGL(final_kernel<true>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf, reservoir, accum);
+    else hipLaunchKernelGGL(final_kernel<false>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf, reservoir,
                        accum);
     return hipGetLastError();
 }
 hipError_t launch_mcpt(const Scene &sc, float4 *accum, uint32_t depth, hipStream_t s) {
-    hipLaunchKernelGGL(mcpt_kernel, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, accum);
+    if (sc.counters) hipLaunchKernelGGL(mcpt_kernel<true>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, accum);
+    else hipLaunchKernelGGL(mcpt_kernel<false>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, accum);
     return hipGetLastError();
 }
 

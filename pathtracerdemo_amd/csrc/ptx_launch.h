@@ -19,4 +19,12 @@ hipError_t launch_final(const Scene &sc, const uint4 *gbuf, const uint4 *reservo
                         uint32_t stack_depth, hipStream_t s);
 hipError_t launch_mcpt(const Scene &sc, float4 *accum, uint32_t stack_depth, hipStream_t s);
 
+// persistent-lane variants (ptx_persist.hip); ctr = a zeroed u32 pixel-queue counter
+hipError_t launch_init_persistent(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, unsigned int *ctr,
+                                  uint32_t stack_depth, hipStream_t s);
+hipError_t launch_final_persistent(const Scene &sc, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
+                                   unsigned int *ctr, uint32_t stack_depth, hipStream_t s);
+hipError_t launch_mcpt_persistent(const Scene &sc, float4 *accum, unsigned int *ctr, uint32_t stack_depth,
+                                  hipStream_t s);
+
 }  // namespace ptx

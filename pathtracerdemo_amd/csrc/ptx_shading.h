@@ -27,7 +27,7 @@ __device__ __forceinline__ float get_transmission(const Scene &sc, uint32_t inst
 }
 
 // GetSurface (SH/PT_1_InitPass.wgsl:438-467) with GetTriangleWorldSpace (:390-407)
-__device__ __noinline__ Surface get_surface(const Scene &sc, Compact x) {
+__device__ __forceinline__ Surface get_surface(const Scene &sc, Compact x) {
     const Inst &I = sc.insts[x.inst];
     const uint32_t *desc = desc_ptr(sc, I.mesh);
     Surface s;
@@ -167,7 +167,7 @@ __device__ __forceinline__ f3 sample_ggx(uint32_t &seed, float R) {
     float st = __builtin_sqrtf(1.0f - ct * ct);
     return normalize(mk(st * cosf(phi), st * sinf(phi), ct));
 }
-__device__ __noinline__ f3 sample_bsdf(uint32_t &seed, const Surface &X, f3 V, uint32_t &lobe) {
+__device__ __forceinline__ f3 sample_bsdf(uint32_t &seed, const Surface &X, f3 V, uint32_t &lobe) {
     bool transparent = rnd(seed) < X.mat.trans;
     if (transparent) {  // SampleBTDF, SH/PT_1_InitPass.wgsl:1063-1098
         bool same = dot(V, X.nrm) > 0.0f;
@@ -255,7 +255,7 @@ __device__ __forceinline__ float pdf_btdf(const Surface &X, f3 V, f3 L) {
     }
     return p_refl * pdf_r + p_trans * pdf_t;
 }
-__device__ __noinline__ float pdf_bsdf(const Surface &X, f3 V, f3 L) {
+__device__ __forceinline__ float pdf_bsdf(const Surface &X, f3 V, f3 L) {
     if (dot(L, X.nrm) * dot(V, X.nrm) > 0.0f) return pdf_brdf(X, V, L);
     return pdf_btdf(X, V, L);
 }
@@ -272,7 +272,7 @@ __device__ __forceinline__ f3 direction_to_light(const Surface &X, const LightSa
 }
 
 // SampleNEE + PDF_LIGHT (SH/PT_1_InitPass.wgsl:970-1025,1220-1245)
-__device__ __noinline__ LightSample sample_nee(const Scene &sc, uint32_t &seed, const Surface &X, f3 V) {
+__device__ __forceinline__ LightSample sample_nee(const Scene &sc, uint32_t &seed, const Surface &X, f3 V) {
     LightSample s;
     float P = rnd(seed);
     uint32_t L = 0, R = sc.U[U_LIGHT_COUNT] - 1u, M = (L + R) >> 1;
@@ -322,6 +322,7 @@ __device__ __forceinline__ f3 l_emit(const LightSample &XL, const Surface &X) {
 }
 
 // Visibility (SH/PT_1_InitPass.wgsl:774-802): up to 5 traces through transmissive hits.
+template <bool COUNT>
 __device__ __noinline__ float visibility(const Scene &sc, f3 start, f3 end, PassEps eps, uint32_t *stack,
                                          uint32_t stride) {
     float T = 1.0f;
@@ -330,7 +331,7 @@ __device__ __noinline__ float visibility(const Scene &sc, f3 start, f3 end, Pass
     Ray r{start, dir};
     float remain = dist;
     for (int it = 0; it < 5; ++it) {
-        Hit h = trace_ray(sc, r, eps, stack, stride);
+        Hit h = trace_ray<COUNT>(sc, r, eps, stack, stride);
         if (!h.valid || h.t > remain) return T;
         float tr = get_transmission(sc, h.s.inst, h.s.mat);
         if (tr == 0.0f) return 0.0f;

@@ -19,14 +19,14 @@ from .scene.world import CompiledScene, World, serialize_world
 
 class Renderer:
     def __init__(self, width: int, height: int, device: int = -1, pipeline: str = "restir",
-                 row_begin: int = 0, row_end: int = 0, count_work: bool = False):
+                 row_begin: int = 0, row_end: int = 0, count_work: bool = False, simple: bool = False):
         self._lib = N.load()
         self.width, self.height = int(width), int(height)
         self.pipeline = pipeline
         cfg = N.PtxConfig(width=self.width, height=self.height, row_begin=row_begin, row_end=row_end,
                           device=device,
                           pipeline=N.PTX_PIPELINE_MCPT if pipeline == "mcpt" else N.PTX_PIPELINE_RESTIR,
-                          flags=N.PTX_FLAG_COUNT_WORK if count_work else 0)
+                          flags=(N.PTX_FLAG_COUNT_WORK if count_work else 0) | (N.PTX_FLAG_SIMPLE_KERNELS if simple else 0))
         self._h = ctypes.c_void_p()
         rc = self._lib.ptx_create(ctypes.byref(cfg), ctypes.byref(self._h))
         if rc != N.PTX_OK:
