@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures (tests/golden/*) from the CPU oracle.
+
+The reference has no runnable WGSL runtime, tests or golden images (SURVEY.md §4,
+§8c), so these fixtures pin the oracle restatement itself: any later change to the
+oracle, the scene compiler or the HIP path that alters them is a regression.
+Run:  python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from helpers import uniform_for  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+from pathtracerdemo_amd.scene.world import compile_scene  # noqa: E402
+
+W, H = 24, 24
+
+
+def frame_fixture(cs, frames):
+    fr = O.Frame(uniform_for(cs, W, H, 1), cs.scene, cs.geometry, cs.accel)
+    for f in range(1, frames + 1):
+        fr.set_frame_index(f)
+        fr.run(O.PASS_RESTIR, threads=1)
+    mc = O.Frame(uniform_for(cs, W, H, 1), cs.scene, cs.geometry, cs.accel)
+    mc.run(O.PASS_MCPT, threads=1)
+    return dict(uniform=fr.uniform, gbuffer=fr.gbuffer, reservoir=fr.reservoir, accum_restir=fr.accum,
+                accum_mcpt=mc.accum)
+
+
+def kat_table():
+    rows = {"pcg": {str(s): O.pcg(s) for s in [0, 1, 2, 3, 1973, 9277, 26699, 2 ** 31, 2 ** 32 - 1]}}
+    n = [0.0, 0.0, 1.0]
+    mats = {"diffuse": [0.8, 0.8, 0.8, 0.0, 1.0, 0.0, 1.5], "metal": [0.9, 0.6, 0.3, 1.0, 0.25, 0.0, 1.5],
+            "glass": [1.0, 1.0, 0.0, 0.0, 0.01, 1.0, 1.5]}
+    v = [0.0, 0.6, 0.8]
+    ls = {"same": [0.48, 0.0, 0.8775], "across": [0.1, -0.5, -0.86]}
+    rows["bsdf"] = {f"{m}/{l}": [float(x) for x in O.bsdf(n, mats[m], v, ls[l])] for m in mats for l in ls}
+    rows["pdf_bsdf"] = {f"{m}/{l}": O.pdf_bsdf(n, mats[m], v, ls[l]) for m in mats for l in ls}
+    rows["sample_bsdf"] = {}
+    for m in mats:
+        for seed in (1, 77, 4096):
+            d, lobe, s2 = O.sample_bsdf(n, mats[m], v, seed)
+            rows["sample_bsdf"][f"{m}/{seed}"] = [[float(x) for x in d], lobe, s2]
+    return rows
+
+
+def main():
+    O.build()
+    cs = compile_scene("dummy_scene_1")
+    np.savez_compressed(os.path.join(HERE, "c1_24x24_4frames.npz"), **frame_fixture(cs, 4))
+    with open(os.path.join(HERE, "kat.json"), "w") as fh:
+        json.dump(kat_table(), fh, indent=1, sort_keys=True)
+    print("wrote", os.listdir(HERE))
+
+
+if __name__ == "__main__":
+    main()
