@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--scene", default="dummy_scene_1")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--simple", action="store_true", help="one-thread-per-pixel kernels (A/B baseline)")
+    ap.add_argument("--variant", choices=["wave", "tiled", "persistent", "simple"], default="wave",
+                    help="kernel variant (A/B): wavefront queues, tile + LDS ray exchange, persistent lanes, 1 thread/pixel")
     return ap.parse_args()
 
 
@@ -73,7 +74,7 @@ def main():
     row_begin, row_end = rank * Hb, (rank + 1) * Hb
     pipeline = args.workload
     r = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
-                 simple=args.simple)
+                 variant=args.variant)
     r.Initialize(cs)
 
     # work census of the exact frame (counting build, untimed): algorithmic bytes

@@ -53,6 +53,7 @@ extern "C" {
 #define PTX_PASS_INIT 1
 #define PTX_PASS_FINAL 2
 #define PTX_PASS_MCPT 3
+#define PTX_PASS_TRACE 4  /* ptx_trace / ptx_trace_device (stats slot only) */
 
 /* buffers for ptx_read_buffer / ptx_write_buffer / ptx_device_pointer */
 #define PTX_BUF_GBUFFER 0    /* band_h * W * 4 u32   */
@@ -61,7 +62,11 @@ extern "C" {
 #define PTX_BUF_COUNTERS 3   /* 8 u64 work counters (PTX_FLAG_COUNT builds) */
 
 #define PTX_FLAG_COUNT_WORK 1u     /* count rays / AABB / triangle tests on device (slower)   */
-#define PTX_FLAG_SIMPLE_KERNELS 2u /* one-thread-per-pixel kernels instead of persistent lanes */
+#define PTX_FLAG_SIMPLE_KERNELS 2u   /* A/B: one thread per pixel, no ray exchange            */
+#define PTX_FLAG_PERSISTENT_LANES 4u /* A/B: persistent lanes with pixel regeneration         */
+#define PTX_FLAG_TILED_EXCHANGE 8u   /* A/B: 16x16 tiles with an LDS ray exchange             */
+/* no variant flag: the wavefront pipeline (compacted ray queues, one trace round per
+   path vertex) -- the default */
 
 typedef struct ptx_config {
     uint32_t width, height;       /* full image size (uniform words 0,1 must match) */
@@ -74,8 +79,8 @@ typedef struct ptx_config {
 
 typedef struct ptx_stats {
     uint64_t frames;              /* ptx_render calls since the last stats reset    */
-    double kernel_ms_total[4];    /* summed device time per pass (HIP events)       */
-    uint64_t kernel_launches[4];  /* launches per pass                              */
+    double kernel_ms_total[8];    /* summed device time per PTX_PASS_* (HIP events) */
+    uint64_t kernel_launches[8];  /* launches per PTX_PASS_*                        */
     uint32_t triangles, bvh_nodes, instances, max_bvh_depth;
     uint64_t device_bytes;        /* device memory held by the handle               */
 } ptx_stats;
@@ -98,6 +103,13 @@ int ptx_reset_stats(ptx_handle *h);
 int ptx_read_buffer(ptx_handle *h, int which, void *host_dst, size_t bytes);
 int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t bytes);
 int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes);
+/* Closest-hit queries (TraceRay, SH/PT_1_InitPass.wgsl:605-715) for arbitrary rays.
+ * rays: n x {o.x,o.y,o.z,d.x, d.y,d.z,-,-} f32 (32 B); hits: n x {t, flags|inst|mat (u32 bits),
+ * prim (u32 bits), bary.x, bary.y, pos.x, pos.y, pos.z} (32 B; flags bit31 = valid).
+ * eps_mode 0 = G-buffer epsilons (PT_01), 1 = secondary-pass epsilons (PT_1/PT_4/MCPT).
+ * ptx_trace takes host arrays (blocking); ptx_trace_device takes device pointers (async). */
+int ptx_trace(ptx_handle *h, const float *rays, float *hits, size_t n, int eps_mode);
+int ptx_trace_device(ptx_handle *h, const void *rays_dev, void *hits_dev, size_t n, int eps_mode);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL restores the own stream. */
 int ptx_set_stream(ptx_handle *h, void *hip_stream);
 int ptx_destroy(ptx_handle *h);

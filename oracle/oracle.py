@@ -57,6 +57,8 @@ def lib():
         _lib.pto_pdf_bsdf.restype = ctypes.c_float
         _lib.pto_sample_bsdf.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_uint32), P,
                                          ctypes.POINTER(ctypes.c_uint32)]
+        _lib.pto_trace.argtypes = [ctypes.POINTER(Inputs), P, P, ctypes.c_size_t, ctypes.c_int,
+                                   ctypes.POINTER(Counters)]
         _lib.pto_ray_triangle.argtypes = [P, P, P, P, P, ctypes.c_float]
         _lib.pto_ray_triangle.restype = ctypes.c_float
     return _lib
@@ -82,6 +84,17 @@ class Frame:
 
     def set_frame_index(self, f: int):
         self.uniform[23] = f
+
+    def trace(self, rays: np.ndarray, eps_mode: int = 1) -> np.ndarray:
+        """Closest hits for (n, 8) f32 rays, same format as ptx_trace."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        hits = np.zeros_like(rays)
+        inp = Inputs(self.uniform.ctypes.data, self.scene.ctypes.data, self.geometry.ctypes.data,
+                     self.accel.ctypes.data)
+        cnt = Counters()
+        lib().pto_trace(ctypes.byref(inp), _ptr(rays), _ptr(hits), len(rays), eps_mode, ctypes.byref(cnt))
+        self.counters["trace"] = cnt.as_dict()
+        return hits
 
     def run(self, pass_id: int, threads: int = 0, rect=None) -> dict:
         threads = threads or os.cpu_count() or 1

@@ -1024,6 +1024,23 @@ void pto_mcpt(const pto_inputs *in, int x0, int y0, int x1, int y1, float *accum
             mcpt_pixel(&c, (uint32_t)x, (uint32_t)y, accum + 4u * ((uint32_t)y * W + (uint32_t)x));
 }
 
+/* ================================================================== ray queries */
+void pto_trace(const pto_inputs *in, const float *rays, float *hits, size_t n, int eps_mode, pto_counters *cnt) {
+    ctx c;
+    ctx_init(&c, in, eps_mode == 0 ? EPS_GBUFFER : EPS_INIT, cnt);
+    for (size_t i = 0; i < n; ++i) {
+        const float *r = rays + 8 * i;
+        ray q = {V3(r[0], r[1], r[2]), V3(r[3], r[4], r[5])};
+        hit h = trace_ray(&c, q);
+        float *o = hits + 8 * i;
+        uint32_t enc = ((uint32_t)h.valid << 31) | (h.s.inst << 16) | h.s.mat;
+        v3 pos = V3(0.0f, 0.0f, 0.0f);
+        if (h.valid) pos = get_surface(&c, h.s).pos;
+        o[0] = h.t; o[1] = f32_of(enc); o[2] = f32_of(h.s.prim); o[3] = h.s.bu;
+        o[4] = h.s.bv; o[5] = pos.x; o[6] = pos.y; o[7] = pos.z;
+    }
+}
+
 /* ================================================================== KAT helpers */
 static surface kat_surface(const float *n, const float *mat) {
     surface s;

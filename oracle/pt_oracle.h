@@ -64,6 +64,11 @@ void pto_mcpt(const pto_inputs *in, int x0, int y0, int x1, int y1, float *accum
 int pto_run(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, uint32_t *gbuffer,
             uint32_t *reservoir, float *accum, pto_counters *cnt);
 
+/* Closest-hit queries, same record formats as ptx_trace (include/ptx.h):
+ * rays n x 8 f32 {o, d.x | d.y, d.z, -, -}; hits n x 8 {t, flags|inst|mat, prim, bu, bv, pos}.
+ * eps_mode 0 = PT_01 epsilons, 1 = PT_1/PT_4/MCPT epsilons. */
+void pto_trace(const pto_inputs *in, const float *rays, float *hits, size_t n, int eps_mode, pto_counters *cnt);
+
 /* Known-answer helpers (SH/PT_1_InitPass.wgsl:810-826). */
 uint32_t pto_pcg(uint32_t seed);
 float pto_random(uint32_t *seed);

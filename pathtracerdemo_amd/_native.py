@@ -13,15 +13,20 @@ LIB_PATH = os.path.join(PKG_DIR, "libptx.so")
 
 PTX_OK = 0
 PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT = 0, 1
-PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT = 0, 1, 2, 3
+PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT, PTX_PASS_TRACE = 0, 1, 2, 3, 4
 PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS = 0, 1, 2, 3
 PTX_FLAG_COUNT_WORK = 1
 PTX_FLAG_SIMPLE_KERNELS = 2
+PTX_FLAG_PERSISTENT_LANES = 4
+PTX_FLAG_TILED_EXCHANGE = 8
+VARIANT_FLAGS = {"wave": 0, "tiled": PTX_FLAG_TILED_EXCHANGE, "persistent": PTX_FLAG_PERSISTENT_LANES,
+                 "simple": PTX_FLAG_SIMPLE_KERNELS}
 
 # every symbol include/ptx.h declares (checked by tests/test_abi.py)
 EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame", "ptx_render", "ptx_run_pass",
             "ptx_reset_accumulation", "ptx_synchronize", "ptx_get_stats", "ptx_reset_stats", "ptx_read_buffer",
-            "ptx_write_buffer", "ptx_device_pointer", "ptx_set_stream", "ptx_destroy", "ptx_last_error"]
+            "ptx_write_buffer", "ptx_device_pointer", "ptx_set_stream", "ptx_destroy", "ptx_last_error",
+            "ptx_trace", "ptx_trace_device"]
 
 
 class PtxConfig(ctypes.Structure):
@@ -31,8 +36,8 @@ class PtxConfig(ctypes.Structure):
 
 
 class PtxStats(ctypes.Structure):
-    _fields_ = [("frames", ctypes.c_uint64), ("kernel_ms_total", ctypes.c_double * 4),
-                ("kernel_launches", ctypes.c_uint64 * 4), ("triangles", ctypes.c_uint32),
+    _fields_ = [("frames", ctypes.c_uint64), ("kernel_ms_total", ctypes.c_double * 8),
+                ("kernel_launches", ctypes.c_uint64 * 8), ("triangles", ctypes.c_uint32),
                 ("bvh_nodes", ctypes.c_uint32), ("instances", ctypes.c_uint32), ("max_bvh_depth", ctypes.c_uint32),
                 ("device_bytes", ctypes.c_uint64)]
 
@@ -68,6 +73,8 @@ def load(path: str = LIB_PATH):
     lib.ptx_write_buffer.argtypes = [H, ctypes.c_int, P, ctypes.c_size_t]
     lib.ptx_device_pointer.argtypes = [H, ctypes.c_int, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.ptx_set_stream.argtypes = [H, P]
+    lib.ptx_trace.argtypes = [H, P, P, ctypes.c_size_t, ctypes.c_int]
+    lib.ptx_trace_device.argtypes = [H, P, P, ctypes.c_size_t, ctypes.c_int]
     lib.ptx_destroy.argtypes = [H]
     lib.ptx_last_error.argtypes = [H]
     lib.ptx_last_error.restype = ctypes.c_char_p

@@ -22,7 +22,7 @@ using namespace ptx;
 
 namespace {
 
-constexpr int kPasses = 4;
+constexpr int kPasses = 8;
 constexpr int kEventRing = 64;
 
 struct DevBuf {
@@ -60,11 +60,15 @@ struct ptx_handle {
     // band buffers
     uint32_t band_h = 0;
     DevBuf d_gbuf, d_res, d_accum, d_counters, d_queue;
+    DevBuf d_qrays, d_qhits;  // staging for ptx_trace (host arrays)
+    // wavefront variant: pixel state, ray queue + ping-pong results / active lists, counters
+    DevBuf d_wstate, d_wrays, d_wres0, d_wres1, d_wact0, d_wact1, d_wctr;
+    size_t wave_ray_cap = 0;
     // stats
     TimedLaunch ring[kEventRing];
     int ring_pos = 0;
-    double ms_total[kPasses] = {0, 0, 0, 0};
-    uint64_t launches[kPasses] = {0, 0, 0, 0};
+    double ms_total[kPasses] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t launches[kPasses] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t frames = 0;
 };
 
@@ -274,6 +278,63 @@ static void resolve_event(TimedLaunch &t, ptx_handle *h) {
     t.pending = false;
 }
 
+// Wavefront buffers, sized for the largest round: PT_1 emits <= 2 rays per pixel, PT_4
+// <= 1, TEST_MCPT <= LightCount + 1 (all shadow rays of a vertex + the next path ray).
+static int wave_buffers(ptx_handle *h, WaveBufs &w) {
+    const size_t npix = (size_t)h->band_h * h->cfg.width;
+    const uint32_t nl = h->uniform[U_LIGHT_COUNT];
+    const size_t per_px = std::max<size_t>(2u, (size_t)nl + 1u);
+    const size_t padded = (size_t)((h->cfg.width + 7u) / 8u) * ((h->band_h + 7u) / 8u) * 64u;
+    const size_t nseg = (padded + kWaveSegPixels - 1u) / kWaveSegPixels;
+    const size_t cap = per_px * kWaveSegPixels * nseg;
+    if (!h->d_wstate.p) {
+        if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wact0, nseg * kWaveSegPixels * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wact1, nseg * kWaveSegPixels * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wctr, 2u * kWaveMaxRounds * nseg * 4u)) return rc;
+    }
+    if (cap > h->wave_ray_cap) {
+        free_buf(h->d_wrays);
+        free_buf(h->d_wres0);
+        free_buf(h->d_wres1);
+        h->wave_ray_cap = 0;
+        if (int rc = alloc_buf(h, h->d_wrays, cap * 32u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wres0, cap * 32u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wres1, cap * 32u)) return rc;
+        h->wave_ray_cap = cap;
+    }
+    w.state = (float4 *)h->d_wstate.p;
+    w.npix = (uint32_t)npix;
+    w.seg_px = kWaveSegPixels;
+    w.nseg = (uint32_t)nseg;
+    w.ray_stride = (uint32_t)(per_px * kWaveSegPixels);
+    w.rays = (float4 *)h->d_wrays.p;
+    w.res[0] = (float4 *)h->d_wres0.p;
+    w.res[1] = (float4 *)h->d_wres1.p;
+    w.act[0] = (uint32_t *)h->d_wact0.p;
+    w.act[1] = (uint32_t *)h->d_wact1.p;
+    w.cnt = (uint32_t *)h->d_wctr.p;
+    return PTX_OK;
+}
+
+// One secondary pass as a fixed sequence of wavefront rounds (no host sync inside).
+static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass) {
+    const uint4 *gb = (const uint4 *)h->d_gbuf.p;
+    uint4 *res = (uint4 *)h->d_res.p;
+    float4 *acc = (float4 *)h->d_accum.p;
+    hipError_t e = hipSuccess;  // every round rewrites all of its segment counts: no memset
+    const int rounds = pass == PTX_PASS_INIT ? kWaveRoundsInit : pass == PTX_PASS_FINAL ? kWaveRoundsFinal
+                                                                                        : kWaveRoundsMcpt;
+    for (int r = 0; e == hipSuccess && r <= rounds; ++r) {
+        if (r > 0) e = wave_trace(sc, w, r - 1, 1, h->stack_depth, h->stream);
+        if (e != hipSuccess) break;
+        e = pass == PTX_PASS_INIT    ? wave_init_round(sc, w, r, gb, res, h->stream)
+            : pass == PTX_PASS_FINAL ? wave_final_round(sc, w, r, gb, res, acc, h->stream)
+                                     : wave_mcpt_round(sc, w, r, acc, h->stream);
+    }
+    return e;
+}
+
 static int timed_launch(ptx_handle *h, int pass) {
     if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before rendering");
     if (!h->layout_valid) {
@@ -283,27 +344,50 @@ static int timed_launch(ptx_handle *h, int pass) {
     h->ring_pos = (h->ring_pos + 1) % kEventRing;
     resolve_event(t, h);
     Scene sc = make_scene(h);
-    const bool simple = (h->cfg.flags & PTX_FLAG_SIMPLE_KERNELS) != 0;
+    // kernel variant: wavefront (default), tile + LDS ray exchange, persistent lanes, or one
+    // thread per pixel
+    const uint32_t fl = h->cfg.flags;
+    const int variant = (fl & PTX_FLAG_SIMPLE_KERNELS)      ? 2
+                        : (fl & PTX_FLAG_PERSISTENT_LANES)  ? 1
+                        : (fl & PTX_FLAG_TILED_EXCHANGE)    ? 0
+                                                            : 3;
     unsigned int *ctr = (unsigned int *)h->d_queue.p + pass;
-    if (!simple && pass != PTX_PASS_GBUFFER) HIP_CHECK(h, hipMemsetAsync(ctr, 0, sizeof(unsigned int), h->stream));
+    if (variant == 1 && pass != PTX_PASS_GBUFFER)
+        HIP_CHECK(h, hipMemsetAsync(ctr, 0, sizeof(unsigned int), h->stream));
+    WaveBufs w{};
+    if (variant == 3 && pass != PTX_PASS_GBUFFER) {
+        if (int rc = wave_buffers(h, w)) return rc;
+    }
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
     hipError_t e = hipSuccess;
     const uint4 *gb = (const uint4 *)h->d_gbuf.p;
+    uint4 *res = (uint4 *)h->d_res.p;
+    float4 *acc = (float4 *)h->d_accum.p;
+    const uint32_t d = h->stack_depth;
+    if (variant == 3 && pass != PTX_PASS_GBUFFER && pass >= PTX_PASS_INIT && pass <= PTX_PASS_MCPT) {
+        e = launch_wave_pass(h, sc, w, pass);
+        if (e != hipSuccess) return fail(h, PTX_E_HIP, "wavefront launch (pass %d): %s", pass, hipGetErrorString(e));
+        HIP_CHECK(h, hipEventRecord(t.stop, h->stream));
+        t.pass = pass;
+        t.pending = true;
+        return PTX_OK;
+    }
     switch (pass) {
-    case PTX_PASS_GBUFFER: e = launch_gbuffer(sc, (uint4 *)h->d_gbuf.p, h->stack_depth, h->stream); break;
+    case PTX_PASS_GBUFFER: e = launch_gbuffer(sc, (uint4 *)h->d_gbuf.p, d, h->stream); break;
     case PTX_PASS_INIT:
-        e = simple ? launch_init(sc, gb, (uint4 *)h->d_res.p, h->stack_depth, h->stream)
-                   : launch_init_persistent(sc, gb, (uint4 *)h->d_res.p, ctr, h->stack_depth, h->stream);
+        e = variant == 0   ? launch_init_tiled(sc, gb, res, d, h->stream)
+            : variant == 1 ? launch_init_persistent(sc, gb, res, ctr, d, h->stream)
+                           : launch_init(sc, gb, res, d, h->stream);
         break;
     case PTX_PASS_FINAL:
-        e = simple ? launch_final(sc, gb, (const uint4 *)h->d_res.p, (float4 *)h->d_accum.p, h->stack_depth,
-                                  h->stream)
-                   : launch_final_persistent(sc, gb, (const uint4 *)h->d_res.p, (float4 *)h->d_accum.p, ctr,
-                                             h->stack_depth, h->stream);
+        e = variant == 0   ? launch_final_tiled(sc, gb, res, acc, d, h->stream)
+            : variant == 1 ? launch_final_persistent(sc, gb, res, acc, ctr, d, h->stream)
+                           : launch_final(sc, gb, res, acc, d, h->stream);
         break;
     case PTX_PASS_MCPT:
-        e = simple ? launch_mcpt(sc, (float4 *)h->d_accum.p, h->stack_depth, h->stream)
-                   : launch_mcpt_persistent(sc, (float4 *)h->d_accum.p, ctr, h->stack_depth, h->stream);
+        e = variant == 0   ? launch_mcpt_tiled(sc, acc, d, h->stream)
+            : variant == 1 ? launch_mcpt_persistent(sc, acc, ctr, d, h->stream)
+                           : launch_mcpt(sc, acc, d, h->stream);
         break;
     default: return fail(h, PTX_E_INVALID, "unknown pass %d", pass);
     }
@@ -492,6 +576,39 @@ int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes) 
     return PTX_OK;
 }
 
+int ptx_trace_device(ptx_handle *h, const void *rays_dev, void *hits_dev, size_t n, int eps_mode) {
+    if (!h || (n && (!rays_dev || !hits_dev)) || n > 0xffffffffu || (eps_mode != 0 && eps_mode != 1))
+        return fail(h, PTX_E_INVALID, "ptx_trace: bad arguments");
+    if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before tracing");
+    if (!h->layout_valid) {
+        if (int rc = build_layout(h)) return rc;
+    }
+    TimedLaunch &t = h->ring[h->ring_pos];
+    h->ring_pos = (h->ring_pos + 1) % kEventRing;
+    resolve_event(t, h);
+    Scene sc = make_scene(h);
+    HIP_CHECK(h, hipEventRecord(t.start, h->stream));
+    hipError_t e = launch_trace_rays(sc, (const float4 *)rays_dev, (float4 *)hits_dev, (uint32_t)n, eps_mode,
+                                     h->stack_depth, h->stream);
+    if (e != hipSuccess) return fail(h, PTX_E_HIP, "trace launch: %s", hipGetErrorString(e));
+    HIP_CHECK(h, hipEventRecord(t.stop, h->stream));
+    t.pass = PTX_PASS_TRACE;
+    t.pending = true;
+    return PTX_OK;
+}
+
+int ptx_trace(ptx_handle *h, const float *rays, float *hits, size_t n, int eps_mode) {
+    if (!h || (n && (!rays || !hits))) return fail(h, PTX_E_INVALID, "ptx_trace: null arrays");
+    if (n == 0) return PTX_OK;
+    if (int rc = alloc_buf(h, h->d_qrays, std::max(h->d_qrays.bytes, n * 32u))) return rc;
+    if (int rc = alloc_buf(h, h->d_qhits, std::max(h->d_qhits.bytes, n * 32u))) return rc;
+    HIP_CHECK(h, hipMemcpyAsync(h->d_qrays.p, rays, n * 32u, hipMemcpyHostToDevice, h->stream));
+    if (int rc = ptx_trace_device(h, h->d_qrays.p, h->d_qhits.p, n, eps_mode)) return rc;
+    HIP_CHECK(h, hipMemcpyAsync(hits, h->d_qhits.p, n * 32u, hipMemcpyDeviceToHost, h->stream));
+    HIP_CHECK(h, hipStreamSynchronize(h->stream));
+    return PTX_OK;
+}
+
 int ptx_set_stream(ptx_handle *h, void *hip_stream) {
     if (!h) return PTX_E_INVALID;
     h->stream = hip_stream ? (hipStream_t)hip_stream : h->own_stream;
@@ -506,7 +623,8 @@ int ptx_destroy(ptx_handle *h) {
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
     for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_gbuf,
-                      &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue})
+                      &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
+                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr})
         free_buf(*b);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;

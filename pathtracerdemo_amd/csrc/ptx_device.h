@@ -217,14 +217,15 @@ __device__ __forceinline__ void barycentric(f3 P, f3 A, f3 B, f3 C, float eps, f
 // (entry k at stack[k * stride]).  Also returns the hit position exactly as
 // GetSurface(hit).Position computes it (same world-space vertices and barycentrics).
 template <bool COUNT>
-__device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack, uint32_t stride) {
+__device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack, uint32_t stride,
+                                          float t_max = 1e10f) {
     Hit best;
     best.valid = false;
     best.t = 0.0f;
     best.s = Compact{0u, 0u, 0u, 0u, 0.0f, 0.0f};
     best.pos = mk(0.0f, 0.0f, 0.0f);
     const float vx = 1e-4f;
-    float vy = 1e10f;
+    float vy = t_max;  // 1e10 in the reference; a smaller bound only prunes hits beyond it
     uint32_t n_aabb = 0, n_tri = 0;
     for (uint32_t ii = 0; ii < sc.n_inst; ++ii) {
         const Inst &I = sc.insts[ii];

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(BLOCK) void gbuffer_kernel(Scene sc, uint4 *gbuf) {
     uint32_t x, y;
     if (!pixel_of(sc, x, y)) return;
     uint32_t *stack = lds_stack + threadIdx.x;
-    Hit h = trace_ray<COUNT>(sc, camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);
+    Hit h = trace_core<COUNT>(sc, camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);
     Compact s = h.s;
     s.valid = h.valid ? 1u : 0u;
     gbuf[band_index(sc, x, y)] = encode(s);
@@ -353,6 +353,32 @@ hipError_t launch_final(const Scene &sc, const uint4 *gbuf, const uint4 *reservo
 hipError_t launch_mcpt(const Scene &sc, float4 *accum, uint32_t depth, hipStream_t s) {
     if (sc.counters) hipLaunchKernelGGL(mcpt_kernel<true>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, accum);
     else hipLaunchKernelGGL(mcpt_kernel<false>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, accum);
+    return hipGetLastError();
+}
+
+// =========================================================================== ray queries
+// One thread per ray; the traversal is trace_core (same code as every pass).
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void trace_rays_kernel(Scene sc, const float4 *rays, float4 *hits, uint32_t n,
+                                                           PassEps eps) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t *stack = lds_stack + threadIdx.x;
+    const float4 a = rays[2u * i], b = rays[2u * i + 1u];
+    Hit h = trace_core<COUNT>(sc, Ray{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y)}, eps, stack, BLOCK);
+    const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
+    hits[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
+    hits[2u * i + 1u] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
+}
+hipError_t launch_trace_rays(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
+                             uint32_t depth, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const PassEps eps = eps_mode == 0 ? PassEps{1e-8f, 1e-6f} : PassEps{1e-4f, 1e-8f};
+    const dim3 grid((n + BLOCK - 1) / BLOCK);
+    if (sc.counters)
+        hipLaunchKernelGGL(trace_rays_kernel<true>, grid, dim3(BLOCK), stack_lds_bytes(depth), s, sc, rays, hits, n, eps);
+    else
+        hipLaunchKernelGGL(trace_rays_kernel<false>, grid, dim3(BLOCK), stack_lds_bytes(depth), s, sc, rays, hits, n, eps);
     return hipGetLastError();
 }
 

@@ -27,4 +27,43 @@ hipError_t launch_final_persistent(const Scene &sc, const uint4 *gbuf, const uin
 hipError_t launch_mcpt_persistent(const Scene &sc, float4 *accum, unsigned int *ctr, uint32_t stack_depth,
                                   hipStream_t s);
 
+// closest-hit queries for a ray array (ptx_kernels.hip)
+hipError_t launch_trace_rays(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
+                             uint32_t stack_depth, hipStream_t s);
+
+// tile + LDS ray-exchange variants (ptx_persist.hip): the default
+hipError_t launch_init_tiled(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, uint32_t stack_depth,
+                             hipStream_t s);
+hipError_t launch_final_tiled(const Scene &sc, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
+                              uint32_t stack_depth, hipStream_t s);
+hipError_t launch_mcpt_tiled(const Scene &sc, float4 *accum, uint32_t stack_depth, hipStream_t s);
+
+// wavefront variant (ptx_wave.hip): the default.  A pass is a fixed sequence of rounds:
+// logic round 0 (start), then {trace r, logic r+1} for r < kWaveRounds[pass].  Every
+// launch has one workgroup per segment; queue lengths live on the device
+// (cnt[(2r) * nseg + j] pixels of segment j active after logic round r, cnt[(2r+1) *
+// nseg + j] rays it emitted), so the host never synchronises inside a pass.
+constexpr uint32_t kWaveStateSlots = 9u;   // float4 per pixel (PT_1 needs the most)
+constexpr uint32_t kWaveSegPixels = 1024u; // padded pixels per segment (16 8x8 tiles)
+constexpr int kWaveRoundsInit = 3, kWaveRoundsFinal = 3, kWaveRoundsMcpt = 4;
+constexpr int kWaveMaxRounds = 5;
+struct WaveBufs {
+    float4 *state;       // kWaveStateSlots * npix, SoA
+    uint32_t npix;       // pixels of the band
+    uint32_t seg_px;     // padded pixels per segment
+    uint32_t nseg;       // segments (= workgroups per launch)
+    uint32_t ray_stride; // ray slots per segment (seg_px * max rays per pixel per round)
+    float4 *rays;        // 2 float4 per ray: {o, remain}, {d, kind}
+    float4 *res[2];      // 2 float4 per ray, ping-pong by round parity
+    uint32_t *act[2];    // active pixel lists (nseg * seg_px), ping-pong
+    uint32_t *cnt;       // 2 * kWaveMaxRounds * nseg counts
+};
+hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t stack_depth,
+                      hipStream_t s);
+hipError_t wave_init_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, uint4 *reservoir,
+                           hipStream_t s);
+hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, const uint4 *reservoir,
+                            float4 *accum, hipStream_t s);
+hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, hipStream_t s);
+
 }  // namespace ptx

@@ -75,23 +75,6 @@ __device__ __forceinline__ void write_colorp(const Scene &sc, float4 *accum, siz
     float4 a = accum[i];
     accum[i] = make_float4(mixf(a.x, c.x, t), mixf(a.y, c.y, t), mixf(a.z, c.z, t), 1.0f);
 }
-// GetSurface at a hit whose position trace_core already produced: normal + material only.
-__device__ __forceinline__ Surface surface_at(const Scene &sc, const Compact &x, f3 pos) {
-    const Inst &I = sc.insts[x.inst];
-    const uint32_t *desc = desc_ptr(sc, I.mesh);
-    Surface s;
-    s.mat = get_material(sc, desc, x.mat);
-    uint32_t id[3];
-    tri_vertex_ids(sc, desc, x.prim, id);
-    f3 n0 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[0]));
-    f3 n1 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[1]));
-    f3 n2 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[2]));
-    float U = x.bu, V = x.bv, W = 1.0f - U - V;
-    s.nrm = normalize((n0 * U + n1 * V) + n2 * W);
-    s.pos = pos;
-    return s;
-}
-
 // Visibility state (SH/PT_1_InitPass.wgsl:774-802) shared by every pass.
 struct Vis {
     f3 org, dir;
@@ -528,6 +511,300 @@ __global__ __launch_bounds__(PBLOCK) void mcpt_persistent(Scene sc, float4 *accu
             else has_ray = mcpt_bsdf_step(sc, s, accum, ray);
         }
     }
+}
+
+// =========================================================================== tile + LDS ray exchange
+// One workgroup owns a 16x16 pixel tile for the whole pass; lane states stay in
+// registers.  Every iteration all 256 lanes post their pending ray to LDS with a bin key
+// (light id for shadow / Visibility rays, direction octant for BSDF and camera rays), a
+// counting sort orders the rays by key, and lane j traces the j-th sorted ray.  The rays
+// of a tile are therefore compacted into the fewest waves and grouped so that a wave
+// traverses rays aimed at the same light or octant (coherent node fetches), while the
+// state machine stays per pixel.  Results remain per-pixel functions: only who traces a
+// ray changes, never what is traced.
+constexpr uint32_t XBINS = 64;           // bin keys: [0,56) lights (id % 56), [56,64) octants
+constexpr uint32_t XLIGHT_BINS = 56;
+
+struct alignas(16) XchgLds {
+    float4 ray0[PBLOCK];   // o.xyz, d.x
+    float4 ray1[PBLOCK];   // d.y, d.z
+    float4 hit0[PBLOCK];   // t, enc(valid|inst|mat), prim, bu
+    float4 hit1[PBLOCK];   // bv, pos.xyz
+    uint32_t cnt[XBINS];
+    uint32_t base[XBINS];
+    uint16_t perm[PBLOCK];
+    uint32_t nrays, pad[3];
+};
+constexpr size_t kXchgBytes = (sizeof(XchgLds) + 15u) & ~size_t(15);
+
+__device__ __forceinline__ uint32_t octant_key(f3 d) {
+    return XLIGHT_BINS + (d.x < 0.0f ? 1u : 0u) + (d.y < 0.0f ? 2u : 0u) + (d.z < 0.0f ? 4u : 0u);
+}
+__device__ __forceinline__ uint32_t light_key(int32_t id, f3 d) {
+    return id >= 0 ? (uint32_t)id % XLIGHT_BINS : octant_key(d);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void xchg_trace(const Scene &sc, XchgLds &X, uint32_t *stack, PassEps eps, bool has_ray,
+                                           const Ray &ray, uint32_t key, Hit &out) {
+    const uint32_t tid = threadIdx.x;
+    if (tid < XBINS) X.cnt[tid] = 0u;
+    __syncthreads();
+    uint32_t rank = 0u;
+    if (has_ray) {
+        rank = atomicAdd(&X.cnt[key], 1u);
+        X.ray0[tid] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.d.x);
+        X.ray1[tid] = make_float4(ray.d.y, ray.d.z, 0.0f, 0.0f);
+    }
+    __syncthreads();
+    if (tid < 64u) {  // wave 0: exclusive scan of the 64 bin counts
+        uint32_t v = X.cnt[tid], incl = v;
+        for (uint32_t o = 1u; o < 64u; o <<= 1) {
+            uint32_t t = __shfl_up(incl, o);
+            if (tid >= o) incl += t;
+        }
+        X.base[tid] = incl - v;
+        if (tid == 63u) X.nrays = incl;
+    }
+    __syncthreads();
+    if (has_ray) X.perm[X.base[key] + rank] = (uint16_t)tid;
+    __syncthreads();
+    if (tid < X.nrays) {
+        const uint32_t src = X.perm[tid];
+        const float4 a = X.ray0[src], b = X.ray1[src];
+        Hit h = trace_core<COUNT>(sc, Ray{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y)}, eps, stack, PBLOCK);
+        const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
+        X.hit0[src] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
+        X.hit1[src] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
+    }
+    __syncthreads();
+    if (has_ray) {
+        const float4 a = X.hit0[tid], b = X.hit1[tid];
+        const uint32_t enc = asu(a.y);
+        out.valid = (enc >> 31) != 0u;
+        out.t = a.x;
+        out.s = Compact{enc >> 31, (enc >> 16) & 0x7fffu, enc & 0xffffu, asu(a.z), a.w, b.x};
+        out.pos = mk(b.y, b.z, b.w);
+    }
+}
+
+__device__ __forceinline__ bool tile_pixel(const Scene &sc, uint32_t &x, uint32_t &y) {
+    const uint32_t tiles_x = (sc.width + 15u) / 16u;
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    x = (blockIdx.x % tiles_x) * 16u + (w & 1u) * 8u + (lane & 7u);
+    y = sc.row_begin + (blockIdx.x / tiles_x) * 16u + (w >> 1) * 8u + (lane >> 3);
+    return x < sc.width && y < sc.row_end;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(PBLOCK) void init_tiled(Scene sc, const uint4 *gbuf, uint4 *reservoir) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    XchgLds &X = *reinterpret_cast<XchgLds *>(lds_raw);
+    uint32_t *stack = reinterpret_cast<uint32_t *>(lds_raw + kXchgBytes) + threadIdx.x;
+    const PassEps eps{1e-4f, 1e-8f};
+    InitState s;
+    Ray ray;
+    bool has_ray = false;
+    uint32_t x, y;
+    if (tile_pixel(sc, x, y)) {
+        s.pix = (y - sc.row_begin) * sc.width + x;
+        const Compact x1 = decode_g(gbuf[s.pix]);
+        if (!x1.valid) {  // reservoir unobservable: PT_4 returns before LoadReservoir (:1404-1408)
+            uint4 *out = reservoir + 8u * (size_t)s.pix;
+            for (int k = 0; k < 8; ++k) out[k] = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            s.seed = pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u);
+            s.f = mk(1.0f, 1.0f, 1.0f);
+            s.p = 1.0f;
+            s.C = 0u; s.w_sum = 0.0f; s.p_hat_sel = 0.0f; s.selected = false;
+            s.lobe1 = 0u; s.lobe2 = 0u; s.bseed1 = 0u; s.bseed2 = 0u;
+            s.cs2 = make_uint4(0u, 0u, 0u, 0u); s.cs3 = s.cs2;
+            s.prev = get_x0p(sc, x, y);
+            s.X = get_surface(sc, x1);
+            s.p1 = s.X.pos; s.r1 = s.X.mat.rough;
+            s.p2 = s.p1; s.r2 = 0.0f; s.p3 = s.p1; s.r3 = 0.0f;
+            s.i = 1u;
+            init_begin_vertex(sc, s, ray);
+            has_ray = true;
+        }
+    }
+    while (__syncthreads_or(has_ray)) {
+        const uint32_t key = has_ray ? (s.phase == 0u ? light_key(s.XL.id, ray.d) : octant_key(ray.d)) : 0u;
+        Hit h;
+        xchg_trace<COUNT>(sc, X, stack, eps, has_ray, ray, key, h);
+        if (!has_ray) continue;
+        if (s.phase == 0u) {  // NEE visibility segment
+            float v;
+            if (!vis_step(sc, s.vis, h, v)) { ray = Ray{s.vis.org, s.vis.dir}; continue; }
+            has_ray = init_after_nee(sc, s, v, reservoir, ray);
+        } else if (!h.valid) {  // BSDF ray escaped: env candidate (PT_1:1447-1461)
+            LightSample env;
+            env.pos = s.X.pos + s.L * INF_F;
+            env.type = LIGHT_ENV;
+            env.dir = -s.L;
+            env.id = -1;
+            env.Le = mk(ENV_C, ENV_C, ENV_C);
+            env.pdf = pdf_bsdf(s.X, s.V, s.L);
+            float ph = luminance(s.f * ENV_C);
+            float ris = ph / s.p;
+            s.C += 1u;
+            s.w_sum += ris;
+            if (rnd(s.seed) < ris / s.w_sum) {
+                s.selected = true;
+                s.p_hat_sel = ph;
+                write_compressed(s, true, env, reservoir + 8u * (size_t)s.pix);
+            }
+            init_finish(sc, s, reservoir);
+            has_ray = false;
+        } else {  // BSDF ray hit: next vertex (PT_1:1464-1468)
+            s.prev = s.X.pos;
+            s.X = surface_at(sc, h.s, h.pos);
+            s.i += 1u;
+            if (s.i == 2u) { s.p2 = s.X.pos; s.r2 = s.X.mat.rough; s.cs2 = encode_g(h.s); }
+            else { s.p3 = s.X.pos; s.r3 = s.X.mat.rough; s.cs3 = encode_g(h.s); }
+            init_begin_vertex(sc, s, ray);
+        }
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(PBLOCK) void final_tiled(Scene sc, const uint4 *gbuf, const uint4 *reservoir,
+                                                      float4 *accum) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    XchgLds &X = *reinterpret_cast<XchgLds *>(lds_raw);
+    uint32_t *stack = reinterpret_cast<uint32_t *>(lds_raw + kXchgBytes) + threadIdx.x;
+    const PassEps eps{1e-4f, 1e-8f};
+    FinalState s;
+    Ray ray;
+    bool has_ray = false;
+    uint32_t x, y;
+    if (tile_pixel(sc, x, y)) {
+        s.pix = (y - sc.row_begin) * sc.width + x;
+        const Compact x1 = decode_g(gbuf[s.pix]);
+        const uint4 *res = reservoir + 8u * (size_t)s.pix;
+        if (!x1.valid) {
+            accum[s.pix] = make_float4(ENV_C, ENV_C, ENV_C, 1.0f);
+        } else {
+            const uint4 r0 = res[0], r1 = res[1], r2 = res[2], r3 = res[3], r5 = res[5], r7 = res[7];
+            s.length = r5.w;
+            if (r7.y == 0u || s.length < 2u) {
+                write_colorp(sc, accum, s.pix, mk(0.0f, 0.0f, 0.0f));
+            } else {
+                s.seeds0 = r0.x; s.seeds1 = r0.y; s.seeds2 = r0.z;
+                s.ucw = asf(r7.x);
+                s.XL.dir = mk(asf(r1.x), asf(r1.y), asf(r1.z));
+                s.XL.type = r1.w;
+                s.XL.pos = mk(asf(r2.x), asf(r2.y), asf(r2.z));
+                s.XL.id = (int32_t)r2.w;
+                s.XL.Le = mk(asf(r3.x), asf(r3.y), asf(r3.z));
+                s.XL.pdf = asf(r3.w);
+                s.prev = get_x0p(sc, x, y);
+                s.cur = get_surface(sc, x1);
+                s.f = mk(1.0f, 1.0f, 1.0f);
+                s.i = 1u;
+                if (s.i + 1u < s.length) final_regen_ray(s, ray);
+                else final_last_segment(s, ray);
+                has_ray = true;
+            }
+        }
+    }
+    while (__syncthreads_or(has_ray)) {
+        const uint32_t key = has_ray ? (s.phase == 0u ? octant_key(ray.d) : light_key(s.XL.id, ray.d)) : 0u;
+        Hit h;
+        xchg_trace<COUNT>(sc, X, stack, eps, has_ray, ray, key, h);
+        if (!has_ray) continue;
+        if (s.phase == 0u) {
+            Surface next = h.valid ? surface_at(sc, h.s, h.pos) : get_surface(sc, h.s);
+            f3 L = normalize(next.pos - s.cur.pos);
+            s.f = s.f * (bsdf(s.cur, L, s.V) * fabsf(dot(s.cur.nrm, L)));
+            s.prev = s.cur.pos;
+            s.cur = next;
+            s.i += 1u;
+            if (s.i + 1u < s.length) final_regen_ray(s, ray);
+            else final_last_segment(s, ray);
+        } else {
+            float v;
+            if (!vis_step(sc, s.vis, h, v)) { ray = Ray{s.vis.org, s.vis.dir}; continue; }
+            s.f = s.f * (s.Le * v);
+            write_colorp(sc, accum, s.pix, s.f * s.ucw);
+            has_ray = false;
+        }
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(PBLOCK) void mcpt_tiled(Scene sc, float4 *accum) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    XchgLds &X = *reinterpret_cast<XchgLds *>(lds_raw);
+    uint32_t *stack = reinterpret_cast<uint32_t *>(lds_raw + kXchgBytes) + threadIdx.x;
+    const PassEps eps{1e-4f, 1e-8f};
+    const uint32_t nl = sc.U[U_LIGHT_COUNT];
+    McptState s;
+    Ray ray;
+    bool has_ray = false;
+    uint32_t x, y;
+    if (tile_pixel(sc, x, y)) {
+        s.pix = (y - sc.row_begin) * sc.width + x;
+        s.seed = pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u);
+        s.path = camera_rayp(sc, x, y);
+        s.color = mk(0.0f, 0.0f, 0.0f);
+        s.f = mk(1.0f, 1.0f, 1.0f);
+        s.p = 1.0f;
+        s.bounce = 0u;
+        s.phase = 0u;
+        ray = s.path;
+        has_ray = true;
+    }
+    while (__syncthreads_or(has_ray)) {
+        const uint32_t key = has_ray ? (s.phase == 0u ? octant_key(ray.d) : s.light % XLIGHT_BINS) : 0u;
+        Hit h;
+        xchg_trace<COUNT>(sc, X, stack, eps, has_ray, ray, key, h);
+        if (!has_ray) continue;
+        if (s.phase == 0u) {
+            if (!h.valid) {
+                s.color = s.color + (s.f / s.p) * ENV_C;
+                write_colorp(sc, accum, s.pix, s.color);
+                has_ray = false;
+                continue;
+            }
+            s.X = surface_at(sc, h.s, h.pos);
+            s.V = normalize(s.path.o - s.X.pos);
+            s.light = 0u;
+            if (nl > 0u) mcpt_begin_light(sc, s, ray);
+            else has_ray = mcpt_bsdf_step(sc, s, accum, ray);
+        } else {
+            float v;
+            if (!vis_step(sc, s.vis, h, v)) { ray = Ray{s.vis.org, s.vis.dir}; continue; }
+            s.color = s.color + (s.f / s.p) * ((s.c * v) / s.lpdf);
+            s.light += 1u;
+            if (s.light < nl) mcpt_begin_light(sc, s, ray);
+            else has_ray = mcpt_bsdf_step(sc, s, accum, ray);
+        }
+    }
+}
+
+static dim3 tiled_grid(const Scene &sc) {
+    return dim3(((sc.width + 15u) / 16u) * ((sc.row_end - sc.row_begin + 15u) / 16u));
+}
+static size_t tiled_lds(uint32_t depth) { return kXchgBytes + stack_lds_bytes(depth); }
+
+hipError_t launch_init_tiled(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, uint32_t depth, hipStream_t s) {
+    if (sc.counters) hipLaunchKernelGGL(init_tiled<true>, tiled_grid(sc), dim3(PBLOCK), tiled_lds(depth), s, sc, gbuf, reservoir);
+    else hipLaunchKernelGGL(init_tiled<false>, tiled_grid(sc), dim3(PBLOCK), tiled_lds(depth), s, sc, gbuf, reservoir);
+    return hipGetLastError();
+}
+hipError_t launch_final_tiled(const Scene &sc, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
+                              uint32_t depth, hipStream_t s) {
+    if (sc.counters)
+        hipLaunchKernelGGL(final_tiled<true>, tiled_grid(sc), dim3(PBLOCK), tiled_lds(depth), s, sc, gbuf, reservoir, accum);
+    else
+        hipLaunchKernelGGL(final_tiled<false>, tiled_grid(sc), dim3(PBLOCK), tiled_lds(depth), s, sc, gbuf, reservoir, accum);
+    return hipGetLastError();
+}
+hipError_t launch_mcpt_tiled(const Scene &sc, float4 *accum, uint32_t depth, hipStream_t s) {
+    if (sc.counters) hipLaunchKernelGGL(mcpt_tiled<true>, tiled_grid(sc), dim3(PBLOCK), tiled_lds(depth), s, sc, accum);
+    else hipLaunchKernelGGL(mcpt_tiled<false>, tiled_grid(sc), dim3(PBLOCK), tiled_lds(depth), s, sc, accum);
+    return hipGetLastError();
 }
 
 // =========================================================================== launches

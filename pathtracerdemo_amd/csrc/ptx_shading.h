@@ -45,6 +45,23 @@ __device__ __forceinline__ Surface get_surface(const Scene &sc, Compact x) {
     s.pos = (p0 * U + p1 * V) + p2 * W;
     return s;
 }
+// GetSurface at a hit whose position trace_core already produced: normal + material only
+// (the position is bit-identical: same world-space vertices and barycentrics).
+__device__ __forceinline__ Surface surface_at(const Scene &sc, const Compact &x, f3 pos) {
+    const Inst &I = sc.insts[x.inst];
+    const uint32_t *desc = desc_ptr(sc, I.mesh);
+    Surface s;
+    s.mat = get_material(sc, desc, x.mat);
+    uint32_t id[3];
+    tri_vertex_ids(sc, desc, x.prim, id);
+    f3 n0 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[0]));
+    f3 n1 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[1]));
+    f3 n2 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[2]));
+    float U = x.bu, V = x.bv, W = 1.0f - U - V;
+    s.nrm = normalize((n0 * U + n1 * V) + n2 * W);
+    s.pos = pos;
+    return s;
+}
 // Position-only GetSurface for Visibility restarts (the normal is unused there).
 __device__ __forceinline__ f3 get_surface_pos(const Scene &sc, Compact x) {
     const Inst &I = sc.insts[x.inst];

@@ -1,0 +1,822 @@
+// ptx_wave.hip -- wavefront form of the secondary passes (the default fast path).
+//
+// Observation that makes this work: in the reference, a Visibility() result never feeds
+// back into the RNG stream or into path construction.  UpdateReservoir always draws
+// exactly one Random() (SH/PT_1_InitPass.wgsl:1298-1320); f, p and Russian roulette do
+// not depend on visibility; in TEST_MCPT the light terms only add to the colour
+// (SH/TEST_MCPT.wgsl:1351-1366).  So at every path vertex the shadow ray(s) AND the next
+// BSDF ray are known before any of them is traced: each vertex costs ONE trace round,
+// and the reservoir update / colour accumulation that needs the visibility is resolved
+// in the next logic step, in the reference's order.  The random draws happen at the same
+// points of the stream as in the WGSL, so results are identical per pixel.
+//
+// Queues are segmented by workgroup: workgroup j of every logic kernel owns pixel segment
+// j (seg_px padded pixels, 8x8 tiles) for the whole pass, keeps that segment's active
+// list, and appends its rays to ray segment j through LDS counters; trace workgroup j
+// traces ray segment j.  No global atomics anywhere (a single device-wide queue counter
+// serialises at ~4 ns per wave-level append, which cost more than the shading itself).
+//
+// Kernels (256-thread workgroups, one per segment):
+//   trace_queue  -- lean closest-hit / Visibility queries over a ray segment (≈70
+//                   VGPRs); the Visibility loop (<=5 traces through transmissive hits,
+//                   SH/PT_1_InitPass.wgsl:774-802) runs inside it, pruned at the light.
+//   *_start      -- per pixel: first vertex, emits the first round of rays.
+//   *_step       -- per active pixel: consumes its results, advances to the next vertex,
+//                   emits the next round.  Pixel state lives in HBM (SoA float4 slots).
+// Rounds: init <= 3 traces (vertices 1..3), final <= 3 (two regenerated BSDF rays + the
+// light visibility), MCPT <= 4 (primary + 3 bounces with all lights' shadow rays).
+#include "ptx_launch.h"
+#include "ptx_shading.h"
+
+namespace ptx {
+
+constexpr uint32_t WB = kBlock;
+enum : uint32_t { Q_CLOSEST = 0u, Q_VIS = 1u };
+
+// ---------------------------------------------------------------- wave helpers
+// Exclusive prefix sum of `v` over the wave and the wave total.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v, uint32_t &total) {
+    const uint32_t lane = __lane_id();
+    uint32_t incl = v;
+    for (uint32_t o = 1u; o < 64u; o <<= 1) {
+        uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    total = __shfl(incl, 63);
+    return incl - v;
+}
+// Reserve `n` consecutive slots of this workgroup's segment (one LDS atomic per wave).
+// Must be reached by every lane of the wave.
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t *lds_ctr, uint32_t n) {
+    uint32_t total;
+    const uint32_t excl = wave_scan(n, total);
+    uint32_t base = 0u;
+    if (__lane_id() == 0u && total) base = atomicAdd(lds_ctr, total);
+    base = __shfl(base, 0);
+    return base + excl;
+}
+
+// This workgroup's view of one logic round: its segments of the queues and LDS counters.
+struct Seg {
+    uint32_t j, round;
+    uint32_t rbase;            // first ray slot of the segment
+    float4 *rays, *res_out;    // rays emitted this round + their result/payload slots
+    const float4 *res_in;      // results of the previous trace round
+    uint32_t *act_out;         // active list written this round (segment-local)
+    const uint32_t *act_in;    // active list of the previous round
+    uint32_t n_in;             // its length
+    uint32_t *l_ray, *l_act;   // LDS counters
+};
+__device__ __forceinline__ Seg seg_begin(const WaveBufs &w, uint32_t round, uint32_t *lds) {
+    Seg g;
+    g.j = blockIdx.x;
+    g.round = round;
+    g.rbase = g.j * w.ray_stride;
+    g.rays = w.rays;
+    g.res_out = w.res[round & 1u];
+    g.res_in = w.res[(round + 1u) & 1u];
+    g.act_out = w.act[round & 1u] + (size_t)g.j * w.seg_px;
+    g.act_in = w.act[(round + 1u) & 1u] + (size_t)g.j * w.seg_px;
+    g.n_in = round ? w.cnt[(2u * (round - 1u)) * w.nseg + g.j] : 0u;
+    g.l_ray = lds;
+    g.l_act = lds + 1;
+    if (threadIdx.x == 0) { lds[0] = 0u; lds[1] = 0u; }
+    __syncthreads();
+    return g;
+}
+__device__ __forceinline__ void seg_end(const WaveBufs &w, const Seg &g) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        w.cnt[(2u * g.round) * w.nseg + g.j] = *g.l_act;
+        w.cnt[(2u * g.round + 1u) * w.nseg + g.j] = *g.l_ray;
+    }
+}
+// Padded pixel handled by this thread at offset k of segment j.  A segment is 16 8x8
+// tiles spread over the whole band (tile j + t * nseg): each wave still shades one
+// coherent tile, while every segment -- and so every trace workgroup -- sees a sample of
+// the whole image, which keeps the per-segment trace cost even.
+__device__ __forceinline__ uint32_t seg_pixel(const WaveBufs &w, uint32_t j, uint32_t k) {
+    const uint32_t t = (k + threadIdx.x) >> 6;  // tile slot within the segment
+    return (j + t * w.nseg) * 64u + (threadIdx.x & 63u);
+}
+// append the active pixel to this round's list (all lanes)
+__device__ __forceinline__ void seg_keep(const Seg &g, bool keep, uint32_t pix) {
+    const uint32_t slot = wave_alloc(g.l_act, keep ? 1u : 0u);
+    if (keep) g.act_out[slot] = pix;
+}
+
+__device__ __forceinline__ void put_ray(float4 *rays, uint32_t idx, f3 o, f3 d, float remain, uint32_t kind) {
+    rays[2u * idx] = make_float4(o.x, o.y, o.z, remain);
+    rays[2u * idx + 1u] = make_float4(d.x, d.y, d.z, asf(kind));
+}
+__device__ __forceinline__ Hit get_hit(const float4 *res, uint32_t idx) {
+    const float4 a = res[2u * idx], b = res[2u * idx + 1u];
+    const uint32_t enc = asu(a.y);
+    Hit h;
+    h.valid = (enc >> 31) != 0u;
+    h.t = a.x;
+    h.s = Compact{enc >> 31, (enc >> 16) & 0x7fffu, enc & 0xffffu, asu(a.z), a.w, b.x};
+    h.pos = mk(b.y, b.z, b.w);
+    return h;
+}
+__device__ __forceinline__ f3 x0_of(const Scene &sc, uint32_t x, uint32_t y) {  // Get_X0, PT_1:732-738
+    const float *vpinv = reinterpret_cast<const float *>(sc.U + U_VPINV);
+    float u = ((float)x + 0.5f) / (float)sc.U[U_W];
+    float v = ((float)y + 0.5f) / (float)sc.U[U_H];
+    return xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
+}
+__device__ __forceinline__ Compact gdecode(uint4 g) {
+    return Compact{(g.x & 0x80000000u) ? 1u : 0u, (g.x & 0x7fff0000u) >> 16, g.x & 0xffffu, g.y, asf(g.z), asf(g.w)};
+}
+__device__ __forceinline__ uint4 gencode(const Compact &s) {
+    return make_uint4((s.valid << 31) | (s.inst << 16) | s.mat, s.prim, asu(s.bu), asu(s.bv));
+}
+__device__ __forceinline__ void mix_color(const Scene &sc, float4 *accum, uint32_t i, f3 c) {
+    float t = 1.0f / (float)(sc.U[U_FRAME] + 1u);  // WriteColor, PT_4:599-606
+    float4 a = accum[i];
+    accum[i] = make_float4(mixf(a.x, c.x, t), mixf(a.y, c.y, t), mixf(a.z, c.z, t), 1.0f);
+}
+// pixel -> (x, y) for the start kernels: 8x8 tiles so a wave's first rays are coherent
+__device__ __forceinline__ bool tile_xy(const Scene &sc, uint32_t p, uint32_t &x, uint32_t &y) {
+    const uint32_t tiles_x = (sc.width + 7u) / 8u, t = p >> 6, l = p & 63u;
+    x = (t % tiles_x) * 8u + (l & 7u);
+    y = sc.row_begin + (t / tiles_x) * 8u + (l >> 3);
+    return x < sc.width && y < sc.row_end;
+}
+__device__ __forceinline__ uint32_t padded_pixels(const Scene &sc) {
+    return ((sc.width + 7u) / 8u) * ((sc.row_end - sc.row_begin + 7u) / 8u) * 64u;
+}
+
+// ---------------------------------------------------------------- trace queue
+// Workgroup j traces ray segment j of `round`.  A Visibility query is traced with its
+// hit range capped at the remaining distance to the light: Visibility only looks at the
+// closest hit when its t <= remain, and the cap leaves the visit order -- hence which of
+// several equal-t triangles wins -- unchanged for every hit inside the cap.
+template <bool COUNT>
+__global__ __launch_bounds__(WB) void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
+    extern __shared__ uint32_t wstack[];
+    uint32_t *stack = wstack + threadIdx.x;
+    const uint32_t j = blockIdx.x;
+    const uint32_t n = w.cnt[(2u * round + 1u) * w.nseg + j];
+    const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
+    float4 *res = w.res[round & 1u] + 2u * (size_t)j * w.ray_stride;
+    for (uint32_t i = threadIdx.x; i < n; i += WB) {
+        const float4 a = rays[2u * i], b = rays[2u * i + 1u];
+        Ray r{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)};
+        const bool vis = asu(b.w) == Q_VIS;
+        // Visibility (SH/PT_1_InitPass.wgsl:774-802) walks through transmissive hits:
+        // one trace site, looped, so the traversal code is emitted once
+        float T = 1.0f, remain = a.w;
+        for (uint32_t it = 0u;; ++it) {
+            const Hit h = trace_core<COUNT>(sc, r, eps, stack, WB, vis ? fminf(remain, 1e10f) : 1e10f);
+            if (!vis) {
+                const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
+                res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
+                res[2u * i + 1u] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
+                break;
+            }
+            float out = -1.0f;
+            if (!h.valid || h.t > remain) out = T;
+            else {
+                const float tr = get_transmission(sc, h.s.inst, h.s.mat);
+                if (tr == 0.0f) out = 0.0f;
+                else {
+                    T *= tr;
+                    remain -= h.t;
+                    r.o = h.pos;
+                    if (it == 4u) out = 0.0f;  // Visibility gives up after 5 segments
+                }
+            }
+            if (out >= 0.0f) {  // only res.x is written: .yzw and res[2i+1] carry the payload
+                res[2u * i].x = out;
+                break;
+            }
+        }
+    }
+}
+
+// =========================================================================== PT_1 (init)
+// Pixel state, SoA float4 slots (slot k of pixel p at state[k * npix + p]).
+enum : uint32_t { IS_HDR, IS_FP, IS_RES, IS_X, IS_XL, IS_L, IS_BSEED, IS_CS2, IS_CS3, IS_COUNT };
+// flags (IS_HDR.y >> 8): bit0 selected, bit1 has BSDF ray, bit2 far12, bit3 far23,
+// bit4 rough1 >= 0.5, bit5 rough2 >= 0.5, bits 8-9 Lobe[1], bits 10-11 Lobe[2]
+enum : uint32_t { F_SEL = 1u, F_BSDF = 2u, F_FAR12 = 4u, F_FAR23 = 8u, F_R1 = 16u, F_R2 = 32u };
+
+struct WInit {
+    uint32_t seed, i, flags, C, vis_idx, bsdf_idx;
+    f3 f; float p;
+    float w_sum, p_hat_sel, pdf_env;
+    f3 xpos; float xrough;
+    f3 xlpos; uint32_t nee_seed;
+    f3 L;
+    uint32_t bseed1, bseed2;
+};
+__device__ __forceinline__ uint32_t lobe_of(uint32_t flags, uint32_t k) { return (flags >> (8u + 2u * (k - 1u))) & 3u; }
+
+// CompressPath for the candidate (vertex i, NEE or env) -- same rules as ptx_persist.hip.
+__device__ __forceinline__ void wcompress(const Scene &sc, const WInit &s, const float4 *state, uint32_t npix,
+                                          uint32_t pix, bool is_env, const LightSample &XL, uint4 *out) {
+    const uint32_t i = s.i, length = i + 1u;
+    const uint32_t L1 = (i > 1u || is_env) ? lobe_of(s.flags, 1u) : 0u;
+    const uint32_t L2 = (i > 2u || (is_env && i == 2u)) ? lobe_of(s.flags, 2u) : 0u;
+    const uint32_t s2 = (i >= 2u || is_env) ? s.bseed1 : s.nee_seed;
+    const uint32_t s3 = (i >= 3u || (i == 2u && is_env)) ? s.bseed2 : (i == 2u ? s.nee_seed : 0u);
+    const uint32_t s4 = (i == 3u) ? s.nee_seed : 0u;
+    uint32_t k = 0u;
+    if (length > 2u) {
+        bool ok = (L1 == LOBE_LAMBERT || (s.flags & F_R1)) && (L2 == LOBE_LAMBERT || (s.flags & F_R2));
+        if ((s.flags & F_FAR12) && ok) k = 2u;
+    }
+    if (k == 0u && length > 3u) {
+        bool ok = (L2 == LOBE_LAMBERT || (s.flags & F_R2));
+        if ((s.flags & F_FAR23) && ok) k = 3u;
+    }
+    if (k == 0u) {
+        bool rough = s.xrough >= RECONNECTION_ROUGHNESS;
+        bool dirl = XL.type == LIGHT_DIRECTION || XL.type == LIGHT_ENV;
+        if ((dirl || length3(s.xpos - XL.pos) >= RECONNECTION_DISTANCE) && rough) k = length;
+    }
+    uint4 rc = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t lk = 0u, lk1 = 0u;
+    if (k == length) {
+        lk = LOBE_LIGHT;
+        lk1 = (k == 2u) ? L1 : (k == 3u) ? L2 : 0u;
+    } else if (k == 2u) {
+        lk = L2; lk1 = L1;
+        const float4 c = state[IS_CS2 * npix + pix];
+        rc = make_uint4(asu(c.x), asu(c.y), asu(c.z), asu(c.w));
+    } else if (k == 3u) {
+        lk1 = L2;
+        const float4 c = state[IS_CS3 * npix + pix];
+        rc = make_uint4(asu(c.x), asu(c.y), asu(c.z), asu(c.w));
+    }
+    out[0] = make_uint4(s2, s3, s4, 0u);
+    out[1] = make_uint4(asu(XL.dir.x), asu(XL.dir.y), asu(XL.dir.z), XL.type);
+    out[2] = make_uint4(asu(XL.pos.x), asu(XL.pos.y), asu(XL.pos.z), (uint32_t)XL.id);
+    out[3] = make_uint4(asu(XL.Le.x), asu(XL.Le.y), asu(XL.Le.z), asu(XL.pdf));
+    out[4] = rc;
+    out[5] = make_uint4(k, lk1, lk, length);
+    out[6] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// Vertex i of the path tree up to (not including) its traces (PT_1:1403-1442): NEE sample,
+// its contribution before Visibility, the UpdateReservoir draw, BSDF sample, throughput,
+// Russian roulette.  Emits the shadow ray (payload in its result slot) and the BSDF ray.
+// Called by every lane of the wave (queue slots are reserved per wave); `emit` selects
+// the lanes that actually have a vertex.
+__device__ __forceinline__ void winit_vertex(const Scene &sc, const Seg &g, bool emit, WInit &s, const Surface &X,
+                                             f3 prev) {
+    float4 *rays = g.rays, *res = g.res_out;
+    const uint32_t vbase = g.rbase + wave_alloc(g.l_ray, emit ? 1u : 0u);
+    bool bsdf_ray = false;
+    if (emit) {
+        const f3 V = normalize(prev - X.pos);
+        s.nee_seed = s.seed;
+        const LightSample XL = sample_nee(sc, s.seed, X, V);
+        const f3 Ln = direction_to_light(X, XL);
+        f3 contrib = s.f * l_emit<false>(XL, X);
+        contrib = contrib * bsdf(X, V, Ln);
+        contrib = contrib * fabsf(dot(X.nrm, Ln));
+        const float denom = s.p * XL.pdf;
+        const float u_update = rnd(s.seed);
+        s.xlpos = XL.pos;
+        s.xpos = X.pos;
+        s.xrough = X.mat.rough;
+        s.vis_idx = vbase;
+        const float dist = length(XL.pos - X.pos);
+        put_ray(rays, vbase, X.pos, (XL.pos - X.pos) / dist, dist, Q_VIS);
+        res[2u * vbase] = make_float4(0.0f, contrib.x, contrib.y, contrib.z);
+        res[2u * vbase + 1u] = make_float4(denom, u_update, XL.pdf, asf((uint32_t)XL.id));
+        if (s.i < 3u) {
+            if (s.i == 1u) s.bseed1 = s.seed;
+            else s.bseed2 = s.seed;
+            uint32_t lobe;
+            const f3 Lb = sample_bsdf(s.seed, X, V, lobe);
+            s.flags |= lobe << (8u + 2u * (s.i - 1u));
+            s.f = s.f * (bsdf(X, V, Lb) * fabsf(dot(X.nrm, Lb)));
+            const float pdfv = pdf_bsdf(X, V, Lb);
+            s.p *= pdfv;
+            const float ps = luminance(s.f) / s.p;
+            if (rnd(s.seed) < ps) {
+                s.p *= ps;
+                s.pdf_env = pdfv;
+                s.L = Lb;
+                bsdf_ray = true;
+            }
+        }
+        s.flags = bsdf_ray ? (s.flags | F_BSDF) : (s.flags & ~F_BSDF);
+    }
+    const uint32_t bbase = g.rbase + wave_alloc(g.l_ray, bsdf_ray ? 1u : 0u);
+    if (bsdf_ray) {
+        s.bsdf_idx = bbase;
+        put_ray(rays, bbase, s.xpos, s.L, -1.0f, Q_CLOSEST);
+    }
+}
+
+__device__ __forceinline__ void winit_store(float4 *state, uint32_t npix, uint32_t pix, const WInit &s) {
+    state[IS_HDR * npix + pix] = make_float4(asf(s.seed), asf(s.i | (s.flags << 8)), asf(s.C), asf(s.vis_idx));
+    state[IS_FP * npix + pix] = make_float4(s.f.x, s.f.y, s.f.z, s.p);
+    state[IS_RES * npix + pix] = make_float4(s.w_sum, s.p_hat_sel, s.pdf_env, asf(s.bsdf_idx));
+    state[IS_X * npix + pix] = make_float4(s.xpos.x, s.xpos.y, s.xpos.z, s.xrough);
+    state[IS_XL * npix + pix] = make_float4(s.xlpos.x, s.xlpos.y, s.xlpos.z, asf(s.nee_seed));
+    state[IS_L * npix + pix] = make_float4(s.L.x, s.L.y, s.L.z, 0.0f);
+    state[IS_BSEED * npix + pix] = make_float4(asf(s.bseed1), asf(s.bseed2), 0.0f, 0.0f);
+}
+__device__ __forceinline__ void winit_load(const float4 *state, uint32_t npix, uint32_t pix, WInit &s) {
+    const float4 h = state[IS_HDR * npix + pix], fp = state[IS_FP * npix + pix], r = state[IS_RES * npix + pix];
+    const float4 x = state[IS_X * npix + pix], xl = state[IS_XL * npix + pix], l = state[IS_L * npix + pix];
+    const float4 b = state[IS_BSEED * npix + pix];
+    s.seed = asu(h.x); s.i = asu(h.y) & 0xffu; s.flags = asu(h.y) >> 8; s.C = asu(h.z); s.vis_idx = asu(h.w);
+    s.f = mk(fp.x, fp.y, fp.z); s.p = fp.w;
+    s.w_sum = r.x; s.p_hat_sel = r.y; s.pdf_env = r.z; s.bsdf_idx = asu(r.w);
+    s.xpos = mk(x.x, x.y, x.z); s.xrough = x.w;
+    s.xlpos = mk(xl.x, xl.y, xl.z); s.nee_seed = asu(xl.w);
+    s.L = mk(l.x, l.y, l.z);
+    s.bseed1 = asu(b.x); s.bseed2 = asu(b.y);
+}
+__device__ __forceinline__ void winit_finish(const WInit &s, uint4 *reservoir, uint32_t pix) {
+    uint4 *out = reservoir + 8u * (size_t)pix;
+    if (!(s.flags & F_SEL))  // zero Path(): length 0, k 0 (no candidate ever accepted)
+        for (int q = 0; q < 7; ++q) out[q] = make_uint4(0u, 0u, 0u, 0u);
+    out[7] = make_uint4(asu(s.w_sum / s.p_hat_sel), s.C, 0u, 0u);
+}
+
+__global__ __launch_bounds__(WB) void winit_start(Scene sc, WaveBufs w, const uint4 *gbuf, uint4 *reservoir) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    float4 *state = w.state;
+    const uint32_t npix = w.npix, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {  // workgroup-uniform loop
+        const uint32_t q = seg_pixel(w, g.j, k);
+        uint32_t x, y, pix = 0u;
+        bool active = false;
+        WInit s;
+        Surface X;
+        f3 prev;
+        if (q < np && tile_xy(sc, q, x, y)) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            const Compact x1 = gdecode(gbuf[pix]);
+            if (!x1.valid) {  // reservoir unobservable: PT_4 returns before LoadReservoir (:1404-1408)
+                uint4 *out = reservoir + 8u * (size_t)pix;
+                for (int k = 0; k < 8; ++k) out[k] = make_uint4(0u, 0u, 0u, 0u);
+            } else {
+                active = true;
+                s.seed = pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u);
+                s.i = 1u; s.flags = 0u; s.C = 0u;
+                s.f = mk(1.0f, 1.0f, 1.0f); s.p = 1.0f;
+                s.w_sum = 0.0f; s.p_hat_sel = 0.0f; s.pdf_env = 0.0f;
+                s.L = mk(0.0f, 0.0f, 0.0f); s.bseed1 = 0u; s.bseed2 = 0u; s.bsdf_idx = 0u;
+                prev = x0_of(sc, x, y);
+                X = get_surface(sc, x1);
+                if (X.mat.rough >= RECONNECTION_ROUGHNESS) s.flags |= F_R1;
+            }
+        }
+        // ray emission is executed by the whole wave (wave_alloc), active or not
+        winit_vertex(sc, g, active, s, X, prev);
+        if (active) winit_store(state, npix, pix, s);
+        seg_keep(g, active, pix);
+    }
+    seg_end(w, g);
+}
+
+__global__ __launch_bounds__(WB) void winit_step(Scene sc, WaveBufs w, uint32_t round, uint4 *reservoir) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, round, lds);
+    float4 *state = w.state;
+    const float4 *res_in = g.res_in;
+    const uint32_t npix = w.npix, n = g.n_in;
+    for (uint32_t base = 0; base < n; base += WB) {
+        const uint32_t q = base + threadIdx.x;
+        bool emit = false;
+        uint32_t pix = 0u;
+        WInit s;
+        Surface X;
+        f3 prev;
+        if (q < n) {
+            pix = g.act_in[q];
+            winit_load(state, npix, pix, s);
+            // 1. resolve the NEE candidate of vertex i with its Visibility (PT_1:1413-1421)
+            const float4 a = res_in[2u * s.vis_idx], b = res_in[2u * s.vis_idx + 1u];
+            const f3 contrib = mk(a.y, a.z, a.w) * a.x;
+            const float p_hat = luminance(contrib);
+            const float ris = p_hat / b.x;
+            s.C += 1u;
+            s.w_sum += ris;
+            if (b.y < ris / s.w_sum) {
+                s.flags |= F_SEL;
+                s.p_hat_sel = p_hat;
+                LightSample XL;
+                const Light ls = get_light(sc, asu(b.w));
+                XL.id = (int32_t)asu(b.w);
+                XL.type = ls.type;
+                XL.Le = ls.color * ls.intensity;
+                XL.pos = s.xlpos;
+                XL.pdf = b.z;
+                XL.dir = ls.type == LIGHT_DIRECTION ? ls.dir
+                         : ls.type == LIGHT_POINT  ? normalize(s.xpos - ls.pos)
+                         : ls.type == LIGHT_RECT   ? normalize(s.xpos - s.xlpos)
+                                                   : mk(0.0f, 0.0f, 0.0f);
+                wcompress(sc, s, state, npix, pix, false, XL, reservoir + 8u * (size_t)pix);
+            }
+            if (!(s.flags & F_BSDF)) {
+                winit_finish(s, reservoir, pix);  // i == 3 or Russian roulette ended the path
+            } else {
+                const Hit h = get_hit(res_in, s.bsdf_idx);
+                if (!h.valid) {  // 2a. BSDF ray escaped: env candidate (PT_1:1447-1461)
+                    const float u = rnd(s.seed);
+                    const float ph = luminance(s.f * ENV_C);
+                    const float ris_e = ph / s.p;
+                    s.C += 1u;
+                    s.w_sum += ris_e;
+                    if (u < ris_e / s.w_sum) {
+                        s.flags |= F_SEL;
+                        s.p_hat_sel = ph;
+                        LightSample env;
+                        env.pos = s.xpos + s.L * INF_F;
+                        env.type = LIGHT_ENV;
+                        env.dir = -s.L;
+                        env.id = -1;
+                        env.Le = mk(ENV_C, ENV_C, ENV_C);
+                        env.pdf = s.pdf_env;
+                        wcompress(sc, s, state, npix, pix, true, env, reservoir + 8u * (size_t)pix);
+                    }
+                    winit_finish(s, reservoir, pix);
+                } else {  // 2b. next vertex (PT_1:1464-1468)
+                    X = surface_at(sc, h.s, h.pos);
+                    prev = s.xpos;
+                    s.i += 1u;
+                    if (s.i == 2u) {
+                        if (length3(prev - X.pos) >= RECONNECTION_DISTANCE) s.flags |= F_FAR12;
+                        if (X.mat.rough >= RECONNECTION_ROUGHNESS) s.flags |= F_R2;
+                        const uint4 e = gencode(h.s);
+                        state[IS_CS2 * npix + pix] = make_float4(asf(e.x), asf(e.y), asf(e.z), asf(e.w));
+                    } else {
+                        if (length3(prev - X.pos) >= RECONNECTION_DISTANCE) s.flags |= F_FAR23;
+                        const uint4 e = gencode(h.s);
+                        state[IS_CS3 * npix + pix] = make_float4(asf(e.x), asf(e.y), asf(e.z), asf(e.w));
+                    }
+                    emit = true;
+                }
+            }
+        }
+        winit_vertex(sc, g, emit, s, X, prev);
+        if (emit) winit_store(state, npix, pix, s);
+        seg_keep(g, emit, pix);
+    }
+    seg_end(w, g);
+}
+
+// =========================================================================== PT_4 (final)
+enum : uint32_t { FS_HDR, FS_F, FS_CUR, FS_NRM, FS_PREV, FS_COUNT };
+// HDR: {i | length<<8 | phase<<16, seed1 (rSeed[1]), ray idx, -}; F: {f.xyz, UCW};
+// CUR: {cur.pos, inst|mat}; NRM: {cur.nrm, -}; PREV: {prev.pos, -}
+
+struct WFinal {
+    uint32_t i, length, phase, seed1, idx;
+    f3 f; float ucw;
+    Surface cur;
+    f3 prev;
+};
+__device__ __forceinline__ LightSample load_xl(const uint4 *res) {
+    const uint4 r1 = res[1], r2 = res[2], r3 = res[3];
+    LightSample XL;
+    XL.dir = mk(asf(r1.x), asf(r1.y), asf(r1.z));
+    XL.type = r1.w;
+    XL.pos = mk(asf(r2.x), asf(r2.y), asf(r2.z));
+    XL.id = (int32_t)r2.w;
+    XL.Le = mk(asf(r3.x), asf(r3.y), asf(r3.z));
+    XL.pdf = asf(r3.w);
+    return XL;
+}
+// Either the next RegeneratePath BSDF ray or the light segment's Visibility ray.
+// Called by every lane of the wave; `emit` selects the lanes with a ray.
+__device__ __forceinline__ void wfinal_emit(const Scene &sc, const Seg &g, bool emit, WFinal &s, const uint4 *resv) {
+    float4 *rays = g.rays, *res = g.res_out;
+    const uint32_t idx = g.rbase + wave_alloc(g.l_ray, emit ? 1u : 0u);
+    if (!emit) return;
+    const f3 V = normalize(s.prev - s.cur.pos);
+    s.idx = idx;
+    if (s.i + 1u < s.length) {  // RegeneratePath step i (PT_4:1367-1381), seed rSeed[i-1]
+        uint32_t seed = s.i == 1u ? resv[0].x : s.seed1;
+        uint32_t lobe;
+        const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
+        s.phase = 0u;
+        put_ray(rays, idx, s.cur.pos, dir, -1.0f, Q_CLOSEST);
+    } else {  // PathContribution's light segment (PT_4:1323-1333)
+        const LightSample XL = load_xl(resv);
+        const f3 L = direction_to_light(s.cur, XL);
+        s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+        const f3 Le = l_emit<true>(XL, s.cur);
+        s.phase = 1u;
+        const float dist = length(XL.pos - s.cur.pos);
+        put_ray(rays, idx, s.cur.pos, (XL.pos - s.cur.pos) / dist, dist, Q_VIS);
+        res[2u * idx] = make_float4(0.0f, Le.x, Le.y, Le.z);
+    }
+}
+__device__ __forceinline__ void wfinal_store(float4 *state, uint32_t npix, uint32_t pix, const WFinal &s,
+                                             uint32_t matref) {
+    state[FS_HDR * npix + pix] = make_float4(asf(s.i | (s.length << 8) | (s.phase << 16)), asf(s.seed1),
+                                             asf(s.idx), 0.0f);
+    state[FS_F * npix + pix] = make_float4(s.f.x, s.f.y, s.f.z, s.ucw);
+    state[FS_CUR * npix + pix] = make_float4(s.cur.pos.x, s.cur.pos.y, s.cur.pos.z, asf(matref));
+    state[FS_NRM * npix + pix] = make_float4(s.cur.nrm.x, s.cur.nrm.y, s.cur.nrm.z, 0.0f);
+    state[FS_PREV * npix + pix] = make_float4(s.prev.x, s.prev.y, s.prev.z, 0.0f);
+}
+
+__global__ __launch_bounds__(WB) void wfinal_start(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir,
+                                                   float4 *accum) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    float4 *state = w.state;
+    const uint32_t npix = w.npix, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, g.j, k);
+        uint32_t x, y, pix = 0u, matref = 0u;
+        bool active = false;
+        WFinal s;
+        if (q < np && tile_xy(sc, q, x, y)) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            const Compact x1 = gdecode(gbuf[pix]);
+            const uint4 *rv = reservoir + 8u * (size_t)pix;
+            if (!x1.valid) {
+                accum[pix] = make_float4(ENV_C, ENV_C, ENV_C, 1.0f);
+            } else {
+                const uint4 r0 = rv[0], r5 = rv[5], r7 = rv[7];
+                s.length = r5.w;
+                if (r7.y == 0u || s.length < 2u) {
+                    mix_color(sc, accum, pix, mk(0.0f, 0.0f, 0.0f));
+                } else {
+                    active = true;
+                    s.seed1 = r0.y;
+                    s.ucw = asf(r7.x);
+                    s.prev = x0_of(sc, x, y);
+                    s.cur = get_surface(sc, x1);
+                    matref = (x1.inst << 16) | x1.mat;
+                    s.f = mk(1.0f, 1.0f, 1.0f);
+                    s.i = 1u;
+                }
+            }
+        }
+        wfinal_emit(sc, g, active, s, reservoir + 8u * (size_t)pix);
+        if (active) wfinal_store(state, npix, pix, s, matref);
+        seg_keep(g, active, pix);
+    }
+    seg_end(w, g);
+}
+
+__global__ __launch_bounds__(WB) void wfinal_step(Scene sc, WaveBufs w, uint32_t round, const uint4 *reservoir,
+                                                  float4 *accum) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, round, lds);
+    float4 *state = w.state;
+    const float4 *res_in = g.res_in;
+    const uint32_t npix = w.npix, n = g.n_in;
+    for (uint32_t base = 0; base < n; base += WB) {
+        const uint32_t q = base + threadIdx.x;
+        bool emit = false;
+        uint32_t pix = 0u, matref = 0u;
+        WFinal s;
+        if (q < n) {
+            pix = g.act_in[q];
+            const float4 hd = state[FS_HDR * npix + pix], fv = state[FS_F * npix + pix];
+            const float4 cu = state[FS_CUR * npix + pix], nr = state[FS_NRM * npix + pix];
+            const float4 pv = state[FS_PREV * npix + pix];
+            const uint32_t w = asu(hd.x);
+            s.i = w & 0xffu; s.length = (w >> 8) & 0xffu; s.phase = w >> 16;
+            s.seed1 = asu(hd.y); s.idx = asu(hd.z);
+            s.f = mk(fv.x, fv.y, fv.z); s.ucw = fv.w;
+            s.prev = mk(pv.x, pv.y, pv.z);
+            matref = asu(cu.w);
+            const Inst &I = sc.insts[matref >> 16];
+            s.cur.pos = mk(cu.x, cu.y, cu.z);
+            s.cur.nrm = mk(nr.x, nr.y, nr.z);
+            s.cur.mat = get_material(sc, desc_ptr(sc, I.mesh), matref & 0xffffu);
+            if (s.phase == 0u) {  // regenerated vertex i+1 (PT_4:1378-1380) and f over vertex i
+                const Hit h = get_hit(res_in, s.idx);
+                const Surface next = h.valid ? surface_at(sc, h.s, h.pos) : get_surface(sc, h.s);
+                const f3 V = normalize(s.prev - s.cur.pos);
+                const f3 L = normalize(next.pos - s.cur.pos);
+                s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+                s.prev = s.cur.pos;
+                s.cur = next;
+                matref = (h.s.inst << 16) | h.s.mat;
+                s.i += 1u;
+                emit = true;
+            } else {  // light segment's Visibility arrived (PT_4:1332)
+                const float4 a = res_in[2u * s.idx];
+                s.f = s.f * (mk(a.y, a.z, a.w) * a.x);
+                mix_color(sc, accum, pix, s.f * s.ucw);
+            }
+        }
+        wfinal_emit(sc, g, emit, s, reservoir + 8u * (size_t)pix);
+        if (emit) wfinal_store(state, npix, pix, s, matref);
+        seg_keep(g, emit, pix);
+    }
+    seg_end(w, g);
+}
+
+// =========================================================================== TEST_MCPT
+enum : uint32_t { MS_HDR, MS_COL, MS_FP, MS_ORG, MS_COUNT };
+// HDR: {seed, bounce | flags<<8, light-ray base idx, path ray idx}; COL: {color, -};
+// FP: {f, p}; ORG: {path ray origin (for V), -}.  flags: 1 = path ray pending
+struct WMcpt {
+    uint32_t seed, bounce, flags, lbase, pidx;
+    f3 color, f;
+    float p;
+    f3 org;
+};
+__device__ __forceinline__ void wmcpt_store(float4 *state, uint32_t npix, uint32_t pix, const WMcpt &s) {
+    state[MS_HDR * npix + pix] = make_float4(asf(s.seed), asf(s.bounce | (s.flags << 8)), asf(s.lbase), asf(s.pidx));
+    state[MS_COL * npix + pix] = make_float4(s.color.x, s.color.y, s.color.z, 0.0f);
+    state[MS_FP * npix + pix] = make_float4(s.f.x, s.f.y, s.f.z, s.p);
+    state[MS_ORG * npix + pix] = make_float4(s.org.x, s.org.y, s.org.z, 0.0f);
+}
+// GetLightColor of light `id` up to its Visibility (TEST_MCPT:1261-1308); the shadow ray
+// goes to queue slot `idx`, the light term {c, pdf, f/p} into that slot's result record.
+__device__ __forceinline__ void mcpt_light_ray(const Scene &sc, uint32_t &seed, const Surface &X, f3 V, f3 fp,
+                                               uint32_t id, uint32_t idx, float4 *rays, float4 *res) {
+    const Light ls = get_light(sc, id);
+    LightSample XL;
+    XL.type = ls.type;
+    XL.Le = ls.color * ls.intensity;
+    XL.pos = mk(0.0f, 0.0f, 0.0f);
+    XL.dir = mk(0.0f, 0.0f, 0.0f);
+    XL.pdf = 0.0f;
+    if (ls.type == LIGHT_DIRECTION) {
+        XL.pos = X.pos - ls.dir * INF_F; XL.dir = ls.dir; XL.pdf = 1.0f;
+    } else if (ls.type == LIGHT_POINT) {
+        XL.pos = ls.pos; XL.dir = normalize(X.pos - ls.pos); XL.pdf = 1.0f;
+    } else if (ls.type == LIGHT_RECT) {
+        const float ru = rnd(seed) * 2.0f - 1.0f;
+        const float rv = rnd(seed) * 2.0f - 1.0f;
+        XL.pos = ls.pos + (ls.U * ru + ls.V * rv);
+        XL.dir = normalize(X.pos - XL.pos);
+        const f3 rr = XL.pos - X.pos;
+        const f3 Ld = normalize(rr);
+        XL.pdf = dot(rr, rr) / fmaxf(ls.area * fabsf(dot(ls.dir, Ld)), EPS_F);
+    }
+    const f3 L = direction_to_light(X, XL);
+    f3 c = l_emit<false>(XL, X) * bsdf(X, V, L);
+    c = c * fabsf(dot(X.nrm, L));
+    const float dist = length(XL.pos - X.pos);
+    put_ray(rays, idx, X.pos, (XL.pos - X.pos) / dist, dist, Q_VIS);
+    res[2u * idx] = make_float4(0.0f, c.x, c.y, c.z);
+    res[2u * idx + 1u] = make_float4(XL.pdf, fp.x, fp.y, fp.z);
+}
+
+// At a path vertex: every light's GetLightColor up to its Visibility (TEST_MCPT:1261-1308),
+// then the BSDF sample + Russian roulette (:1356-1366).  Light terms ride in their shadow
+// rays' result slots: {T, c.xyz | pdf, (f/p).xyz}.  Called by every lane of the wave;
+// `emit` selects the lanes with a vertex.
+__device__ __forceinline__ void wmcpt_vertex(const Scene &sc, const Seg &g, bool emit, WMcpt &s, const Surface &X) {
+    float4 *rays = g.rays, *res = g.res_out;
+    const uint32_t nl = sc.U[U_LIGHT_COUNT];
+    const uint32_t lbase = g.rbase + wave_alloc(g.l_ray, emit ? nl : 0u);
+    bool path_ray = false;
+    f3 Lb = mk(0.0f, 0.0f, 0.0f);
+    if (emit) {
+        const f3 V = normalize(s.org - X.pos);
+        const f3 fp = s.f / s.p;
+        for (uint32_t id = 0; id < nl; ++id) mcpt_light_ray(sc, s.seed, X, V, fp, id, lbase + id, rays, res);
+        s.lbase = lbase;
+        uint32_t lobe;
+        Lb = sample_bsdf(s.seed, X, V, lobe);
+        s.f = s.f * (bsdf(X, V, Lb) * fabsf(dot(X.nrm, Lb)));
+        s.p *= pdf_bsdf(X, V, Lb);
+        s.org = X.pos;
+        const float ps = luminance(s.f) / s.p;
+        if (rnd(s.seed) < ps) {
+            s.p *= ps;
+            s.bounce += 1u;
+            path_ray = s.bounce < 3u;
+        }
+        s.flags = path_ray ? 1u : 0u;
+    }
+    const uint32_t pidx = g.rbase + wave_alloc(g.l_ray, path_ray ? 1u : 0u);
+    if (path_ray) {
+        s.pidx = pidx;
+        put_ray(rays, pidx, s.org, Lb, -1.0f, Q_CLOSEST);
+    }
+}
+
+__global__ __launch_bounds__(WB) void wmcpt_start(Scene sc, WaveBufs w) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    float4 *state = w.state, *rays = g.rays;
+    const uint32_t npix = w.npix, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, g.j, k);
+        uint32_t x, y, pix = 0u;
+        const bool active = q < np && tile_xy(sc, q, x, y);
+        WMcpt s;
+        const uint32_t idx = g.rbase + wave_alloc(g.l_ray, active ? 1u : 0u);
+        if (active) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            s.seed = pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u);
+            const float *vpinv = reinterpret_cast<const float *>(sc.U + U_VPINV);  // PT_01:496-507
+            const float u = ((float)x + 0.5f) / (float)sc.U[U_W];
+            const float v = ((float)y + 0.5f) / (float)sc.U[U_H];
+            const f3 st = xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
+            const f3 en = xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f + 1.0f));
+            s.org = st;
+            s.bounce = 0u; s.flags = 1u; s.lbase = 0u; s.pidx = idx;
+            s.color = mk(0.0f, 0.0f, 0.0f); s.f = mk(1.0f, 1.0f, 1.0f); s.p = 1.0f;
+            put_ray(rays, idx, st, normalize(en - st), -1.0f, Q_CLOSEST);
+            wmcpt_store(state, npix, pix, s);
+        }
+        seg_keep(g, active, pix);
+    }
+    seg_end(w, g);
+}
+
+template <int FIRST>
+__global__ __launch_bounds__(WB) void wmcpt_step(Scene sc, WaveBufs w, uint32_t round, float4 *accum) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, round, lds);
+    float4 *state = w.state;
+    const float4 *res_in = g.res_in;
+    const uint32_t npix = w.npix, n = g.n_in;
+    const uint32_t nl = sc.U[U_LIGHT_COUNT];
+    for (uint32_t base = 0; base < n; base += WB) {
+        const uint32_t q = base + threadIdx.x;
+        bool emit = false;
+        uint32_t pix = 0u;
+        WMcpt s;
+        Surface X;
+        if (q < n) {
+            pix = g.act_in[q];
+            const float4 hd = state[MS_HDR * npix + pix], co = state[MS_COL * npix + pix];
+            const float4 fp = state[MS_FP * npix + pix], og = state[MS_ORG * npix + pix];
+            s.seed = asu(hd.x); s.bounce = asu(hd.y) & 0xffu; s.flags = asu(hd.y) >> 8;
+            s.lbase = asu(hd.z); s.pidx = asu(hd.w);
+            s.color = mk(co.x, co.y, co.z); s.f = mk(fp.x, fp.y, fp.z); s.p = fp.w;
+            s.org = mk(og.x, og.y, og.z);
+            // 1. light terms of the previous vertex, in light order (TEST_MCPT:1351-1354)
+            if (!FIRST) {
+                for (uint32_t id = 0; id < nl; ++id) {
+                    const float4 a = res_in[2u * (s.lbase + id)], b = res_in[2u * (s.lbase + id) + 1u];
+                    const f3 term = (mk(a.y, a.z, a.w) * a.x) / b.x;
+                    s.color = s.color + mk(b.y, b.z, b.w) * term;
+                }
+            }
+            if (!(s.flags & 1u)) {
+                mix_color(sc, accum, pix, s.color);  // RR ended the path or 3 bounces done
+            } else {
+                const Hit h = get_hit(res_in, s.pidx);
+                if (!h.valid) {  // escaped: environment (TEST_MCPT:1340-1344)
+                    s.color = s.color + (s.f / s.p) * ENV_C;
+                    mix_color(sc, accum, pix, s.color);
+                } else {
+                    X = surface_at(sc, h.s, h.pos);
+                    emit = true;
+                }
+            }
+        }
+        wmcpt_vertex(sc, g, emit, s, X);
+        if (emit) wmcpt_store(state, npix, pix, s);
+        seg_keep(g, emit, pix);
+    }
+    seg_end(w, g);
+}
+
+// =========================================================================== host side
+hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t depth, hipStream_t s) {
+    const PassEps eps = eps_mode == 0 ? PassEps{1e-8f, 1e-6f} : PassEps{1e-4f, 1e-8f};
+    const size_t lds = stack_lds_bytes(depth);
+    if (sc.counters)
+        hipLaunchKernelGGL(trace_queue<true>, dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+    else
+        hipLaunchKernelGGL(trace_queue<false>, dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+    return hipGetLastError();
+}
+
+// Logic round r consumes the results of trace round r-1 and emits the rays of trace round r.
+hipError_t wave_init_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, uint4 *reservoir,
+                           hipStream_t s) {
+    if (round == 0)
+        hipLaunchKernelGGL(winit_start, dim3(w.nseg), dim3(WB), 0, s, sc, w, gbuf, reservoir);
+    else
+        hipLaunchKernelGGL(winit_step, dim3(w.nseg), dim3(WB), 0, s, sc, w, (uint32_t)round, reservoir);
+    return hipGetLastError();
+}
+
+hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, const uint4 *reservoir,
+                            float4 *accum, hipStream_t s) {
+    if (round == 0)
+        hipLaunchKernelGGL(wfinal_start, dim3(w.nseg), dim3(WB), 0, s, sc, w, gbuf, reservoir, accum);
+    else
+        hipLaunchKernelGGL(wfinal_step, dim3(w.nseg), dim3(WB), 0, s, sc, w, (uint32_t)round, reservoir, accum);
+    return hipGetLastError();
+}
+
+hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, hipStream_t s) {
+    if (round == 0)
+        hipLaunchKernelGGL(wmcpt_start, dim3(w.nseg), dim3(WB), 0, s, sc, w);
+    else if (round == 1)
+        hipLaunchKernelGGL(wmcpt_step<1>, dim3(w.nseg), dim3(WB), 0, s, sc, w, (uint32_t)round, accum);
+    else
+        hipLaunchKernelGGL(wmcpt_step<0>, dim3(w.nseg), dim3(WB), 0, s, sc, w, (uint32_t)round, accum);
+    return hipGetLastError();
+}
+
+}  // namespace ptx

@@ -19,14 +19,14 @@ from .scene.world import CompiledScene, World, serialize_world
 
 class Renderer:
     def __init__(self, width: int, height: int, device: int = -1, pipeline: str = "restir",
-                 row_begin: int = 0, row_end: int = 0, count_work: bool = False, simple: bool = False):
+                 row_begin: int = 0, row_end: int = 0, count_work: bool = False, variant: str = "wave"):
         self._lib = N.load()
         self.width, self.height = int(width), int(height)
         self.pipeline = pipeline
         cfg = N.PtxConfig(width=self.width, height=self.height, row_begin=row_begin, row_end=row_end,
                           device=device,
                           pipeline=N.PTX_PIPELINE_MCPT if pipeline == "mcpt" else N.PTX_PIPELINE_RESTIR,
-                          flags=(N.PTX_FLAG_COUNT_WORK if count_work else 0) | (N.PTX_FLAG_SIMPLE_KERNELS if simple else 0))
+                          flags=(N.PTX_FLAG_COUNT_WORK if count_work else 0) | N.VARIANT_FLAGS[variant])
         self._h = ctypes.c_void_p()
         rc = self._lib.ptx_create(ctypes.byref(cfg), ctypes.byref(self._h))
         if rc != N.PTX_OK:
@@ -117,6 +117,14 @@ class Renderer:
         return {"frames": s.frames, "kernel_ms_total": list(s.kernel_ms_total),
                 "kernel_launches": list(s.kernel_launches), "triangles": s.triangles, "bvh_nodes": s.bvh_nodes,
                 "instances": s.instances, "max_bvh_depth": s.max_bvh_depth, "device_bytes": s.device_bytes}
+
+    def trace(self, rays: np.ndarray, eps_mode: int = 1) -> np.ndarray:
+        """Closest hits for an (n, 8) f32 ray array {o.xyz, d.xyz, -, -}; returns (n, 8) f32
+        {t, flags|inst|mat bits, prim bits, bary.x, bary.y, pos.xyz} (include/ptx.h)."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        hits = np.zeros_like(rays)
+        self._call("ptx_trace", self._h, rays.ctypes.data, hits.ctypes.data, len(rays), eps_mode)
+        return hits
 
     def reset_stats(self) -> None:
         self._call("ptx_reset_stats", self._h)

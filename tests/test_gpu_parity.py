@@ -116,6 +116,34 @@ def test_mcpt(scene1, oracle_mod, native, W, H):
     assert err <= 1e-3
 
 
+@pytest.mark.parametrize("variant", ["tiled", "persistent", "simple"])
+def test_alternate_variants(scene1, oracle_mod, native, variant):
+    """The A/B kernel variants obey the same bars as the default wavefront path."""
+    W, H = 96, 64
+    fr = oracle_frame(oracle_mod, scene1, W, H)
+    fr.run(oracle_mod.PASS_GBUFFER)
+    fr.run(oracle_mod.PASS_INIT)
+    fr.run(oracle_mod.PASS_FINAL)
+    r = make_renderer(scene1, W, H, variant=variant)
+    r.set_uniform(fr.uniform)
+    r.write_buffer(native.PTX_BUF_GBUFFER, fr.gbuffer)
+    r.run_pass(native.PTX_PASS_INIT)
+    res = r.read_reservoir()
+    valid = (fr.gbuffer[..., 0] >> 31) == 1
+    ints = [0, 1, 2, 3, 7, 11, 20, 21, 22, 23, 29]
+    assert np.all(res[..., ints] == fr.reservoir[..., ints], axis=-1)[valid].mean() >= 0.999
+    r.write_buffer(native.PTX_BUF_RESERVOIR, fr.reservoir)
+    r.reset_accumulation()
+    r.run_pass(native.PTX_PASS_FINAL)
+    assert rel_l2(r.read_image()[..., :3], fr.accum[..., :3]) <= 1e-3
+    fm = oracle_frame(oracle_mod, scene1, W, H)
+    fm.run(oracle_mod.PASS_MCPT)
+    m = make_renderer(scene1, W, H, pipeline="mcpt", variant=variant)
+    m.set_uniform(fm.uniform)
+    m.run_pass(native.PTX_PASS_MCPT)
+    assert rel_l2(m.read_image()[..., :3], fm.accum[..., :3]) <= 1e-3
+
+
 def test_restir_pipeline_4_frames(scene1, oracle_mod):
     """Config C1 shape: 256x256, FrameIndex 1..4 accumulated through the Renderer surface."""
     W = H = 256
@@ -150,6 +178,25 @@ def test_band_split_is_bit_identical(scene1, oracle_mod):
         b.Render()
         parts.append(b.read_image())
     np.testing.assert_array_equal(np.concatenate(parts, axis=0), ref)
+
+
+@pytest.mark.parametrize("eps_mode", [0, 1])
+def test_trace_queries_bit_exact(scene1, oracle_mod, eps_mode):
+    """ptx_trace on random rays (origins in and around the room) == oracle TraceRay, bit for bit."""
+    rng = np.random.default_rng(42 + eps_mode)
+    n = 4096
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = rng.uniform([-4, -2.2, -7.5], [4, 3.1, 5.0], size=(n, 3))
+    d = rng.normal(size=(n, 3))
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:64, 3:6] = [0.0, 0.0, -1.0]          # axis-aligned directions (1/0 = inf slabs)
+    fr = oracle_frame(oracle_mod, scene1, 32, 32)
+    ref = fr.trace(rays, eps_mode)
+    r = make_renderer(scene1, 32, 32)
+    r.set_uniform(fr.uniform)
+    got = r.trace(rays, eps_mode)
+    np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert (got[:, 1].view(np.uint32) >> 31).mean() > 0.5
 
 
 def test_work_counters_match_oracle(scene1, oracle_mod, native):
