@@ -52,6 +52,9 @@ def lib():
         _lib.pto_pcg.restype = ctypes.c_uint32
         _lib.pto_random.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
         _lib.pto_random.restype = ctypes.c_float
+        for fn in ("pto_sin", "pto_cos", "pto_pow5"):
+            getattr(_lib, fn).argtypes = [ctypes.c_float]
+            getattr(_lib, fn).restype = ctypes.c_float
         _lib.pto_bsdf.argtypes = [P, P, P, P, P]
         _lib.pto_pdf_bsdf.argtypes = [P, P, P, P]
         _lib.pto_pdf_bsdf.restype = ctypes.c_float
@@ -85,8 +88,8 @@ class Frame:
     def set_frame_index(self, f: int):
         self.uniform[23] = f
 
-    def trace(self, rays: np.ndarray, eps_mode: int = 1) -> np.ndarray:
-        """Closest hits for (n, 8) f32 rays, same format as ptx_trace."""
+    def trace(self, rays: np.ndarray, eps_mode: int = 1, return_counters: bool = False):
+        """Closest hits for (n, 8) f32 rays, same format as ptx_trace (+ the traversal work)."""
         rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
         hits = np.zeros_like(rays)
         inp = Inputs(self.uniform.ctypes.data, self.scene.ctypes.data, self.geometry.ctypes.data,
@@ -94,7 +97,7 @@ class Frame:
         cnt = Counters()
         lib().pto_trace(ctypes.byref(inp), _ptr(rays), _ptr(hits), len(rays), eps_mode, ctypes.byref(cnt))
         self.counters["trace"] = cnt.as_dict()
-        return hits
+        return (hits, self.counters["trace"]) if return_counters else hits
 
     def run(self, pass_id: int, threads: int = 0, rect=None) -> dict:
         threads = threads or os.cpu_count() or 1
@@ -112,6 +115,19 @@ class Frame:
 
 def pcg(seed: int) -> int:
     return int(lib().pto_pcg(seed & 0xFFFFFFFF))
+
+
+def fixed_sin(x: float) -> float:
+    """The fixed f32 sin both sides use for BSDF sampling angles (x >= 0)."""
+    return float(lib().pto_sin(x))
+
+
+def fixed_cos(x: float) -> float:
+    return float(lib().pto_cos(x))
+
+
+def fixed_pow5(x: float) -> float:
+    return float(lib().pto_pow5(x))
 
 
 def bsdf(n, mat, v, l) -> np.ndarray:

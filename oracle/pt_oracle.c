@@ -387,8 +387,42 @@ static float geom_shadow(float NdotV, float NdotL, float R) {
     float K = r * r / 8.0f;
     return 1.0f / ((NdotV * (1.0f - K) + K) * (NdotL * (1.0f - K) + K));
 }
+/* WGSL pow / sin / cos are implementation-defined (pow is exp2(y*log2(x)) on most
+ * WebGPU backends; sin/cos carry an absolute error bound of 2^-11).  Both sides of the
+ * parity check use the same fixed f32 definitions below instead of libm, so the oracle
+ * and the HIP path agree bit for bit (each is within ~2 ulp of the true function).
+ * pow(x, 5): two squarings and a product. */
+static inline float pow5_(float x) {
+    float x2 = x * x;
+    return (x2 * x2) * x;
+}
+/* sin and cos of x >= 0 (the only use: BSDF sampling angles 2*PI_F*u, u in [0,1]).
+ * Cody-Waite reduction by pi/4 in three parts (the first exact for the octant counts
+ * used), then the classic single-precision minimax polynomials on [-pi/4, pi/4]. */
+static void sincos_(float x, float *s, float *c) {
+    int j = (int)(x * 1.27323954473516f);
+    float y = (float)j;
+    if (j & 1) {
+        j += 1;
+        y += 1.0f;
+    }
+    j &= 7;
+    float z = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    float zz = z * z;
+    float ps = ((-1.9515295891e-4f * zz + 8.3321608736e-3f) * zz - 1.6666654611e-1f) * zz * z + z;
+    float pc = ((2.443315711809948e-5f * zz - 1.388731625493765e-3f) * zz + 4.166664568298827e-2f) * zz * zz -
+               0.5f * zz + 1.0f;
+    if (j == 0) { *s = ps; *c = pc; }
+    else if (j == 2) { *s = pc; *c = -ps; }
+    else if (j == 4) { *s = -ps; *c = -pc; }
+    else { *s = -pc; *c = ps; }
+}
+float pto_sin(float x) { float s, c; sincos_(x, &s, &c); return s; }
+float pto_cos(float x) { float s, c; sincos_(x, &s, &c); return c; }
+float pto_pow5(float x) { return pow5_(x); }
+
 static v3 fresnel(float d, v3 F0) {
-    float p = powf(1.0f - saturate_(d), 5.0f);
+    float p = pow5_(1.0f - saturate_(d));
     return V3(F0.x + (1.0f - F0.x) * p, F0.y + (1.0f - F0.y) * p, F0.z + (1.0f - F0.z) * p);
 }
 static v3 brdf(const surface *X, v3 V, v3 L) {
@@ -461,16 +495,18 @@ static inline v3 refract_(v3 I, v3 N, float eta) {
 static v3 sample_cosine(uint32_t *seed) {
     float r1 = pto_random(seed), r2 = pto_random(seed);
     float R = sqrtf(r1);
-    float phi = 2.0f * PI_F * r2;
-    return V3(R * cosf(phi), R * sinf(phi), sqrtf(1.0f - r1));
+    float phi = 2.0f * PI_F * r2, sp, cp;
+    sincos_(phi, &sp, &cp);
+    return V3(R * cp, R * sp, sqrtf(1.0f - r1));
 }
 static v3 sample_ggx(uint32_t *seed, float R) {
     float r1 = pto_random(seed), r2 = pto_random(seed);
     float a = R * R;
     float phi = 2.0f * PI_F * r1;
     float ct = sqrtf((1.0f - r2) / (1.0f + (a * a - 1.0f) * r2));
-    float st = sqrtf(1.0f - ct * ct);
-    return vnormalize(V3(st * cosf(phi), st * sinf(phi), ct));
+    float st = sqrtf(1.0f - ct * ct), sp, cp;
+    sincos_(phi, &sp, &cp);
+    return vnormalize(V3(st * cp, st * sp, ct));
 }
 static v3 sample_brdf(uint32_t *seed, const surface *X, v3 V, uint32_t *lobe) {
     float metal = X->mat.metalness;

@@ -72,6 +72,10 @@ void pto_trace(const pto_inputs *in, const float *rays, float *hits, size_t n, i
 /* Known-answer helpers (SH/PT_1_InitPass.wgsl:810-826). */
 uint32_t pto_pcg(uint32_t seed);
 float pto_random(uint32_t *seed);
+/* fixed f32 sin/cos (x >= 0) and pow(x, 5) shared with the HIP path (see pt_oracle.c) */
+float pto_sin(float x);
+float pto_cos(float x);
+float pto_pow5(float x);
 
 /* BSDF / PDF known-answer helpers on an explicit surface (SH/PT_1_InitPass.wgsl:834-1245).
  * mat = {albedo r,g,b, metalness, roughness, transmission, ior} AFTER GetMaterial's tweaks. */

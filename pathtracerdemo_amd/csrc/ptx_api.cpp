@@ -588,8 +588,11 @@ int ptx_trace_device(ptx_handle *h, const void *rays_dev, void *hits_dev, size_t
     resolve_event(t, h);
     Scene sc = make_scene(h);
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
-    hipError_t e = launch_trace_rays(sc, (const float4 *)rays_dev, (float4 *)hits_dev, (uint32_t)n, eps_mode,
-                                     h->stack_depth, h->stream);
+    // one thread per ray with the SIMPLE_KERNELS flag; otherwise the lane-refill kernel the
+    // wavefront passes trace with
+    const bool simple = (h->cfg.flags & PTX_FLAG_SIMPLE_KERNELS) != 0;
+    hipError_t e = (simple ? launch_trace_rays : launch_trace_rays_sm)(
+        sc, (const float4 *)rays_dev, (float4 *)hits_dev, (uint32_t)n, eps_mode, h->stack_depth, h->stream);
     if (e != hipSuccess) return fail(h, PTX_E_HIP, "trace launch: %s", hipGetErrorString(e));
     HIP_CHECK(h, hipEventRecord(t.stop, h->stream));
     t.pass = PTX_PASS_TRACE;

@@ -211,12 +211,27 @@ __device__ __forceinline__ void barycentric(f3 P, f3 A, f3 B, f3 C, float eps, f
     by = u;
 }
 
+// Barycentrics and world position of a closest hit whose inst/prim/t are set.
+__device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, PassEps eps, Hit &best) {
+    best.s.valid = 1u;
+    const Inst &I = sc.insts[best.s.inst];
+    const uint32_t *desc = desc_ptr(sc, I.mesh);
+    uint32_t id[3];
+    tri_vertex_ids(sc, desc, best.s.prim, id);
+    f3 A = xform_point(I.m, vtx_pos(sc, desc, id[0]));
+    f3 B = xform_point(I.m, vtx_pos(sc, desc, id[1]));
+    f3 C = xform_point(I.m, vtx_pos(sc, desc, id[2]));
+    f3 P = ray.o + ray.d * best.t;
+    barycentric(P, A, B, C, eps.bary_eps, best.s.bu, best.s.bv);
+    const float U = best.s.bu, V = best.s.bv, W = 1.0f - U - V;
+    best.pos = (A * U + B * V) + C * W;
+}
 // TraceRay (SH/PT_1_InitPass.wgsl:605-715; PT_01:509-621): closest hit over every
 // instance and sub-mesh root, ordered-stack BLAS traversal, ties replace (`if (best < t)
 // continue`).  `stack` is this thread's column of the workgroup's LDS stack
 // (entry k at stack[k * stride]).  Also returns the hit position exactly as
 // GetSurface(hit).Position computes it (same world-space vertices and barycentrics).
-template <bool COUNT>
+template <bool COUNT, bool SPEC = false>
 __device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack, uint32_t stride,
                                           float t_max = 1e10f) {
     Hit best;
@@ -242,10 +257,28 @@ __device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps,
             if (!box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) continue;
             int sp = 0;
             stack[0] = R.ref;
-            while (sp >= 0) {
-                uint32_t ref = stack[(uint32_t)sp * stride];
-                --sp;
-                if (!(ref & LEAF_BIT)) {
+            // while-while traversal: lanes descend interior nodes until each has a leaf (or an
+            // empty stack), then the wave processes leaves together.  Per lane the pops, tests
+            // and pushes happen in exactly the if/else order of the reference loop.
+            // SPEC (speculative): a lane holding a leaf keeps descending while another lane of
+            // the wave still has none, postponing it; a second leaf ends its descent.  Leaves
+            // are still processed in discovery order and every extra visit is a box beyond
+            // the current best hit, so the hit -- ties included -- is unchanged; only the
+            // AABB/triangle work counts grow, hence SPEC is off in counting builds.
+            uint32_t leaf = 0u, leaf2 = 0u;
+            for (;;) {
+                while (sp >= 0 && (SPEC || leaf == 0u)) {
+                    const uint32_t ref = stack[(uint32_t)sp * stride];
+                    --sp;
+                    if (ref & LEAF_BIT) {
+                        if (leaf == 0u) {
+                            leaf = ref;
+                            if (!SPEC || !__any(leaf == 0u)) break;
+                            continue;
+                        }
+                        leaf2 = ref;
+                        break;
+                    }
                     const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + ref);
                     float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
                     float lmin[3] = {q0.x, q0.y, q0.z}, lmax[3] = {q0.w, q1.x, q1.y};
@@ -265,10 +298,13 @@ __device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps,
                         stack[(uint32_t)(sp + 1) * stride] = hl ? lref : rref;
                         sp += 1;
                     }
-                    continue;
+                    if (SPEC && !__any(leaf == 0u)) break;
                 }
-                const uint32_t first = ref & LEAF_FIRST_MASK;
-                const uint32_t count = (ref >> 24) & 0x7Fu;
+                if (leaf == 0u) break;  // stack exhausted
+                const uint32_t first = leaf & LEAF_FIRST_MASK;
+                const uint32_t count = (leaf >> 24) & 0x7Fu;
+                leaf = leaf2;
+                leaf2 = 0u;
                 const float4 *tp = sc.tris + 3u * (I.tri_base + first);
                 for (uint32_t k = 0; k < count; ++k) {
                     float4 a = tp[3u * k + 0u], b = tp[3u * k + 1u], c = tp[3u * k + 2u];
@@ -293,18 +329,7 @@ __device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps,
     }
     if (best.valid) {
         best.t = vy;
-        best.s.valid = 1u;
-        const Inst &I = sc.insts[best.s.inst];
-        const uint32_t *desc = desc_ptr(sc, I.mesh);
-        uint32_t id[3];
-        tri_vertex_ids(sc, desc, best.s.prim, id);
-        f3 A = xform_point(I.m, vtx_pos(sc, desc, id[0]));
-        f3 B = xform_point(I.m, vtx_pos(sc, desc, id[1]));
-        f3 C = xform_point(I.m, vtx_pos(sc, desc, id[2]));
-        f3 P = ray.o + ray.d * best.t;
-        barycentric(P, A, B, C, eps.bary_eps, best.s.bu, best.s.bv);
-        const float U = best.s.bu, V = best.s.bv, W = 1.0f - U - V;
-        best.pos = (A * U + B * V) + C * W;
+        complete_hit(sc, ray, eps, best);
     }
     return best;
 }

@@ -31,7 +31,7 @@ hipError_t launch_mcpt_persistent(const Scene &sc, float4 *accum, unsigned int *
 hipError_t launch_trace_rays(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
                              uint32_t stack_depth, hipStream_t s);
 
-// tile + LDS ray-exchange variants (ptx_persist.hip): the default
+// tile + LDS ray-exchange variants (ptx_persist.hip): A/B
 hipError_t launch_init_tiled(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, uint32_t stack_depth,
                              hipStream_t s);
 hipError_t launch_final_tiled(const Scene &sc, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
@@ -64,6 +64,8 @@ hipError_t wave_init_round(const Scene &sc, const WaveBufs &w, int round, const 
                            hipStream_t s);
 hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, const uint4 *reservoir,
                             float4 *accum, hipStream_t s);
+hipError_t launch_trace_rays_sm(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
+                                uint32_t stack_depth, hipStream_t s);
 hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, hipStream_t s);
 
 }  // namespace ptx

@@ -106,8 +106,34 @@ __device__ __forceinline__ float geom_shadow(float NdotV, float NdotL, float R) 
     float K = r * r / 8.0f;
     return 1.0f / ((NdotV * (1.0f - K) + K) * (NdotL * (1.0f - K) + K));
 }
+// Fixed f32 pow(x, 5) / sin / cos shared with the oracle (oracle/pt_oracle.c pow5_,
+// sincos_): WGSL leaves them implementation-defined, and one definition on both sides
+// keeps the whole path bit-exact (libm and ocml differ in the last ulp).  ~2 ulp of true.
+__device__ __forceinline__ float pow5(float x) {
+    float x2 = x * x;
+    return (x2 * x2) * x;
+}
+// x >= 0 only (BSDF sampling angles): Cody-Waite reduction by pi/4, minimax polynomials.
+__device__ __forceinline__ void fsincos(float x, float &s, float &c) {
+    int j = (int)(x * 1.27323954473516f);
+    float y = (float)j;
+    if (j & 1) {
+        j += 1;
+        y += 1.0f;
+    }
+    j &= 7;
+    float z = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    float zz = z * z;
+    float ps = ((-1.9515295891e-4f * zz + 8.3321608736e-3f) * zz - 1.6666654611e-1f) * zz * z + z;
+    float pc = ((2.443315711809948e-5f * zz - 1.388731625493765e-3f) * zz + 4.166664568298827e-2f) * zz * zz -
+               0.5f * zz + 1.0f;
+    const bool swap = (j & 2) != 0;           // octants 2, 6: sin <- cos poly, cos <- sin poly
+    const float sv = swap ? pc : ps, cv = swap ? ps : pc;
+    s = (j == 4 || j == 6) ? -sv : sv;        // sin negative in octants 4, 6
+    c = (j == 2 || j == 4) ? -cv : cv;        // cos negative in octants 2, 4
+}
 __device__ __forceinline__ f3 fresnel(float d, f3 F0) {
-    float p = powf(1.0f - saturate(d), 5.0f);
+    float p = pow5(1.0f - saturate(d));
     return mk(F0.x + (1.0f - F0.x) * p, F0.y + (1.0f - F0.y) * p, F0.z + (1.0f - F0.z) * p);
 }
 __device__ __forceinline__ f3 brdf(const Surface &X, f3 V, f3 L) {
@@ -173,16 +199,18 @@ __device__ __forceinline__ f3 refract3(f3 I, f3 N, float eta) {
 __device__ __forceinline__ f3 sample_cosine(uint32_t &seed) {
     float r1 = rnd(seed), r2 = rnd(seed);
     float R = __builtin_sqrtf(r1);
-    float phi = 2.0f * PI_F * r2;
-    return mk(R * cosf(phi), R * sinf(phi), __builtin_sqrtf(1.0f - r1));
+    float phi = 2.0f * PI_F * r2, sp, cp;
+    fsincos(phi, sp, cp);
+    return mk(R * cp, R * sp, __builtin_sqrtf(1.0f - r1));
 }
 __device__ __forceinline__ f3 sample_ggx(uint32_t &seed, float R) {
     float r1 = rnd(seed), r2 = rnd(seed);
     float a = R * R;
     float phi = 2.0f * PI_F * r1;
     float ct = __builtin_sqrtf((1.0f - r2) / (1.0f + (a * a - 1.0f) * r2));
-    float st = __builtin_sqrtf(1.0f - ct * ct);
-    return normalize(mk(st * cosf(phi), st * sinf(phi), ct));
+    float st = __builtin_sqrtf(1.0f - ct * ct), sp, cp;
+    fsincos(phi, sp, cp);
+    return normalize(mk(st * cp, st * sp, ct));
 }
 __device__ __forceinline__ f3 sample_bsdf(uint32_t &seed, const Surface &X, f3 V, uint32_t &lobe) {
     bool transparent = rnd(seed) < X.mat.trans;

@@ -28,6 +28,8 @@
 #include "ptx_launch.h"
 #include "ptx_shading.h"
 
+#include <cstdlib>
+
 namespace ptx {
 
 constexpr uint32_t WB = kBlock;
@@ -152,8 +154,9 @@ __device__ __forceinline__ uint32_t padded_pixels(const Scene &sc) {
 // hit range capped at the remaining distance to the light: Visibility only looks at the
 // closest hit when its t <= remain, and the cap leaves the visit order -- hence which of
 // several equal-t triangles wins -- unchanged for every hit inside the cap.
-template <bool COUNT>
-__global__ __launch_bounds__(WB) void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
+template <bool COUNT, int WAVES, bool SPEC>
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
+void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     extern __shared__ uint32_t wstack[];
     uint32_t *stack = wstack + threadIdx.x;
     const uint32_t j = blockIdx.x;
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(WB) void trace_queue(Scene sc, WaveBufs w, uint32_t
         // one trace site, looped, so the traversal code is emitted once
         float T = 1.0f, remain = a.w;
         for (uint32_t it = 0u;; ++it) {
-            const Hit h = trace_core<COUNT>(sc, r, eps, stack, WB, vis ? fminf(remain, 1e10f) : 1e10f);
+            const Hit h = trace_core<COUNT, SPEC>(sc, r, eps, stack, WB, vis ? fminf(remain, 1e10f) : 1e10f);
             if (!vis) {
                 const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
                 res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
@@ -190,6 +193,181 @@ __global__ __launch_bounds__(WB) void trace_queue(Scene sc, WaveBufs w, uint32_t
             if (out >= 0.0f) {  // only res.x is written: .yzw and res[2i+1] carry the payload
                 res[2u * i].x = out;
                 break;
+            }
+        }
+    }
+}
+
+// Lane-refill form of the same queries.  The whole traversal -- instance loop, sub-root
+// loop, BLAS stack walk, leaf triangle loop and the Visibility continuation -- is one
+// flat per-lane state machine: every iteration a lane does ONE unit of work (a node-pair
+// test, a triangle test, or a root/instance step), and a lane whose ray is done takes
+// the segment's next ray at once instead of idling until the wave's slowest ray ends.
+// Per ray the visit order (and so the hit, ties included, and the work counters) is the
+// reference's exactly: only the interleaving across lanes changes.
+// Workgroup j handles segment j: `cnt` given -> cnt[j] rays at j * stride (queue layout
+// {o, remain}, {d, kind}); `cnt` null -> rays [j * stride, min((j+1) * stride, n_total))
+// in the public ptx_trace layout {o.xyz, d.x}, {d.yz, -, -} (closest hit only).
+template <bool COUNT>
+__global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *rays_all, float4 *res_all,
+                                                     const uint32_t *cnt, uint32_t stride, uint32_t n_total,
+                                                     PassEps eps) {
+    extern __shared__ uint32_t wstack[];
+    uint32_t *stack = wstack + threadIdx.x;
+    const uint32_t j = blockIdx.x;
+    const bool pub = cnt == nullptr;
+    const uint32_t n = pub ? min(stride, n_total - j * stride) : cnt[j];
+    const float4 *rays = rays_all + 2u * (size_t)j * stride;
+    float4 *res = res_all + 2u * (size_t)j * stride;
+    const float vx = 1e-4f;
+    const uint32_t n_inst = sc.n_inst;
+
+    uint32_t next = threadIdx.x, cur = 0u;
+    bool have = false;
+    Ray r{};                       // world ray of the current trace
+    bool vis = false;              // Visibility query (else closest hit)
+    float T = 1.0f, remain = 0.0f; // Visibility product / remaining distance
+    uint32_t vit = 0u;             // Visibility segment (0..4)
+    uint32_t ii = 0u, s = 0u, nsub = 0u, grp = 0u, sub_base = 0u, tri_base = 0u;
+    f3 lo{}, ld{}, inv{};          // ray in the current instance's space
+    int sp = -1;
+    uint32_t tcount = 0u, tprim = 0u, tidx = 0u;  // leaf cursor
+    float vy = 1e10f;
+    bool bvalid = false;
+    uint32_t binst = 0u, bmat = 0u, bprim = 0u;
+    uint32_t n_aabb = 0u, n_tri = 0u;
+
+    for (;;) {
+        if (!have && next < n) {  // fetch the next ray of the segment
+            cur = next;
+            next += WB;
+            const float4 a = rays[2u * cur], b = rays[2u * cur + 1u];
+            r = pub ? Ray{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y)} : Ray{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)};
+            vis = !pub && asu(b.w) == Q_VIS;
+            T = 1.0f;
+            remain = a.w;
+            vit = 0u;
+            have = true;
+            ii = 0xffffffffu; s = 0u; nsub = 0u; sp = -1; tcount = 0u;
+            vy = vis ? fminf(remain, 1e10f) : 1e10f;
+            bvalid = false; n_aabb = 0u; n_tri = 0u;
+        }
+        if (__ballot(have) == 0ull) break;
+        if (!have) continue;
+
+        bool do_node = false;
+        uint32_t node = 0u;
+        if (tcount == 0u) {
+            if (sp >= 0) {
+                const uint32_t ref = stack[(uint32_t)sp * WB];
+                --sp;
+                if (ref & LEAF_BIT) {
+                    tcount = (ref >> 24) & 0x7Fu;
+                    tprim = ref & LEAF_FIRST_MASK;
+                    tidx = 3u * (tri_base + tprim);
+                } else {
+                    do_node = true;
+                    node = ref;
+                }
+            } else if (s < nsub) {  // next sub-mesh root of this instance
+                const SubRoot &R = sc.subs[sub_base + s];
+                grp = s;
+                ++s;
+                ++n_aabb;
+                float tn;
+                if (box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) {
+                    sp = 0;
+                    stack[0] = R.ref;
+                }
+            } else if (ii + 1u < n_inst) {  // next instance (ii starts at ~0u: wraps to 0)
+                ii = ii + 1u;
+                const Inst &I = sc.insts[ii];
+                lo = xform_point(I.minv, r.o);
+                const f3 le = xform_point(I.minv, r.o + r.d);
+                ld = le - lo;
+                inv = mk(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
+                nsub = I.nsub;
+                sub_base = I.sub_base;
+                tri_base = I.tri_base;
+                s = 0u;
+            } else {  // this trace is complete
+                if (COUNT) {
+                    atomicAdd(&sc.counters[CNT_RAYS], 1ull);
+                    atomicAdd(&sc.counters[CNT_INST], (unsigned long long)n_inst);
+                    atomicAdd(&sc.counters[CNT_AABB], (unsigned long long)n_aabb);
+                    atomicAdd(&sc.counters[CNT_TRI], (unsigned long long)n_tri);
+                    if (bvalid) atomicAdd(&sc.counters[CNT_HITS], 1ull);
+                }
+                Hit h;
+                h.valid = bvalid;
+                h.t = bvalid ? vy : 0.0f;
+                h.s = Compact{0u, bvalid ? binst : 0u, bvalid ? bmat : 0u, bvalid ? bprim : 0u, 0.0f, 0.0f};
+                h.pos = mk(0.0f, 0.0f, 0.0f);
+                if (!vis) {
+                    if (bvalid) complete_hit(sc, r, eps, h);
+                    const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
+                    res[2u * cur] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
+                    res[2u * cur + 1u] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
+                    have = false;
+                } else {  // Visibility step (SH/PT_1_InitPass.wgsl:774-802)
+                    float out = -1.0f;
+                    if (!h.valid || h.t > remain) out = T;
+                    else {
+                        const float tr = get_transmission(sc, h.s.inst, h.s.mat);
+                        if (tr == 0.0f) out = 0.0f;
+                        else {
+                            T *= tr;
+                            remain -= h.t;
+                            if (vit == 4u) out = 0.0f;  // gives up after 5 segments
+                            else {
+                                complete_hit(sc, r, eps, h);
+                                r.o = h.pos;
+                                ++vit;
+                                ii = 0xffffffffu; s = 0u; nsub = 0u; sp = -1; tcount = 0u;
+                                vy = fminf(remain, 1e10f);
+                                bvalid = false; n_aabb = 0u; n_tri = 0u;
+                            }
+                        }
+                    }
+                    if (out >= 0.0f) {  // only res.x: .yzw and res[2i+1] carry the payload
+                        res[2u * cur].x = out;
+                        have = false;
+                    }
+                }
+                continue;
+            }
+        }
+        if (tcount > 0u) {  // one triangle of the current leaf
+            const float4 a = sc.tris[tidx], b = sc.tris[tidx + 1u], c = sc.tris[tidx + 2u];
+            const float t = ray_tri(lo, ld, a, b, c, eps.det_eps);
+            ++n_tri;
+            if (!(vy < t)) {
+                vy = t;
+                bvalid = true;
+                binst = ii;
+                bmat = grp;
+                bprim = tprim;
+            }
+            tidx += 3u;
+            ++tprim;
+            --tcount;
+        } else if (do_node) {  // one interior node: both children, nearer on top
+            const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + node);
+            const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+            const float lmin[3] = {q0.x, q0.y, q0.z}, lmax[3] = {q0.w, q1.x, q1.y};
+            const float rmin[3] = {q1.z, q1.w, q2.x}, rmax[3] = {q2.y, q2.z, q2.w};
+            const uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
+            float tl, tr;
+            const bool hl = box_overlap(lo, inv, lmin, lmax, vx, vy, tl);
+            const bool hr = box_overlap(lo, inv, rmin, rmax, vx, vy, tr);
+            n_aabb += 2u;
+            if (hl && hr) {
+                stack[(uint32_t)(sp + 1) * WB] = tl < tr ? rref : lref;
+                stack[(uint32_t)(sp + 2) * WB] = tl < tr ? lref : rref;
+                sp += 2;
+            } else if (hl || hr) {
+                stack[(uint32_t)(sp + 1) * WB] = hl ? lref : rref;
+                sp += 1;
             }
         }
     }
@@ -783,10 +961,44 @@ __global__ __launch_bounds__(WB) void wmcpt_step(Scene sc, WaveBufs w, uint32_t 
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t depth, hipStream_t s) {
     const PassEps eps = eps_mode == 0 ? PassEps{1e-8f, 1e-6f} : PassEps{1e-4f, 1e-8f};
     const size_t lds = stack_lds_bytes(depth);
+    static const bool refill = getenv("PTX_TRACE_REFILL") != nullptr;  // A/B switch for profiling
+    if (refill) {
+        const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.nseg;
+        float4 *res = w.res[round & 1];
+        if (sc.counters)
+            hipLaunchKernelGGL(trace_queue_sm<true>, dim3(w.nseg), dim3(WB), lds, s, sc, w.rays, res, cnt,
+                               w.ray_stride, 0u, eps);
+        else
+            hipLaunchKernelGGL(trace_queue_sm<false>, dim3(w.nseg), dim3(WB), lds, s, sc, w.rays, res, cnt,
+                               w.ray_stride, 0u, eps);
+    } else if (sc.counters)
+        hipLaunchKernelGGL((trace_queue<true, 6, false>), dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+    else {
+        // A/B switches (profiling only): occupancy target and speculative traversal.  8 waves
+        // per SIMD measured ~2% faster than 6 despite a small spill; speculation is neutral.
+        static const int occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 8;
+        static const bool spec = getenv("PTX_TRACE_SPEC") != nullptr;
+        auto k = spec       ? trace_queue<false, 8, true>
+                 : occ >= 8 ? trace_queue<false, 8, false>
+                 : occ == 7 ? trace_queue<false, 7, false> : trace_queue<false, 6, false>;
+        hipLaunchKernelGGL(k, dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+    }
+    return hipGetLastError();
+}
+
+// ptx_trace / ptx_trace_device queries (public ray layout) through the same kernel.
+hipError_t launch_trace_rays_sm(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
+                                uint32_t depth, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const PassEps eps = eps_mode == 0 ? PassEps{1e-8f, 1e-6f} : PassEps{1e-4f, 1e-8f};
+    const uint32_t per_wg = 4u * WB;
+    const dim3 grid((n + per_wg - 1u) / per_wg);
     if (sc.counters)
-        hipLaunchKernelGGL(trace_queue<true>, dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+        hipLaunchKernelGGL(trace_queue_sm<true>, grid, dim3(WB), stack_lds_bytes(depth), s, sc, rays, hits, nullptr,
+                           per_wg, n, eps);
     else
-        hipLaunchKernelGGL(trace_queue<false>, dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+        hipLaunchKernelGGL(trace_queue_sm<false>, grid, dim3(WB), stack_lds_bytes(depth), s, sc, rays, hits, nullptr,
+                           per_wg, n, eps);
     return hipGetLastError();
 }
 

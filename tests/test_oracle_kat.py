@@ -116,3 +116,21 @@ def test_pdf_brdf_integrates_to_about_one(oracle_mod):
     vals = np.array([oracle_mod.pdf_bsdf(n, mat, v, l) for l in dirs])
     est = vals.mean() * 2 * np.pi
     assert 0.85 < est < 1.15
+
+
+def test_fixed_transcendentals_are_faithful(oracle_mod):
+    """The shared f32 sin/cos/pow5 (both sides use them instead of libm/ocml) stay within
+    2 ulp of the float64 truth over the sampling domain [0, 2*PI_F] (plus pow5 on [0, 1])."""
+    xs = np.float32(2.0 * 3.141592) * np.linspace(0.0, 1.0, 20001, dtype=np.float32)
+    xs = np.concatenate([xs, np.float32([0.0, 1e-30, 1e-7, 0.7853981, 0.7853982, 6.283184])])
+    for fn, ref in ((oracle_mod.fixed_sin, np.sin), (oracle_mod.fixed_cos, np.cos)):
+        got = np.array([fn(float(x)) for x in xs], np.float32)
+        truth = ref(xs.astype(np.float64))
+        ulp = np.spacing(np.maximum(np.abs(truth), 2.0 ** -24).astype(np.float32)).astype(np.float64)
+        err = np.abs(got.astype(np.float64) - truth) / ulp
+        assert err.max() <= 2.0, (fn.__name__, float(xs[np.argmax(err)]), err.max())
+    ps = np.linspace(0.0, 1.0, 5001, dtype=np.float32)
+    got = np.array([oracle_mod.fixed_pow5(float(p)) for p in ps], np.float32).astype(np.float64)
+    truth = ps.astype(np.float64) ** 5
+    ulp = np.spacing(np.maximum(truth, 2.0 ** -126).astype(np.float32)).astype(np.float64)
+    assert (np.abs(got - truth) / ulp).max() <= 3.0
