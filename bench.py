@@ -79,7 +79,7 @@ def main():
 
     # work census of the exact frame (counting build, untimed): algorithmic bytes
     rc = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
-                  count_work=True)
+                  count_work=True, variant=args.variant)
     rc.Initialize(cs)
     rc.Update()
     passes = ["gbuffer", "init", "final"] if pipeline == "restir" else ["mcpt"]
@@ -123,6 +123,28 @@ def main():
     img = r.read_image()
     nonfinite = int((~np.isfinite(img[..., :3])).sum())
 
+    # Second timed region, same K steps, with HIP events around every wavefront launch
+    # (PTX_FLAG_TIME_LAUNCHES costs ~5% of a frame, so the headline region above runs
+    # without them): per-launch durations of the dominant kernel for the roofline.
+    st_k = None
+    if args.variant == "wave":
+        rk = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
+                      variant=args.variant, time_launches=True)
+        rk.Initialize(cs)
+        for _ in range(max(1, args.warmup)):
+            rk.Update()
+            rk.Render()
+        rk.synchronize()
+        rk.reset_stats()
+        barrier()
+        for _ in range(args.steps):
+            rk.Update()
+            rk.Render()
+        rk.synchronize()
+        barrier()
+        st_k = rk.stats()
+        rk.close()
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -131,13 +153,37 @@ def main():
     value = samples / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
     kms = {p: st["kernel_ms_total"][pid[p]] / max(1, st["kernel_launches"][pid[p]]) for p in passes}
-    dom = max(passes, key=lambda p: kms[p])
-    achieved = alg_bytes[dom] / (kms[dom] * 1e-3) / 1e9
+    # frame-level figure of SURVEY.md §8d: algorithmic bytes of the frame / kernel time
+    frame_bytes = sum(alg_bytes.values())
+    frame_kernel_s = sum(kms.values()) * 1e-3
+    n_trace = st_k["kernel_launches"][N.PTX_STAT_WAVE_TRACE] if st_k else 0
+    if n_trace:
+        # wavefront: the dominant kernel is trace_queue (every trace round of every pass).
+        # Its algorithmic bytes per launch = the frame's traversal bytes (+ 32 B ray record
+        # read and 32 B hit record written per query) / trace launches per frame; its
+        # duration is the HIP-event average over the timed region.
+        dom = "trace_queue"
+        traced = [p for p in passes if p != "gbuffer"]
+        work = {k: sum(counts[p][k] for p in traced) for k in counts[traced[0]]}
+        per_frame = n_trace / args.steps
+        dom_bytes = (ray_bytes(work) + 64 * work["rays"]) / per_frame
+        dom_ms = st_k["kernel_ms_total"][N.PTX_STAT_WAVE_TRACE] / n_trace
+        logic_ms = (st_k["kernel_ms_total"][N.PTX_STAT_WAVE_LOGIC]
+                    / max(1, st_k["kernel_launches"][N.PTX_STAT_WAVE_LOGIC]))
+        extra = {"launches_per_frame": per_frame, "logic_kernel_avg_ms": round(logic_ms, 4)}
+    else:
+        dom = max(passes, key=lambda p: kms[p])
+        work = counts[dom]
+        dom_bytes = alg_bytes[dom]
+        dom_ms = kms[dom]
+        extra = {}
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     prof = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(prof):
         try:
-            traffic = json.load(open(prof)).get(f"{pipeline}:{dom}:{W}x{Hb}")
+            entry = json.load(open(prof)).get(f"{pipeline}:{dom}:{W}x{Hb}")
+            traffic = entry["bytes_per_launch"] if isinstance(entry, dict) else entry
         except Exception:
             traffic = None
     cpu = None
@@ -156,8 +202,11 @@ def main():
         "nonfinite_px": nonfinite,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes[dom], "alg_bytes_per_sample": round(alg_bytes[dom] / px, 1),
-                     "work": counts[dom]},
+                     "avg_launch_ms": round(dom_ms, 4), "alg_bytes_per_launch": int(dom_bytes),
+                     "work_per_frame": work, **extra,
+                     "frame": {"alg_bytes": int(frame_bytes), "alg_bytes_per_sample": round(frame_bytes / px, 1),
+                               "kernel_ms": round(frame_kernel_s * 1e3, 4),
+                               "frac": round(frame_bytes / frame_kernel_s / (HBM_PEAK_GBS * 1e9), 4)}},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))

@@ -54,6 +54,9 @@ extern "C" {
 #define PTX_PASS_FINAL 2
 #define PTX_PASS_MCPT 3
 #define PTX_PASS_TRACE 4  /* ptx_trace / ptx_trace_device (stats slot only) */
+/* stats-only slots: every launch of the wavefront pipeline's kernels, by kind */
+#define PTX_STAT_WAVE_TRACE 5  /* trace_queue launches (ray-segment traversal)      */
+#define PTX_STAT_WAVE_LOGIC 6  /* start/step launches (shading, RIS, queue appends) */
 
 /* buffers for ptx_read_buffer / ptx_write_buffer / ptx_device_pointer */
 #define PTX_BUF_GBUFFER 0    /* band_h * W * 4 u32   */
@@ -65,6 +68,8 @@ extern "C" {
 #define PTX_FLAG_SIMPLE_KERNELS 2u   /* A/B: one thread per pixel, no ray exchange            */
 #define PTX_FLAG_PERSISTENT_LANES 4u /* A/B: persistent lanes with pixel regeneration         */
 #define PTX_FLAG_TILED_EXCHANGE 8u   /* A/B: 16x16 tiles with an LDS ray exchange             */
+#define PTX_FLAG_TIME_LAUNCHES 16u   /* HIP events around every wavefront launch (stats slots
+                                        PTX_STAT_WAVE_*); costs ~5% of frame time            */
 /* no variant flag: the wavefront pipeline (compacted ray queues, one trace round per
    path vertex) -- the default */
 

@@ -14,11 +14,13 @@ LIB_PATH = os.path.join(PKG_DIR, "libptx.so")
 PTX_OK = 0
 PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT = 0, 1
 PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT, PTX_PASS_TRACE = 0, 1, 2, 3, 4
+PTX_STAT_WAVE_TRACE, PTX_STAT_WAVE_LOGIC = 5, 6  # stats-only slots (include/ptx.h)
 PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS = 0, 1, 2, 3
 PTX_FLAG_COUNT_WORK = 1
 PTX_FLAG_SIMPLE_KERNELS = 2
 PTX_FLAG_PERSISTENT_LANES = 4
 PTX_FLAG_TILED_EXCHANGE = 8
+PTX_FLAG_TIME_LAUNCHES = 16
 VARIANT_FLAGS = {"wave": 0, "tiled": PTX_FLAG_TILED_EXCHANGE, "persistent": PTX_FLAG_PERSISTENT_LANES,
                  "simple": PTX_FLAG_SIMPLE_KERNELS}
 

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -23,7 +24,7 @@ using namespace ptx;
 namespace {
 
 constexpr int kPasses = 8;
-constexpr int kEventRing = 64;
+constexpr int kEventRing = 256;  // ~15 event pairs per wavefront frame
 
 struct DevBuf {
     void *p = nullptr;
@@ -318,6 +319,20 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
 }
 
 // One secondary pass as a fixed sequence of wavefront rounds (no host sync inside).
+// Event pair around one launch, accounted to stats slot `slot` (resolved lazily).
+static TimedLaunch *event_begin(ptx_handle *h, int slot) {
+    if (!(h->cfg.flags & PTX_FLAG_TIME_LAUNCHES)) return nullptr;  // events cost ~5% of a frame
+    TimedLaunch &t = h->ring[h->ring_pos];
+    h->ring_pos = (h->ring_pos + 1) % kEventRing;
+    resolve_event(t, h);
+    if (hipEventRecord(t.start, h->stream) != hipSuccess) return nullptr;
+    t.pass = slot;
+    return &t;
+}
+static void event_end(ptx_handle *h, TimedLaunch *t) {
+    if (t && hipEventRecord(t->stop, h->stream) == hipSuccess) t->pending = true;
+}
+
 static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass) {
     const uint4 *gb = (const uint4 *)h->d_gbuf.p;
     uint4 *res = (uint4 *)h->d_res.p;
@@ -326,11 +341,17 @@ static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBuf
     const int rounds = pass == PTX_PASS_INIT ? kWaveRoundsInit : pass == PTX_PASS_FINAL ? kWaveRoundsFinal
                                                                                         : kWaveRoundsMcpt;
     for (int r = 0; e == hipSuccess && r <= rounds; ++r) {
-        if (r > 0) e = wave_trace(sc, w, r - 1, 1, h->stack_depth, h->stream);
+        if (r > 0) {
+            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE);
+            e = wave_trace(sc, w, r - 1, 1, h->stack_depth, h->stream);
+            event_end(h, t);
+        }
         if (e != hipSuccess) break;
+        TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC);
         e = pass == PTX_PASS_INIT    ? wave_init_round(sc, w, r, gb, res, h->stream)
             : pass == PTX_PASS_FINAL ? wave_final_round(sc, w, r, gb, res, acc, h->stream)
                                      : wave_mcpt_round(sc, w, r, acc, h->stream);
+        event_end(h, t);
     }
     return e;
 }
