@@ -1,0 +1,123 @@
+'use strict';
+/**
+ * NativeRenderer -- the drop-in for the reference's Renderer_TEST
+ * (apps/frontend/src/graphics-core/Renderer_TEST.ts) over the ptx_node N-API addon.
+ *
+ * Same surface: constructor, async Initialize(world), Update(), Render(), GetCamera(),
+ * ResetFrameCount(); WebGPUEngine's loop (GC/service/WebGPUEngine.ts:199-200) calls
+ * Update() then Render() per tick exactly as before.  Instead of a canvas it renders into
+ * the accumulated RGBA f32 image (ReadImage / RenderAsync(out)); presenting it is the
+ * caller's (putImageData), the WebGPU present pass being out of scope (SURVEY.md §8b).
+ *
+ * `world` is the output of SerializeWorldData plus what Update() reads from the World:
+ * { scene, geometry, accel: Uint32Array, offsets: number[7], instanceCount, lightCount }
+ * (scene_io.loadCompiledScene builds it from a compiled scene directory).
+ * There is no CPU fallback: a missing addon or libptx.so throws at require time.
+ */
+const path = require('path');
+const { Camera } = require('./Camera');
+const { mat4 } = require('./wgpu_math');
+
+const addon = require(path.join(__dirname, '..', 'ptx_node.node'));
+
+const PIPELINE = { restir: 0, mcpt: 1 };
+const PASS = { GBUFFER: 0, INIT: 1, FINAL: 2, MCPT: 3, TRACE: 4, WAVE_TRACE: 5, WAVE_LOGIC: 6 };
+const BUF = { GBUFFER: 0, RESERVOIR: 1, ACCUM: 2, COUNTERS: 3 };
+const FLAGS = { COUNT_WORK: 1, SIMPLE_KERNELS: 2, PERSISTENT_LANES: 4, TILED_EXCHANGE: 8, TIME_LAUNCHES: 16 };
+const UNIFORM_WORDS = 33;
+
+/** The 33-word uniform block of Renderer_TEST.Update (Renderer_TEST.ts:165-206). */
+function buildUniform(width, height, camera, frameCount, world) {
+  const data = new ArrayBuffer(4 * UNIFORM_WORDS);
+  const f32 = new Float32Array(data);
+  const u32 = new Uint32Array(data);
+  const loc = camera.GetLocation();
+  const vpInv = mat4.invert(camera.GetViewProjectionMatrix());
+  u32[0] = width;
+  u32[1] = height;
+  u32[2] = 10; // Max Bounce (unused by the kernels)
+  u32[3] = 1;  // SPP
+  for (let i = 0; i < 16; i++) f32[4 + i] = vpInv[i];
+  f32[20] = loc[0];
+  f32[21] = loc[1];
+  f32[22] = loc[2];
+  u32[23] = frameCount;
+  for (let i = 0; i < 7; i++) u32[24 + i] = world.offsets[i];
+  u32[31] = world.instanceCount;
+  u32[32] = world.lightCount;
+  return u32;
+}
+
+class NativeRenderer {
+  /**
+   * @param {number} width  image width (Canvas.width in the reference)
+   * @param {number} height image height
+   * @param {object} [options] {pipeline: 'restir'|'mcpt', device, rowBegin, rowEnd, flags}
+   */
+  constructor(width, height, options = {}) {
+    this.Width = width;
+    this.Height = height;
+    this.Pipeline = options.pipeline || 'restir';
+    if (!(this.Pipeline in PIPELINE)) throw new Error(`unknown pipeline ${this.Pipeline}`);
+    this.RowBegin = options.rowBegin || 0;
+    this.RowEnd = options.rowEnd || height;
+    this.Handle = addon.create({
+      width, height, rowBegin: this.RowBegin, rowEnd: this.RowEnd,
+      device: options.device === undefined ? -1 : options.device,
+      pipeline: PIPELINE[this.Pipeline], flags: options.flags || 0,
+    });
+    this.World = null;
+    this.Camera = null;
+    this.FrameCount = 0;
+    this.Uniform = null;
+  }
+
+  GetCamera() { return this.Camera; }
+
+  ResetFrameCount() { this.FrameCount = 0; }
+
+  /** Renderer_TEST.Initialize (:141-163): camera at (0,0,6), yaw/pitch 0, upload the world. */
+  async Initialize(world) {
+    this.Camera = new Camera(this.Width, this.Height);
+    this.Camera.SetLocationFromXYZ(0, 0, 6);
+    this.Camera.SetYaw(0);
+    this.Camera.SetPitch(0);
+    this.World = world;
+    this.ResetFrameCount();
+    addon.uploadScene(this.Handle, world.scene, world.geometry, world.accel);
+    addon.resetAccumulation(this.Handle);
+  }
+
+  /** Renderer_TEST.Update (:165-206): FrameCount++, then the uniform block. */
+  Update() {
+    this.FrameCount++;
+    this.Uniform = buildUniform(this.Width, this.Height, this.Camera, this.FrameCount, this.World);
+    addon.setFrame(this.Handle, this.Uniform);
+  }
+
+  /** Renderer_TEST.Render (:208-261): all passes + accumulation, asynchronous on the GPU. */
+  Render() { addon.render(this.Handle); }
+
+  /** Render off the event loop; resolves once the frame (and the optional copy) is done. */
+  RenderAsync(out) { return addon.renderAsync(this.Handle, out || null); }
+
+  /** The accumulated band image, RGBA f32 (the reference's Scene texture). */
+  ReadImage(out) {
+    const img = out || new Float32Array((this.RowEnd - this.RowBegin) * this.Width * 4);
+    addon.readBuffer(this.Handle, BUF.ACCUM, img);
+    return img;
+  }
+
+  RunPass(pass) { addon.runPass(this.Handle, pass); }
+  Synchronize() { addon.synchronize(this.Handle); }
+  GetStats() { return addon.getStats(this.Handle); }
+  Trace(rays, hits, epsMode = 1) { addon.trace(this.Handle, rays, hits, epsMode); }
+
+  /** DestroyGPUResources (:462-476). */
+  Destroy() {
+    if (this.Handle) addon.destroy(this.Handle);
+    this.Handle = null;
+  }
+}
+
+module.exports = { NativeRenderer, buildUniform, addon, PASS, BUF, FLAGS, UNIFORM_WORDS };

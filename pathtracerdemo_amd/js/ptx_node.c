@@ -1,0 +1,465 @@
+/*
+ * ptx_node.c -- thin Node N-API addon over the C ABI of include/ptx.h (libptx.so).
+ *
+ * This is the binding a TypeScript maintainer adds behind the reference's Renderer
+ * surface (apps/frontend/src/graphics-core/Renderer_TEST.ts): NativeRenderer.js calls
+ * these functions where Renderer_TEST issues WebGPU calls.  Plain data only crosses the
+ * boundary: typed arrays in, typed arrays / numbers / plain objects out.  Errors become
+ * JS exceptions carrying ptx_last_error().  renderAsync runs ptx_render on the libuv
+ * thread pool (napi_create_async_work) so the event loop never blocks; one render may be
+ * in flight per handle.
+ */
+#define NAPI_VERSION 6
+#include <node_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/ptx.h"
+
+typedef struct {
+    ptx_handle *h;
+    int busy;  /* a renderAsync is in flight */
+} Handle;
+
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref out_ref; /* keeps the output Float32Array alive */
+    Handle *H;
+    float *out;
+    int rc;
+    char err[512];
+} RenderJob;
+
+#define CHECK_NAPI(env, call)                                                    \
+    do {                                                                         \
+        if ((call) != napi_ok) {                                                 \
+            napi_throw_error((env), NULL, "N-API call failed: " #call);          \
+            return NULL;                                                         \
+        }                                                                        \
+    } while (0)
+
+static napi_value throw_ptx(napi_env env, Handle *H, int rc, const char *what) {
+    char msg[768];
+    const char *detail = H && H->h ? ptx_last_error(H->h) : "";
+    snprintf(msg, sizeof msg, "%s failed (%d)%s%s", what, rc, detail && *detail ? ": " : "", detail ? detail : "");
+    napi_throw_error(env, NULL, msg);
+    return NULL;
+}
+
+static void finalize_handle(napi_env env, void *data, void *hint) {
+    (void)env;
+    (void)hint;
+    Handle *H = (Handle *)data;
+    if (H && H->h && !H->busy) ptx_destroy(H->h);
+    free(H);
+}
+
+static Handle *get_handle(napi_env env, napi_value v) {
+    void *p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+        napi_throw_type_error(env, NULL, "expected a ptx handle");
+        return NULL;
+    }
+    Handle *H = (Handle *)p;
+    if (!H->h) {
+        napi_throw_error(env, NULL, "ptx handle already destroyed");
+        return NULL;
+    }
+    return H;
+}
+
+static int get_u32_prop(napi_env env, napi_value obj, const char *name, uint32_t dflt, uint32_t *out) {
+    bool has = false;
+    *out = dflt;
+    if (napi_has_named_property(env, obj, name, &has) != napi_ok || !has) return 0;
+    napi_value v;
+    if (napi_get_named_property(env, obj, name, &v) != napi_ok) return -1;
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t == napi_undefined || t == napi_null) return 0;
+    int32_t i;
+    if (napi_get_value_int32(env, v, &i) != napi_ok) return -1;
+    *out = (uint32_t)i;
+    return 0;
+}
+
+/* typed array view: data pointer, element count, element size */
+static int typed_view(napi_env env, napi_value v, void **data, size_t *count, size_t *elem,
+                      napi_typedarray_type *type_out) {
+    bool is_ta = false;
+    if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return -1;
+    napi_typedarray_type type;
+    size_t length, offset;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, v, &type, &length, data, &ab, &offset) != napi_ok) return -1;
+    size_t es = 1;
+    switch (type) {
+    case napi_int8_array: case napi_uint8_array: case napi_uint8_clamped_array: es = 1; break;
+    case napi_int16_array: case napi_uint16_array: es = 2; break;
+    case napi_int32_array: case napi_uint32_array: case napi_float32_array: es = 4; break;
+    case napi_float64_array: es = 8; break;
+    default: es = 8; break;
+    }
+    *count = length;
+    *elem = es;
+    if (type_out) *type_out = type;
+    return 0;
+}
+
+static napi_value js_abi_version(napi_env env, napi_callback_info info) {
+    (void)info;
+    napi_value r;
+    CHECK_NAPI(env, napi_create_int32(env, ptx_abi_version(), &r));
+    return r;
+}
+
+/* create({width, height, rowBegin, rowEnd, device, pipeline, flags}) -> handle */
+static napi_value js_create(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    if (argc < 1) {
+        napi_throw_type_error(env, NULL, "create(config) needs a config object");
+        return NULL;
+    }
+    ptx_config cfg;
+    memset(&cfg, 0, sizeof cfg);
+    uint32_t dev = 0xffffffffu;
+    if (get_u32_prop(env, argv[0], "width", 0, &cfg.width) || get_u32_prop(env, argv[0], "height", 0, &cfg.height) ||
+        get_u32_prop(env, argv[0], "rowBegin", 0, &cfg.row_begin) ||
+        get_u32_prop(env, argv[0], "rowEnd", 0, &cfg.row_end) || get_u32_prop(env, argv[0], "device", dev, &dev) ||
+        get_u32_prop(env, argv[0], "pipeline", PTX_PIPELINE_RESTIR, &cfg.pipeline) ||
+        get_u32_prop(env, argv[0], "flags", 0, &cfg.flags)) {
+        napi_throw_type_error(env, NULL, "create: config fields must be integers");
+        return NULL;
+    }
+    cfg.device = (int32_t)dev;
+    ptx_handle *h = NULL;
+    int rc = ptx_create(&cfg, &h);
+    if (rc != PTX_OK) return throw_ptx(env, NULL, rc, "ptx_create");
+    Handle *H = (Handle *)calloc(1, sizeof(Handle));
+    if (!H) {
+        ptx_destroy(h);
+        napi_throw_error(env, NULL, "out of memory");
+        return NULL;
+    }
+    H->h = h;
+    napi_value ext;
+    CHECK_NAPI(env, napi_create_external(env, H, finalize_handle, NULL, &ext));
+    return ext;
+}
+
+/* uploadScene(h, Uint32Array scene, Uint32Array geometry, Uint32Array accel) */
+static napi_value js_upload_scene(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    void *p[3];
+    size_t n[3], es;
+    for (int i = 0; i < 3; ++i) {
+        napi_typedarray_type t;
+        if ((size_t)(i + 1) >= argc || typed_view(env, argv[i + 1], &p[i], &n[i], &es, &t) || t != napi_uint32_array) {
+            napi_throw_type_error(env, NULL, "uploadScene(h, scene, geometry, accel) takes three Uint32Arrays");
+            return NULL;
+        }
+    }
+    int rc = ptx_upload_scene(H->h, (const uint32_t *)p[0], n[0], (const uint32_t *)p[1], n[1],
+                              (const uint32_t *)p[2], n[2]);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_upload_scene");
+    return NULL;
+}
+
+/* setFrame(h, Uint32Array(33)) */
+static napi_value js_set_frame(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    void *p;
+    size_t n, es;
+    napi_typedarray_type t;
+    if (argc < 2 || typed_view(env, argv[1], &p, &n, &es, &t) || t != napi_uint32_array || n != PTX_UNIFORM_WORDS) {
+        napi_throw_type_error(env, NULL, "setFrame(h, uniform) takes a Uint32Array of 33 words");
+        return NULL;
+    }
+    int rc = ptx_set_frame(H->h, (const uint32_t *)p);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_set_frame");
+    return NULL;
+}
+
+/* render(h [, Float32Array out]) -- blocking when out is given, else asynchronous on the GPU */
+static napi_value js_render(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    if (H->busy) {
+        napi_throw_error(env, NULL, "a renderAsync is in flight on this handle");
+        return NULL;
+    }
+    float *out = NULL;
+    if (argc >= 2) {
+        napi_valuetype vt;
+        napi_typeof(env, argv[1], &vt);
+        if (vt != napi_undefined && vt != napi_null) {
+            void *p;
+            size_t n, es;
+            napi_typedarray_type t;
+            if (typed_view(env, argv[1], &p, &n, &es, &t) || t != napi_float32_array) {
+                napi_throw_type_error(env, NULL, "render(h, out): out must be a Float32Array (band_h*W*4)");
+                return NULL;
+            }
+            out = (float *)p;
+        }
+    }
+    int rc = ptx_render(H->h, out);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_render");
+    return NULL;
+}
+
+static void render_execute(napi_env env, void *data) {
+    (void)env;
+    RenderJob *J = (RenderJob *)data;
+    J->rc = ptx_render(J->H->h, J->out);
+    if (J->rc == PTX_OK) J->rc = ptx_synchronize(J->H->h);
+    if (J->rc != PTX_OK) snprintf(J->err, sizeof J->err, "ptx_render failed (%d): %s", J->rc, ptx_last_error(J->H->h));
+}
+
+static void render_complete(napi_env env, napi_status status, void *data) {
+    RenderJob *J = (RenderJob *)data;
+    J->H->busy = 0;
+    napi_value v;
+    if (status == napi_ok && J->rc == PTX_OK) {
+        napi_get_undefined(env, &v);
+        napi_resolve_deferred(env, J->deferred, v);
+    } else {
+        napi_value msg;
+        napi_create_string_utf8(env, J->err[0] ? J->err : "render cancelled", NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, NULL, msg, &v);
+        napi_reject_deferred(env, J->deferred, v);
+    }
+    if (J->out_ref) napi_delete_reference(env, J->out_ref);
+    napi_delete_async_work(env, J->work);
+    free(J);
+}
+
+/* renderAsync(h [, Float32Array out]) -> Promise: ptx_render + synchronize off the event loop */
+static napi_value js_render_async(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    if (H->busy) {
+        napi_throw_error(env, NULL, "a renderAsync is already in flight on this handle");
+        return NULL;
+    }
+    RenderJob *J = (RenderJob *)calloc(1, sizeof(RenderJob));
+    if (!J) {
+        napi_throw_error(env, NULL, "out of memory");
+        return NULL;
+    }
+    J->H = H;
+    if (argc >= 2) {
+        napi_valuetype vt;
+        napi_typeof(env, argv[1], &vt);
+        if (vt != napi_undefined && vt != napi_null) {
+            void *p;
+            size_t n, es;
+            napi_typedarray_type t;
+            if (typed_view(env, argv[1], &p, &n, &es, &t) || t != napi_float32_array) {
+                free(J);
+                napi_throw_type_error(env, NULL, "renderAsync(h, out): out must be a Float32Array");
+                return NULL;
+            }
+            J->out = (float *)p;
+            napi_create_reference(env, argv[1], 1, &J->out_ref);
+        }
+    }
+    napi_value promise, name;
+    CHECK_NAPI(env, napi_create_promise(env, &J->deferred, &promise));
+    CHECK_NAPI(env, napi_create_string_utf8(env, "ptx_render", NAPI_AUTO_LENGTH, &name));
+    CHECK_NAPI(env, napi_create_async_work(env, NULL, name, render_execute, render_complete, J, &J->work));
+    H->busy = 1;
+    CHECK_NAPI(env, napi_queue_async_work(env, J->work));
+    return promise;
+}
+
+static napi_value simple_call(napi_env env, napi_callback_info info, int (*fn)(ptx_handle *), const char *what) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    int rc = fn(H->h);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, what);
+    return NULL;
+}
+static napi_value js_reset_accumulation(napi_env env, napi_callback_info info) {
+    return simple_call(env, info, ptx_reset_accumulation, "ptx_reset_accumulation");
+}
+static napi_value js_synchronize(napi_env env, napi_callback_info info) {
+    return simple_call(env, info, ptx_synchronize, "ptx_synchronize");
+}
+static napi_value js_reset_stats(napi_env env, napi_callback_info info) {
+    return simple_call(env, info, ptx_reset_stats, "ptx_reset_stats");
+}
+
+/* runPass(h, pass) */
+static napi_value js_run_pass(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    int32_t pass = -1;
+    if (argc < 2 || napi_get_value_int32(env, argv[1], &pass) != napi_ok) {
+        napi_throw_type_error(env, NULL, "runPass(h, pass) needs an integer pass");
+        return NULL;
+    }
+    int rc = ptx_run_pass(H->h, pass);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_run_pass");
+    return NULL;
+}
+
+/* read/writeBuffer(h, which, TypedArray) -- byte count = the array's byte length */
+static napi_value buffer_io(napi_env env, napi_callback_info info, int write) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    int32_t which = -1;
+    void *p;
+    size_t n, es;
+    if (argc < 3 || napi_get_value_int32(env, argv[1], &which) != napi_ok ||
+        typed_view(env, argv[2], &p, &n, &es, NULL)) {
+        napi_throw_type_error(env, NULL, "read/writeBuffer(h, which, typedArray)");
+        return NULL;
+    }
+    int rc = write ? ptx_write_buffer(H->h, which, p, n * es) : ptx_read_buffer(H->h, which, p, n * es);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, write ? "ptx_write_buffer" : "ptx_read_buffer");
+    return NULL;
+}
+static napi_value js_read_buffer(napi_env env, napi_callback_info info) { return buffer_io(env, info, 0); }
+static napi_value js_write_buffer(napi_env env, napi_callback_info info) { return buffer_io(env, info, 1); }
+
+/* trace(h, Float32Array rays (n*8), Float32Array hits (n*8), epsMode) */
+static napi_value js_trace(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    void *pr, *ph;
+    size_t nr, nh, es;
+    napi_typedarray_type tr, th;
+    int32_t eps = 1;
+    if (argc < 3 || typed_view(env, argv[1], &pr, &nr, &es, &tr) || typed_view(env, argv[2], &ph, &nh, &es, &th) ||
+        tr != napi_float32_array || th != napi_float32_array || nr % 8 || nh < nr) {
+        napi_throw_type_error(env, NULL, "trace(h, rays: Float32Array n*8, hits: Float32Array n*8, epsMode)");
+        return NULL;
+    }
+    if (argc >= 4) napi_get_value_int32(env, argv[3], &eps);
+    int rc = ptx_trace(H->h, (const float *)pr, (float *)ph, nr / 8, eps);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_trace");
+    return NULL;
+}
+
+/* getStats(h) -> {frames, kernelMsTotal[8], kernelLaunches[8], triangles, bvhNodes, instances, maxBvhDepth, deviceBytes} */
+static napi_value js_get_stats(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    ptx_stats st;
+    int rc = ptx_get_stats(H->h, &st);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_get_stats");
+    napi_value o, v, ms, la;
+    CHECK_NAPI(env, napi_create_object(env, &o));
+    CHECK_NAPI(env, napi_create_array_with_length(env, 8, &ms));
+    CHECK_NAPI(env, napi_create_array_with_length(env, 8, &la));
+    for (uint32_t i = 0; i < 8; ++i) {
+        napi_create_double(env, st.kernel_ms_total[i], &v);
+        napi_set_element(env, ms, i, v);
+        napi_create_double(env, (double)st.kernel_launches[i], &v);
+        napi_set_element(env, la, i, v);
+    }
+    napi_set_named_property(env, o, "kernelMsTotal", ms);
+    napi_set_named_property(env, o, "kernelLaunches", la);
+    napi_create_double(env, (double)st.frames, &v);
+    napi_set_named_property(env, o, "frames", v);
+    napi_create_uint32(env, st.triangles, &v);
+    napi_set_named_property(env, o, "triangles", v);
+    napi_create_uint32(env, st.bvh_nodes, &v);
+    napi_set_named_property(env, o, "bvhNodes", v);
+    napi_create_uint32(env, st.instances, &v);
+    napi_set_named_property(env, o, "instances", v);
+    napi_create_uint32(env, st.max_bvh_depth, &v);
+    napi_set_named_property(env, o, "maxBvhDepth", v);
+    napi_create_double(env, (double)st.device_bytes, &v);
+    napi_set_named_property(env, o, "deviceBytes", v);
+    return o;
+}
+
+/* destroy(h) -- idempotent; the GC finalizer also releases an undestroyed handle */
+static napi_value js_destroy(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    void *p = NULL;
+    if (argc < 1 || napi_get_value_external(env, argv[0], &p) != napi_ok || !p) {
+        napi_throw_type_error(env, NULL, "destroy(h) needs a ptx handle");
+        return NULL;
+    }
+    Handle *H = (Handle *)p;
+    if (H->busy) {
+        napi_throw_error(env, NULL, "destroy: a renderAsync is in flight");
+        return NULL;
+    }
+    if (H->h) ptx_destroy(H->h);
+    H->h = NULL;
+    return NULL;
+}
+
+static napi_value js_last_error(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], s;
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    CHECK_NAPI(env, napi_create_string_utf8(env, ptx_last_error(H->h), NAPI_AUTO_LENGTH, &s));
+    return s;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+    static const struct {
+        const char *name;
+        napi_callback fn;
+    } fns[] = {
+        {"abiVersion", js_abi_version},     {"create", js_create},
+        {"uploadScene", js_upload_scene},   {"setFrame", js_set_frame},
+        {"render", js_render},              {"renderAsync", js_render_async},
+        {"runPass", js_run_pass},           {"resetAccumulation", js_reset_accumulation},
+        {"synchronize", js_synchronize},    {"getStats", js_get_stats},
+        {"resetStats", js_reset_stats},     {"readBuffer", js_read_buffer},
+        {"writeBuffer", js_write_buffer},   {"trace", js_trace},
+        {"destroy", js_destroy},            {"lastError", js_last_error},
+    };
+    for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
+        napi_value f;
+        if (napi_create_function(env, fns[i].name, NAPI_AUTO_LENGTH, fns[i].fn, NULL, &f) != napi_ok ||
+            napi_set_named_property(env, exports, fns[i].name, f) != napi_ok)
+            return NULL;
+    }
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

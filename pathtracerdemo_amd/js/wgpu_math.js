@@ -1,0 +1,100 @@
+'use strict';
+/**
+ * The wgpu-matrix@3.4.0 subset the reference's host uses (Camera.ts, Renderer_TEST.ts:172),
+ * with its storage semantics: every function computes in JS numbers (f64) and stores
+ * its result into a Float32Array.  The library is not installed here (SURVEY.md §8c);
+ * these restate its published formulas and match pathtracerdemo_amd/scene/wgpu_math.py
+ * operation for operation, so the Python and JS hosts build bit-identical uniforms.
+ */
+
+function out(values) {
+  return Float32Array.from(values);
+}
+
+const mat4 = {
+  identity() {
+    return out([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1]);
+  },
+  translation(v) {
+    return out([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, Math.fround(v[0]), Math.fround(v[1]), Math.fround(v[2]), 1]);
+  },
+  // column-major a * b
+  multiply(a, b) {
+    const r = new Array(16);
+    for (let c = 0; c < 4; c++) {
+      for (let row = 0; row < 4; row++) {
+        r[c * 4 + row] =
+          a[0 * 4 + row] * b[c * 4 + 0] + a[1 * 4 + row] * b[c * 4 + 1] +
+          a[2 * 4 + row] * b[c * 4 + 2] + a[3 * 4 + row] * b[c * 4 + 3];
+      }
+    }
+    return out(r);
+  },
+  // cofactor expansion (2x2 sub-determinants of the top and bottom row pairs)
+  invert(m) {
+    const [a00, a01, a02, a03, a10, a11, a12, a13, a20, a21, a22, a23, a30, a31, a32, a33] = Array.from(m);
+    const b00 = a00 * a11 - a01 * a10, b01 = a00 * a12 - a02 * a10, b02 = a00 * a13 - a03 * a10;
+    const b03 = a01 * a12 - a02 * a11, b04 = a01 * a13 - a03 * a11, b05 = a02 * a13 - a03 * a12;
+    const b06 = a20 * a31 - a21 * a30, b07 = a20 * a32 - a22 * a30, b08 = a20 * a33 - a23 * a30;
+    const b09 = a21 * a32 - a22 * a31, b10 = a21 * a33 - a23 * a31, b11 = a22 * a33 - a23 * a32;
+    const det = b00 * b11 - b01 * b10 + b02 * b09 + b03 * b08 - b04 * b07 + b05 * b06;
+    const inv = 1.0 / det;
+    return out([
+      (a11 * b11 - a12 * b10 + a13 * b09) * inv, (a02 * b10 - a01 * b11 - a03 * b09) * inv,
+      (a31 * b05 - a32 * b04 + a33 * b03) * inv, (a22 * b04 - a21 * b05 - a23 * b03) * inv,
+      (a12 * b08 - a10 * b11 - a13 * b07) * inv, (a00 * b11 - a02 * b08 + a03 * b07) * inv,
+      (a32 * b02 - a30 * b05 - a33 * b01) * inv, (a20 * b05 - a22 * b02 + a23 * b01) * inv,
+      (a10 * b10 - a11 * b08 + a13 * b06) * inv, (a01 * b08 - a00 * b10 - a03 * b06) * inv,
+      (a30 * b04 - a31 * b02 + a33 * b00) * inv, (a21 * b02 - a20 * b04 - a23 * b00) * inv,
+      (a11 * b07 - a10 * b09 - a12 * b06) * inv, (a00 * b09 - a01 * b07 + a02 * b06) * inv,
+      (a31 * b01 - a30 * b03 - a32 * b00) * inv, (a20 * b03 - a21 * b01 + a22 * b00) * inv,
+    ]);
+  },
+  fromQuat(q) {
+    const [x, y, z, w] = Array.from(q);
+    const x2 = x + x, y2 = y + y, z2 = z + z;
+    const xx = x * x2, yx = y * x2, yy = y * y2;
+    const zx = z * x2, zy = z * y2, zz = z * z2;
+    const wx = w * x2, wy = w * y2, wz = w * z2;
+    return out([1 - yy - zz, yx + wz, zx - wy, 0,
+      yx - wz, 1 - xx - zz, zy + wx, 0,
+      zx + wy, zy - wx, 1 - xx - yy, 0,
+      0, 0, 0, 1]);
+  },
+  // WebGPU clip space (z in [0, 1])
+  perspective(fovy, aspect, near, far) {
+    const f = Math.tan(Math.PI * 0.5 - 0.5 * fovy);
+    const m = new Array(16).fill(0);
+    m[0] = f / aspect;
+    m[5] = f;
+    m[11] = -1;
+    if (Number.isFinite(far)) {
+      const rangeInv = 1 / (near - far);
+      m[10] = far * rangeInv;
+      m[14] = far * near * rangeInv;
+    } else {
+      m[10] = -1;
+      m[14] = -near;
+    }
+    return out(m);
+  },
+};
+
+const quat = {
+  fromEuler(x, y, z, order) {
+    if (order !== 'yxz') throw new Error(`quat.fromEuler: order ${order} not supported`);
+    const sx = Math.sin(x * 0.5), cx = Math.cos(x * 0.5);
+    const sy = Math.sin(y * 0.5), cy = Math.cos(y * 0.5);
+    const sz = Math.sin(z * 0.5), cz = Math.cos(z * 0.5);
+    return out([sx * cy * cz + cx * sy * sz, cx * sy * cz - sx * cy * sz,
+      cx * cy * sz - sx * sy * cz, cx * cy * cz + sx * sy * sz]);
+  },
+};
+
+const vec3 = {
+  fromValues(x, y, z) {
+    return out([x, y, z]);
+  },
+};
+
+module.exports = { mat4, quat, vec3 };

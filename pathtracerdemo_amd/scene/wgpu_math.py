@@ -38,15 +38,38 @@ def mat4_scaling(v) -> np.ndarray:
 
 
 def mat4_multiply(a, b) -> np.ndarray:
-    """Column-major a*b (wgpu-matrix mat4.multiply)."""
-    A = np.asarray(a, dtype=np.float32).astype(np.float64).reshape(4, 4).T
-    B = np.asarray(b, dtype=np.float32).astype(np.float64).reshape(4, 4).T
-    return _out((A @ B).T.reshape(-1))
+    """Column-major a*b (wgpu-matrix mat4.multiply); left-to-right f64 sums, as the JS host
+    (pathtracerdemo_amd/js/wgpu_math.js) computes them."""
+    a = [float(v) for v in np.asarray(a, dtype=np.float32)]
+    b = [float(v) for v in np.asarray(b, dtype=np.float32)]
+    r = [0.0] * 16
+    for c in range(4):
+        for row in range(4):
+            r[c * 4 + row] = (a[row] * b[c * 4] + a[4 + row] * b[c * 4 + 1]
+                              + a[8 + row] * b[c * 4 + 2] + a[12 + row] * b[c * 4 + 3])
+    return _out(r)
 
 
 def mat4_invert(m) -> np.ndarray:
-    M = np.asarray(m, dtype=np.float32).astype(np.float64).reshape(4, 4).T
-    return _out(np.linalg.inv(M).T.reshape(-1))
+    """wgpu-matrix mat4.invert: cofactor expansion over 2x2 sub-determinants, f64."""
+    (a00, a01, a02, a03, a10, a11, a12, a13,
+     a20, a21, a22, a23, a30, a31, a32, a33) = (float(v) for v in np.asarray(m, dtype=np.float32))
+    b00, b01, b02 = a00 * a11 - a01 * a10, a00 * a12 - a02 * a10, a00 * a13 - a03 * a10
+    b03, b04, b05 = a01 * a12 - a02 * a11, a01 * a13 - a03 * a11, a02 * a13 - a03 * a12
+    b06, b07, b08 = a20 * a31 - a21 * a30, a20 * a32 - a22 * a30, a20 * a33 - a23 * a30
+    b09, b10, b11 = a21 * a32 - a22 * a31, a21 * a33 - a23 * a31, a22 * a33 - a23 * a32
+    det = b00 * b11 - b01 * b10 + b02 * b09 + b03 * b08 - b04 * b07 + b05 * b06
+    inv = 1.0 / det
+    return _out([
+        (a11 * b11 - a12 * b10 + a13 * b09) * inv, (a02 * b10 - a01 * b11 - a03 * b09) * inv,
+        (a31 * b05 - a32 * b04 + a33 * b03) * inv, (a22 * b04 - a21 * b05 - a23 * b03) * inv,
+        (a12 * b08 - a10 * b11 - a13 * b07) * inv, (a00 * b11 - a02 * b08 + a03 * b07) * inv,
+        (a32 * b02 - a30 * b05 - a33 * b01) * inv, (a20 * b05 - a22 * b02 + a23 * b01) * inv,
+        (a10 * b10 - a11 * b08 + a13 * b06) * inv, (a01 * b08 - a00 * b10 - a03 * b06) * inv,
+        (a30 * b04 - a31 * b02 + a33 * b00) * inv, (a21 * b02 - a20 * b04 - a23 * b00) * inv,
+        (a11 * b07 - a10 * b09 - a12 * b06) * inv, (a00 * b09 - a01 * b07 + a02 * b06) * inv,
+        (a31 * b01 - a30 * b03 - a32 * b00) * inv, (a20 * b03 - a21 * b01 + a22 * b00) * inv,
+    ])
 
 
 def mat4_from_quat(q) -> np.ndarray:
