@@ -62,7 +62,7 @@ extern "C" {
 #define PTX_BUF_GBUFFER 0    /* band_h * W * 4 u32   */
 #define PTX_BUF_RESERVOIR 1  /* band_h * W * 32 u32  */
 #define PTX_BUF_ACCUM 2      /* band_h * W * 4 f32 (Scene texture: accumulated radiance) */
-#define PTX_BUF_COUNTERS 3   /* 8 u64 work counters (PTX_FLAG_COUNT builds) */
+#define PTX_BUF_COUNTERS 3   /* 32 u64: work counters [0..4] (PTX_FLAG_COUNT builds), diagnostics [8..) */
 
 #define PTX_FLAG_COUNT_WORK 1u     /* count rays / AABB / triangle tests on device (slower)   */
 #define PTX_FLAG_SIMPLE_KERNELS 2u   /* A/B: one thread per pixel, no ray exchange            */

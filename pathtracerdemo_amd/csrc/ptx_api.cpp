@@ -51,7 +51,7 @@ struct ptx_handle {
     DevBuf d_scene, d_geometry;
     // derived MI355X layout
     DevBuf d_tris, d_nodes, d_subs, d_insts;
-    uint32_t n_tris = 0, n_nodes = 0, n_inst = 0, max_depth = 0, stack_depth = 0;
+    uint32_t n_tris = 0, n_nodes = 0, n_inst = 0, n_subs = 0, max_depth = 0, stack_depth = 0;
     uint32_t layout_key[8] = {0};
     bool layout_valid = false;
     bool scene_loaded = false;
@@ -238,6 +238,7 @@ static int build_layout(ptx_handle *h) {
     if (int rc = upload(h, h->d_tris, tris.data(), tris.size() * sizeof(float))) return rc;
     if (int rc = upload(h, h->d_nodes, nodes.data(), nodes.size() * sizeof(NodePair))) return rc;
     if (int rc = upload(h, h->d_subs, subs.data(), subs.size() * sizeof(SubRoot))) return rc;
+    h->n_subs = (uint32_t)subs.size();
     if (int rc = upload(h, h->d_insts, insts.data(), std::max<size_t>(1, insts.size()) * sizeof(Inst))) return rc;
     (void)off_mat;
     h->n_tris = (uint32_t)(tris.size() / 12);
@@ -261,6 +262,7 @@ static Scene make_scene(ptx_handle *h) {
     sc.subs = (const SubRoot *)h->d_subs.p;
     sc.insts = (const Inst *)h->d_insts.p;
     sc.n_inst = h->n_inst;
+    sc.n_subs = h->n_subs;
     sc.width = h->cfg.width;
     sc.height = h->cfg.height;
     sc.row_begin = h->cfg.row_begin;
@@ -463,7 +465,7 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!rc) rc = alloc_buf(h, h->d_gbuf, px * 16u);
     if (!rc) rc = alloc_buf(h, h->d_res, px * 128u);
     if (!rc) rc = alloc_buf(h, h->d_accum, px * 16u);
-    if (!rc) rc = alloc_buf(h, h->d_counters, 64u);
+    if (!rc) rc = alloc_buf(h, h->d_counters, kCounterWords * 8u);
     if (!rc) rc = alloc_buf(h, h->d_queue, 64u);
     if (!rc && hipMemset(h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (!rc && hipMemset(h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;

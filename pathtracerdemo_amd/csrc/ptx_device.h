@@ -71,7 +71,7 @@ struct Scene {
     const NodePair *nodes;
     const SubRoot *subs;
     const Inst *insts;
-    uint32_t n_inst;
+    uint32_t n_inst, n_subs;
     uint32_t width, height, row_begin, row_end;
     unsigned long long *counters;  // nullptr unless PTX_FLAG_COUNT_WORK
 };
@@ -139,6 +139,17 @@ __device__ __forceinline__ float rnd(uint32_t &seed) {
 
 // ------------------------------------------------------------------ counters
 enum { CNT_RAYS = 0, CNT_INST = 1, CNT_AABB = 2, CNT_TRI = 3, CNT_HITS = 4 };
+// SIMD-utilisation profile of trace_core (COUNT == 2 builds, diagnostics only): per region
+// {wave-level executions, active lanes summed over them} at counters[8 + 2*region]
+enum { PROF_ROOT = 0, PROF_NODE = 1, PROF_LEAF = 2, PROF_TRI = 3, PROF_INST = 4, PROF_REGIONS = 5 };
+constexpr int kCounterWords = 32;
+struct Prof {
+    uint32_t wave[PROF_REGIONS], lane[PROF_REGIONS];
+    __device__ __forceinline__ void hit(int r) {
+        lane[r] += 1u;
+        if (__lane_id() == (uint32_t)__builtin_ctzll(__ballot(1))) wave[r] += 1u;
+    }
+};
 
 // ------------------------------------------------------------------ ray / hit
 struct Ray { f3 o, d; };
@@ -231,9 +242,11 @@ __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, Pa
 // continue`).  `stack` is this thread's column of the workgroup's LDS stack
 // (entry k at stack[k * stride]).  Also returns the hit position exactly as
 // GetSurface(hit).Position computes it (same world-space vertices and barycentrics).
-template <bool COUNT, bool SPEC = false>
-__device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack, uint32_t stride,
-                                          float t_max = 1e10f) {
+// `subs` / `insts` are the scene's sub-root and instance tables, or LDS copies of them.
+template <bool COUNT, bool PROF = false>
+__device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *subs, const Inst *insts, Ray ray,
+                                              PassEps eps, uint32_t *stack, uint32_t stride, float t_max = 1e10f) {
+    Prof pf{};
     Hit best;
     best.valid = false;
     best.t = 0.0f;
@@ -243,40 +256,56 @@ __device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps,
     float vy = t_max;  // 1e10 in the reference; a smaller bound only prunes hits beyond it
     uint32_t n_aabb = 0, n_tri = 0;
     for (uint32_t ii = 0; ii < sc.n_inst; ++ii) {
-        const Inst &I = sc.insts[ii];
+        const Inst &I = insts[ii];
+        if (PROF) pf.hit(PROF_INST);
         // TransformRayWithMat4x4(InRay, M^-1, false), SH/PT_1_InitPass.wgsl:486-496
         f3 lo = xform_point(I.minv, ray.o);
         f3 le = xform_point(I.minv, ray.o + ray.d);
         f3 ld = le - lo;
         f3 inv = mk(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
         const uint32_t nsub = I.nsub;
-        for (uint32_t s = 0; s < nsub; ++s) {
-            const SubRoot &R = sc.subs[I.sub_base + s];
-            float tn;
-            ++n_aabb;
-            if (!box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) continue;
-            int sp = 0;
-            stack[0] = R.ref;
-            // while-while traversal: lanes descend interior nodes until each has a leaf (or an
-            // empty stack), then the wave processes leaves together.  Per lane the pops, tests
-            // and pushes happen in exactly the if/else order of the reference loop.
-            // SPEC (speculative): a lane holding a leaf keeps descending while another lane of
-            // the wave still has none, postponing it; a second leaf ends its descent.  Leaves
-            // are still processed in discovery order and every extra visit is a box beyond
-            // the current best hit, so the hit -- ties included -- is unchanged; only the
-            // AABB/triangle work counts grow, hence SPEC is off in counting builds.
-            uint32_t leaf = 0u, leaf2 = 0u;
+        const SubRoot *roots = subs + I.sub_base;
+        const float4 *tris = sc.tris + 3u * I.tri_base;
+        n_aabb += nsub;  // the reference tests every sub-mesh root once
+        for (uint32_t s0 = 0; s0 < nsub; s0 += 32u) {
+            const uint32_t nc = nsub - s0 < 32u ? nsub - s0 : 32u;
+            // Coherent pre-filter: every root against the best t at this point.  The
+            // reference tests root s against the best t after roots < s (never larger), so
+            // this keeps every root it enters; the exact test is repeated when the root is
+            // taken below, with the then-current best -- the reference's own test.
+            uint32_t mask = 0u;
+#pragma unroll 1
+            for (uint32_t k = 0; k < nc; ++k) {
+                float tn;
+                if (PROF) pf.hit(PROF_ROOT);
+                if (box_overlap(lo, inv, roots[s0 + k].bmin, roots[s0 + k].bmax, vx, vy, tn)) mask |= 1u << k;
+            }
+            // while-while traversal over all of this lane's roots: lanes descend interior
+            // nodes (taking their next root, in index order, when the stack runs dry) until
+            // each has a leaf or nothing left, then the wave tests leaves together.  Per lane
+            // the root tests, pops, tests and pushes happen in exactly the reference's order
+            // (SH/PT_1_InitPass.wgsl:605-715), so hits, ties and work counts are unchanged.
+            int sp = -1;
+            uint32_t grp = 0u, leaf = 0u;
             for (;;) {
-                while (sp >= 0 && (SPEC || leaf == 0u)) {
+                while (leaf == 0u && (sp >= 0 || mask != 0u)) {
+                    if (PROF) pf.hit(PROF_NODE);
+                    if (sp < 0) {
+                        const uint32_t k = (uint32_t)__builtin_ctz(mask);
+                        mask &= mask - 1u;
+                        const SubRoot &R = roots[s0 + k];
+                        float tn;
+                        if (box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) {
+                            stack[0] = R.ref;
+                            sp = 0;
+                            grp = s0 + k;
+                        }
+                        continue;
+                    }
                     const uint32_t ref = stack[(uint32_t)sp * stride];
                     --sp;
                     if (ref & LEAF_BIT) {
-                        if (leaf == 0u) {
-                            leaf = ref;
-                            if (!SPEC || !__any(leaf == 0u)) break;
-                            continue;
-                        }
-                        leaf2 = ref;
+                        leaf = ref;
                         break;
                     }
                     const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + ref);
@@ -298,15 +327,15 @@ __device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps,
                         stack[(uint32_t)(sp + 1) * stride] = hl ? lref : rref;
                         sp += 1;
                     }
-                    if (SPEC && !__any(leaf == 0u)) break;
                 }
-                if (leaf == 0u) break;  // stack exhausted
+                if (leaf == 0u) break;  // roots and stack exhausted
+                if (PROF) pf.hit(PROF_LEAF);
                 const uint32_t first = leaf & LEAF_FIRST_MASK;
                 const uint32_t count = (leaf >> 24) & 0x7Fu;
-                leaf = leaf2;
-                leaf2 = 0u;
-                const float4 *tp = sc.tris + 3u * (I.tri_base + first);
+                leaf = 0u;
+                const float4 *tp = tris + 3u * first;
                 for (uint32_t k = 0; k < count; ++k) {
+                    if (PROF) pf.hit(PROF_TRI);
                     float4 a = tp[3u * k + 0u], b = tp[3u * k + 1u], c = tp[3u * k + 2u];
                     float t = ray_tri(lo, ld, a, b, c, eps.det_eps);
                     ++n_tri;
@@ -314,10 +343,16 @@ __device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps,
                     vy = t;
                     best.valid = true;
                     best.s.inst = ii;
-                    best.s.mat = s;
+                    best.s.mat = grp;
                     best.s.prim = first + k;
                 }
             }
+        }
+    }
+    if (PROF) {
+        for (int r = 0; r < PROF_REGIONS; ++r) {
+            if (pf.wave[r]) atomicAdd(&sc.counters[8 + 2 * r], (unsigned long long)pf.wave[r]);
+            if (pf.lane[r]) atomicAdd(&sc.counters[9 + 2 * r], (unsigned long long)pf.lane[r]);
         }
     }
     if (COUNT) {
@@ -332,6 +367,28 @@ __device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps,
         complete_hit(sc, ray, eps, best);
     }
     return best;
+}
+// Sub-root and instance tables staged in LDS when they fit: every ray tests every root of
+// every instance, ~16 table reads per query otherwise paid as scalar-load round trips.
+// Called by all threads of the workgroup (ends with a barrier).
+constexpr uint32_t kLdsSubs = 128, kLdsInsts = 8;
+__device__ __forceinline__ bool tables_fit_lds(const Scene &sc) {
+    return sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts;
+}
+__device__ __forceinline__ void stage_tables(const Scene &sc, SubRoot *l_subs, Inst *l_insts) {
+    const uint32_t *gs = reinterpret_cast<const uint32_t *>(sc.subs);
+    uint32_t *ls = reinterpret_cast<uint32_t *>(l_subs);
+    for (uint32_t i = threadIdx.x; i < sc.n_subs * (uint32_t)(sizeof(SubRoot) / 4u); i += blockDim.x) ls[i] = gs[i];
+    const uint32_t *gi = reinterpret_cast<const uint32_t *>(sc.insts);
+    uint32_t *li = reinterpret_cast<uint32_t *>(l_insts);
+    for (uint32_t i = threadIdx.x; i < sc.n_inst * (uint32_t)(sizeof(Inst) / 4u); i += blockDim.x) li[i] = gi[i];
+    __syncthreads();
+}
+
+template <bool COUNT, bool PROF = false>
+__device__ __forceinline__ Hit trace_core(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack, uint32_t stride,
+                                          float t_max = 1e10f) {
+    return trace_core_tab<COUNT, PROF>(sc, sc.subs, sc.insts, ray, eps, stack, stride, t_max);
 }
 template <bool COUNT>
 __device__ __attribute__((noinline)) Hit trace_ray(const Scene &sc, Ray ray, PassEps eps, uint32_t *stack,

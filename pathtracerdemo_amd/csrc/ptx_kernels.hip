@@ -70,12 +70,16 @@ __device__ __forceinline__ void write_color(const Scene &sc, float4 *accum, size
 }
 
 // =========================================================================== PT_01
-template <bool COUNT>
+template <bool COUNT, bool LDS_TABLES = false>
 __global__ __launch_bounds__(BLOCK) void gbuffer_kernel(Scene sc, uint4 *gbuf) {
+    __shared__ SubRoot l_subs[LDS_TABLES ? kLdsSubs : 1];
+    __shared__ Inst l_insts[LDS_TABLES ? kLdsInsts : 1];
+    if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
     uint32_t x, y;
     if (!pixel_of(sc, x, y)) return;
     uint32_t *stack = lds_stack + threadIdx.x;
-    Hit h = trace_core<COUNT>(sc, camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);
+    Hit h = trace_core_tab<COUNT>(sc, LDS_TABLES ? l_subs : sc.subs, LDS_TABLES ? l_insts : sc.insts,
+                                  camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);
     Compact s = h.s;
     s.valid = h.valid ? 1u : 0u;
     gbuf[band_index(sc, x, y)] = encode(s);
@@ -334,8 +338,13 @@ static dim3 grid_of(const Scene &sc) {
     return dim3((sc.width + TILE - 1) / TILE, (sc.row_end - sc.row_begin + TILE - 1) / TILE, 1);
 }
 hipError_t launch_gbuffer(const Scene &sc, uint4 *gbuf, uint32_t depth, hipStream_t s) {
-    if (sc.counters) hipLaunchKernelGGL(gbuffer_kernel<true>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
-    else hipLaunchKernelGGL(gbuffer_kernel<false>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
+    const bool tables_fit = sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts;
+    if (sc.counters)
+        hipLaunchKernelGGL(gbuffer_kernel<true>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
+    else if (tables_fit)
+        hipLaunchKernelGGL((gbuffer_kernel<false, true>), grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
+    else
+        hipLaunchKernelGGL(gbuffer_kernel<false>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
     return hipGetLastError();
 }
 hipError_t launch_init(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, uint32_t depth, hipStream_t s) {

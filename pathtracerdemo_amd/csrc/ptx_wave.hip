@@ -154,11 +154,16 @@ __device__ __forceinline__ uint32_t padded_pixels(const Scene &sc) {
 // hit range capped at the remaining distance to the light: Visibility only looks at the
 // closest hit when its t <= remain, and the cap leaves the visit order -- hence which of
 // several equal-t triangles wins -- unchanged for every hit inside the cap.
-template <bool COUNT, int WAVES, bool SPEC>
+template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true>
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     extern __shared__ uint32_t wstack[];
     uint32_t *stack = wstack + threadIdx.x;
+    __shared__ SubRoot l_subs[LDS_TABLES ? kLdsSubs : 1];
+    __shared__ Inst l_insts[LDS_TABLES ? kLdsInsts : 1];
+    if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
+    const SubRoot *subs = LDS_TABLES ? l_subs : sc.subs;
+    const Inst *insts = LDS_TABLES ? l_insts : sc.insts;
     const uint32_t j = blockIdx.x;
     const uint32_t n = w.cnt[(2u * round + 1u) * w.nseg + j];
     const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
@@ -171,7 +176,8 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         // one trace site, looped, so the traversal code is emitted once
         float T = 1.0f, remain = a.w;
         for (uint32_t it = 0u;; ++it) {
-            const Hit h = trace_core<COUNT, SPEC>(sc, r, eps, stack, WB, vis ? fminf(remain, 1e10f) : 1e10f);
+            const Hit h = trace_core_tab<COUNT, PROF>(sc, subs, insts, r, eps, stack, WB,
+                                                      vis ? fminf(remain, 1e10f) : 1e10f);
             if (!vis) {
                 const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
                 res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
@@ -536,7 +542,7 @@ __global__ __launch_bounds__(WB) void winit_start(Scene sc, WaveBufs w, const ui
             const Compact x1 = gdecode(gbuf[pix]);
             if (!x1.valid) {  // reservoir unobservable: PT_4 returns before LoadReservoir (:1404-1408)
                 uint4 *out = reservoir + 8u * (size_t)pix;
-                for (int k = 0; k < 8; ++k) out[k] = make_uint4(0u, 0u, 0u, 0u);
+                for (int q8 = 0; q8 < 8; ++q8) out[q8] = make_uint4(0u, 0u, 0u, 0u);
             } else {
                 active = true;
                 s.seed = pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u);
@@ -759,8 +765,8 @@ __global__ __launch_bounds__(WB) void wfinal_step(Scene sc, WaveBufs w, uint32_t
             const float4 hd = state[FS_HDR * npix + pix], fv = state[FS_F * npix + pix];
             const float4 cu = state[FS_CUR * npix + pix], nr = state[FS_NRM * npix + pix];
             const float4 pv = state[FS_PREV * npix + pix];
-            const uint32_t w = asu(hd.x);
-            s.i = w & 0xffu; s.length = (w >> 8) & 0xffu; s.phase = w >> 16;
+            const uint32_t hw = asu(hd.x);
+            s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = hw >> 16;
             s.seed1 = asu(hd.y); s.idx = asu(hd.z);
             s.f = mk(fv.x, fv.y, fv.z); s.ucw = fv.w;
             s.prev = mk(pv.x, pv.y, pv.z);
@@ -971,16 +977,20 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
         else
             hipLaunchKernelGGL(trace_queue_sm<false>, dim3(w.nseg), dim3(WB), lds, s, sc, w.rays, res, cnt,
                                w.ray_stride, 0u, eps);
-    } else if (sc.counters)
-        hipLaunchKernelGGL((trace_queue<true, 6, false>), dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+    } else if (sc.counters && getenv("PTX_TRACE_PROF"))  // SIMD-utilisation diagnostics
+        hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round,
+                           eps);
+    else if (sc.counters)
+        hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     else {
-        // A/B switches (profiling only): occupancy target and speculative traversal.  8 waves
-        // per SIMD measured ~2% faster than 6 despite a small spill; speculation is neutral.
-        static const int occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 8;
-        static const bool spec = getenv("PTX_TRACE_SPEC") != nullptr;
-        auto k = spec       ? trace_queue<false, 8, true>
-                 : occ >= 8 ? trace_queue<false, 8, false>
-                 : occ == 7 ? trace_queue<false, 7, false> : trace_queue<false, 6, false>;
+        // A/B switches (profiling only): occupancy target, LDS-staged tables.  Measured at
+        // 1080p C1: 5 waves/SIMD (94 VGPRs, no spill) with LDS tables is fastest; capping
+        // registers lower spills in the traversal loop.
+        static const int occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 5;
+        const bool tables_fit = sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts && !getenv("PTX_TRACE_NOLDS");
+        auto k = !tables_fit ? trace_queue<false, 5, false, false>
+                 : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
+                 : occ == 6  ? trace_queue<false, 6> : occ == 5 ? trace_queue<false, 5> : trace_queue<false, 4>;
         hipLaunchKernelGGL(k, dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     }
     return hipGetLastError();

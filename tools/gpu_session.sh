@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 STEPS=${STEPS:-10}
-timeout -k 10 ${TEST_TIMEOUT:-420} python -m pytest tests -m gpu -q -s ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${TEST_TIMEOUT:-420} python -u -m pytest tests -m gpu -q -s -p timeout --timeout 150 ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -n 30 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: pytest crashed/timed out"; exit $rc; fi
