@@ -57,6 +57,9 @@ extern "C" {
 /* stats-only slots: every launch of the wavefront pipeline's kernels, by kind */
 #define PTX_STAT_WAVE_TRACE 5  /* trace_queue launches (ray-segment traversal)      */
 #define PTX_STAT_WAVE_LOGIC 6  /* start/step launches (shading, RIS, queue appends) */
+#define PTX_STAT_FRAME 7       /* whole ptx_render frames of the wavefront ReSTIR path, which
+                                  overlaps its passes: slots 0..2 then only get the per-part
+                                  G-buffer launches, with PTX_FLAG_TIME_LAUNCHES          */
 
 /* buffers for ptx_read_buffer / ptx_write_buffer / ptx_device_pointer */
 #define PTX_BUF_GBUFFER 0    /* band_h * W * 4 u32   */

@@ -9,12 +9,13 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libptx.so")
+# PTX_LIB_PATH overrides the in-tree library (same-box A/B of two builds); it must still exist
+LIB_PATH = os.environ.get("PTX_LIB_PATH") or os.path.join(PKG_DIR, "libptx.so")
 
 PTX_OK = 0
 PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT = 0, 1
 PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT, PTX_PASS_TRACE = 0, 1, 2, 3, 4
-PTX_STAT_WAVE_TRACE, PTX_STAT_WAVE_LOGIC = 5, 6  # stats-only slots (include/ptx.h)
+PTX_STAT_WAVE_TRACE, PTX_STAT_WAVE_LOGIC, PTX_STAT_FRAME = 5, 6, 7  # stats-only slots (include/ptx.h)
 PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS = 0, 1, 2, 3
 PTX_FLAG_COUNT_WORK = 1
 PTX_FLAG_SIMPLE_KERNELS = 2

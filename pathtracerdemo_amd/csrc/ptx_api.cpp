@@ -65,6 +65,11 @@ struct ptx_handle {
     // wavefront variant: pixel state, ray queue + ping-pong results / active lists, counters
     DevBuf d_wstate, d_wrays, d_wres0, d_wres1, d_wact0, d_wact1, d_wctr;
     size_t wave_ray_cap = 0;
+    // second stream: the two halves of the segments run as independent launch sequences so
+    // one half's latency-bound traces overlap the other's ALU-bound shading
+    static constexpr int kMaxSplit = 4;  // GPU_MAX_HW_QUEUES is 4 on the target boxes
+    hipStream_t sub[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};  // sub[0] unused (= stream)
+    hipEvent_t ev_fork = nullptr, ev_join[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
     // stats
     TimedLaunch ring[kEventRing];
     int ring_pos = 0;
@@ -317,25 +322,28 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     w.act[0] = (uint32_t *)h->d_wact0.p;
     w.act[1] = (uint32_t *)h->d_wact1.p;
     w.cnt = (uint32_t *)h->d_wctr.p;
+    w.seg_base = 0;
+    w.seg_count = w.nseg;
     return PTX_OK;
 }
 
 // One secondary pass as a fixed sequence of wavefront rounds (no host sync inside).
 // Event pair around one launch, accounted to stats slot `slot` (resolved lazily).
-static TimedLaunch *event_begin(ptx_handle *h, int slot) {
+static TimedLaunch *event_begin(ptx_handle *h, int slot, hipStream_t st) {
     if (!(h->cfg.flags & PTX_FLAG_TIME_LAUNCHES)) return nullptr;  // events cost ~5% of a frame
     TimedLaunch &t = h->ring[h->ring_pos];
     h->ring_pos = (h->ring_pos + 1) % kEventRing;
     resolve_event(t, h);
-    if (hipEventRecord(t.start, h->stream) != hipSuccess) return nullptr;
+    if (hipEventRecord(t.start, st) != hipSuccess) return nullptr;
     t.pass = slot;
     return &t;
 }
-static void event_end(ptx_handle *h, TimedLaunch *t) {
-    if (t && hipEventRecord(t->stop, h->stream) == hipSuccess) t->pending = true;
+static void event_end(TimedLaunch *t, hipStream_t st) {
+    if (t && hipEventRecord(t->stop, st) == hipSuccess) t->pending = true;
 }
 
-static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass) {
+// One pass over the segments [w.seg_base, w.seg_base + w.seg_count) on stream `st`.
+static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass, hipStream_t st) {
     const uint4 *gb = (const uint4 *)h->d_gbuf.p;
     uint4 *res = (uint4 *)h->d_res.p;
     float4 *acc = (float4 *)h->d_accum.p;
@@ -344,18 +352,96 @@ static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBuf
                                                                                         : kWaveRoundsMcpt;
     for (int r = 0; e == hipSuccess && r <= rounds; ++r) {
         if (r > 0) {
-            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE);
-            e = wave_trace(sc, w, r - 1, 1, h->stack_depth, h->stream);
-            event_end(h, t);
+            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
+            e = wave_trace(sc, w, r - 1, 1, h->stack_depth, st);
+            event_end(t, st);
         }
         if (e != hipSuccess) break;
-        TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC);
-        e = pass == PTX_PASS_INIT    ? wave_init_round(sc, w, r, gb, res, h->stream)
-            : pass == PTX_PASS_FINAL ? wave_final_round(sc, w, r, gb, res, acc, h->stream)
-                                     : wave_mcpt_round(sc, w, r, acc, h->stream);
-        event_end(h, t);
+        TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
+        e = pass == PTX_PASS_INIT    ? wave_init_round(sc, w, r, gb, res, st)
+            : pass == PTX_PASS_FINAL ? wave_final_round(sc, w, r, gb, res, acc, st)
+                                     : wave_mcpt_round(sc, w, r, acc, st);
+        event_end(t, st);
     }
     return e;
+}
+
+// Passes over the segments split into K independent launch sequences on K streams
+// (fork/join through events on the handle's stream), so one part's latency-bound traces
+// overlap another's ALU-bound shading and trace tails.  Each part runs `passes` in order
+// over its own segments (a frame: G-buffer -> init -> final per part, nothing shared).
+// PTX_WAVE_STREAMS=1..4 overrides K (A/B; 2 measured best, 4 oversubscribes the queues).
+static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes,
+                                   int npasses) {
+    static const int env_k = getenv("PTX_WAVE_STREAMS") ? atoi(getenv("PTX_WAVE_STREAMS")) : 0;
+    int k = env_k > 0 ? env_k : 2;
+    k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
+    if ((uint32_t)k > w.nseg) k = (int)w.nseg;
+    hipError_t e = hipSuccess;
+    if (k > 1) {
+        if (!h->ev_fork && (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return e;
+        for (int q = 1; q < k; ++q) {
+            if (!h->sub[q] && (e = hipStreamCreateWithFlags(&h->sub[q], hipStreamNonBlocking)) != hipSuccess)
+                return e;
+            if (!h->ev_join[q] &&
+                (e = hipEventCreateWithFlags(&h->ev_join[q], hipEventDisableTiming)) != hipSuccess)
+                return e;
+        }
+        if ((e = hipEventRecord(h->ev_fork, h->stream)) != hipSuccess) return e;
+        for (int q = 1; q < k; ++q)
+            if ((e = hipStreamWaitEvent(h->sub[q], h->ev_fork, 0)) != hipSuccess) return e;
+    }
+    for (int q = 0; q < k; ++q) {
+        WaveBufs part = w;
+        part.seg_base = (uint32_t)((uint64_t)w.nseg * q / k);
+        part.seg_count = (uint32_t)((uint64_t)w.nseg * (q + 1) / k) - part.seg_base;
+        hipStream_t st = q ? h->sub[q] : h->stream;
+        for (int i = 0; i < npasses; ++i) {
+            if (passes[i] == PTX_PASS_GBUFFER) {
+                TimedLaunch *t = event_begin(h, PTX_PASS_GBUFFER, st);
+                e = wave_gbuffer(sc, part, (uint4 *)h->d_gbuf.p, h->stack_depth, st);
+                event_end(t, st);
+            } else {
+                e = launch_wave_seq(h, sc, part, passes[i], st);
+            }
+            if (e != hipSuccess) return e;
+        }
+    }
+    for (int q = 1; q < k; ++q) {
+        if ((e = hipEventRecord(h->ev_join[q], h->sub[q])) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(h->stream, h->ev_join[q], 0)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass) {
+    return launch_wave_parts(h, sc, w, &pass, 1);
+}
+
+// A whole ReSTIR frame in wavefront form (G-buffer -> init -> final per segment group), timed
+// as one unit in stats slot PTX_STAT_FRAME.  Returns 1 if this path does not apply.
+static int timed_wave_frame(ptx_handle *h) {
+    const uint32_t fl = h->cfg.flags;
+    if (fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE | PTX_FLAG_COUNT_WORK))
+        return 1;
+    if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before rendering");
+    if (!h->layout_valid) {
+        if (int rc = build_layout(h)) return rc;
+    }
+    Scene sc = make_scene(h);
+    if (!tables_fit_lds(sc)) return 1;
+    WaveBufs w{};
+    if (int rc = wave_buffers(h, w)) return rc;
+    TimedLaunch &t = h->ring[h->ring_pos];
+    h->ring_pos = (h->ring_pos + 1) % kEventRing;
+    resolve_event(t, h);
+    HIP_CHECK(h, hipEventRecord(t.start, h->stream));
+    static const int passes[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL};
+    hipError_t e = launch_wave_parts(h, sc, w, passes, 3);
+    if (e != hipSuccess) return fail(h, PTX_E_HIP, "wavefront frame launch: %s", hipGetErrorString(e));
+    HIP_CHECK(h, hipEventRecord(t.stop, h->stream));
+    t.pass = PTX_STAT_FRAME;
+    t.pending = true;
+    return PTX_OK;
 }
 
 static int timed_launch(ptx_handle *h, int pass) {
@@ -519,8 +605,11 @@ int ptx_run_pass(ptx_handle *h, int pass) {
 int ptx_render(ptx_handle *h, float *rgba_out) {
     if (!h) return PTX_E_INVALID;
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR) {
-        for (int p : {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL})
-            if (int rc = timed_launch(h, p)) return rc;
+        int rc = timed_wave_frame(h);
+        if (rc < 0) return rc;
+        if (rc == 1)  // other variants / counting builds: pass by pass
+            for (int p : {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL})
+                if ((rc = timed_launch(h, p))) return rc;
     } else {
         if (int rc = timed_launch(h, PTX_PASS_MCPT)) return rc;
     }
@@ -643,6 +732,9 @@ int ptx_set_stream(ptx_handle *h, void *hip_stream) {
 
 int ptx_destroy(ptx_handle *h) {
     if (!h) return PTX_E_INVALID;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (hipStream_t q : h->sub)
+        if (q) (void)hipStreamSynchronize(q);
     if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
     for (auto &t : h->ring) {
         if (t.start) (void)hipEventDestroy(t.start);
@@ -652,6 +744,11 @@ int ptx_destroy(ptx_handle *h) {
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr})
         free_buf(*b);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {
+        if (h->ev_join[q]) (void)hipEventDestroy(h->ev_join[q]);
+        if (h->sub[q]) (void)hipStreamDestroy(h->sub[q]);
+    }
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
     return PTX_OK;

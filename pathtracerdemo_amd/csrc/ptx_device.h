@@ -372,7 +372,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
 // every instance, ~16 table reads per query otherwise paid as scalar-load round trips.
 // Called by all threads of the workgroup (ends with a barrier).
 constexpr uint32_t kLdsSubs = 128, kLdsInsts = 8;
-__device__ __forceinline__ bool tables_fit_lds(const Scene &sc) {
+__host__ __device__ __forceinline__ bool tables_fit_lds(const Scene &sc) {
     return sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts;
 }
 __device__ __forceinline__ void stage_tables(const Scene &sc, SubRoot *l_subs, Inst *l_insts) {

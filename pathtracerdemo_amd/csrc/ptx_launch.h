@@ -51,7 +51,9 @@ struct WaveBufs {
     float4 *state;       // kWaveStateSlots * npix, SoA
     uint32_t npix;       // pixels of the band
     uint32_t seg_px;     // padded pixels per segment
-    uint32_t nseg;       // segments (= workgroups per launch)
+    uint32_t nseg;       // segments of the band
+    uint32_t seg_base;   // first segment of this launch sequence (workgroup j -> segment
+    uint32_t seg_count;  //   seg_base + j), and how many it covers
     uint32_t ray_stride; // ray slots per segment (seg_px * max rays per pixel per round)
     float4 *rays;        // 2 float4 per ray: {o, remain}, {d, kind}
     float4 *res[2];      // 2 float4 per ray, ping-pong by round parity
@@ -64,6 +66,7 @@ hipError_t wave_init_round(const Scene &sc, const WaveBufs &w, int round, const 
                            hipStream_t s);
 hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, const uint4 *reservoir,
                             float4 *accum, hipStream_t s);
+hipError_t wave_gbuffer(const Scene &sc, const WaveBufs &w, uint4 *gbuf, uint32_t stack_depth, hipStream_t s);
 hipError_t launch_trace_rays_sm(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
                                 uint32_t stack_depth, hipStream_t s);
 hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, hipStream_t s);

@@ -71,7 +71,7 @@ struct Seg {
 };
 __device__ __forceinline__ Seg seg_begin(const WaveBufs &w, uint32_t round, uint32_t *lds) {
     Seg g;
-    g.j = blockIdx.x;
+    g.j = w.seg_base + blockIdx.x;
     g.round = round;
     g.rbase = g.j * w.ray_stride;
     g.rays = w.rays;
@@ -164,7 +164,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
     const SubRoot *subs = LDS_TABLES ? l_subs : sc.subs;
     const Inst *insts = LDS_TABLES ? l_insts : sc.insts;
-    const uint32_t j = blockIdx.x;
+    const uint32_t j = w.seg_base + blockIdx.x;
     const uint32_t n = w.cnt[(2u * round + 1u) * w.nseg + j];
     const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
     float4 *res = w.res[round & 1u] + 2u * (size_t)j * w.ray_stride;
@@ -377,6 +377,33 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
             }
         }
     }
+}
+
+// =========================================================================== PT_01 (G-buffer)
+// PT_01 over the pixels of segments [seg_base, seg_base + seg_count): 4 workgroups per
+// segment, one 8x8 tile per wave, so a frame can run G-buffer -> init -> final per segment
+// group with no dependency between groups.  Same ray, epsilons and traversal as
+// gbuffer_kernel (SH/PT_01_GBufferPass.wgsl:496-507,643-656).
+__global__ __launch_bounds__(WB) void wgbuffer(Scene sc, WaveBufs w, uint4 *gbuf) {
+    extern __shared__ uint32_t wstack[];
+    uint32_t *stack = wstack + threadIdx.x;
+    __shared__ SubRoot l_subs[kLdsSubs];
+    __shared__ Inst l_insts[kLdsInsts];
+    stage_tables(sc, l_subs, l_insts);
+    const uint32_t j = w.seg_base + blockIdx.x / 4u, k = (blockIdx.x % 4u) * WB;
+    const uint32_t q = seg_pixel(w, j, k);
+    uint32_t x, y;
+    if (q >= padded_pixels(sc) || !tile_xy(sc, q, x, y)) return;
+    const float *vpinv = reinterpret_cast<const float *>(sc.U + U_VPINV);
+    const float u = ((float)x + 0.5f) / (float)sc.U[U_W];
+    const float v = ((float)y + 0.5f) / (float)sc.U[U_H];
+    const f3 st = xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
+    const f3 en = xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f + 1.0f));
+    const Hit h = trace_core_tab<false>(sc, l_subs, l_insts, Ray{st, normalize(en - st)}, PassEps{1e-8f, 1e-6f},
+                                        stack, WB);
+    Compact c = h.s;
+    c.valid = h.valid ? 1u : 0u;
+    gbuf[(y - sc.row_begin) * sc.width + x] = gencode(c);
 }
 
 // =========================================================================== PT_1 (init)
@@ -969,19 +996,21 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
     const size_t lds = stack_lds_bytes(depth);
     static const bool refill = getenv("PTX_TRACE_REFILL") != nullptr;  // A/B switch for profiling
     if (refill) {
-        const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.nseg;
-        float4 *res = w.res[round & 1];
+        const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.nseg + w.seg_base;
+        float4 *res = w.res[round & 1] + 2u * (size_t)w.seg_base * w.ray_stride;
         if (sc.counters)
-            hipLaunchKernelGGL(trace_queue_sm<true>, dim3(w.nseg), dim3(WB), lds, s, sc, w.rays, res, cnt,
+            hipLaunchKernelGGL(trace_queue_sm<true>, dim3(w.seg_count), dim3(WB), lds, s, sc,
+                               w.rays + 2u * (size_t)w.seg_base * w.ray_stride, res, cnt,
                                w.ray_stride, 0u, eps);
         else
-            hipLaunchKernelGGL(trace_queue_sm<false>, dim3(w.nseg), dim3(WB), lds, s, sc, w.rays, res, cnt,
+            hipLaunchKernelGGL(trace_queue_sm<false>, dim3(w.seg_count), dim3(WB), lds, s, sc,
+                               w.rays + 2u * (size_t)w.seg_base * w.ray_stride, res, cnt,
                                w.ray_stride, 0u, eps);
     } else if (sc.counters && getenv("PTX_TRACE_PROF"))  // SIMD-utilisation diagnostics
-        hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round,
+        hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round,
                            eps);
     else if (sc.counters)
-        hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+        hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     else {
         // A/B switches (profiling only): occupancy target, LDS-staged tables.  Measured at
         // 1080p C1: 5 waves/SIMD (94 VGPRs, no spill) with LDS tables is fastest; capping
@@ -991,7 +1020,7 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
                  : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
                  : occ == 6  ? trace_queue<false, 6> : occ == 5 ? trace_queue<false, 5> : trace_queue<false, 4>;
-        hipLaunchKernelGGL(k, dim3(w.nseg), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+        hipLaunchKernelGGL(k, dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     }
     return hipGetLastError();
 }
@@ -1012,32 +1041,38 @@ hipError_t launch_trace_rays_sm(const Scene &sc, const float4 *rays, float4 *hit
     return hipGetLastError();
 }
 
+hipError_t wave_gbuffer(const Scene &sc, const WaveBufs &w, uint4 *gbuf, uint32_t depth, hipStream_t s) {
+    if (!tables_fit_lds(sc)) return hipErrorInvalidValue;  // caller falls back to gbuffer_kernel
+    hipLaunchKernelGGL(wgbuffer, dim3(4u * w.seg_count), dim3(WB), stack_lds_bytes(depth), s, sc, w, gbuf);
+    return hipGetLastError();
+}
+
 // Logic round r consumes the results of trace round r-1 and emits the rays of trace round r.
 hipError_t wave_init_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, uint4 *reservoir,
                            hipStream_t s) {
     if (round == 0)
-        hipLaunchKernelGGL(winit_start, dim3(w.nseg), dim3(WB), 0, s, sc, w, gbuf, reservoir);
+        hipLaunchKernelGGL(winit_start, dim3(w.seg_count), dim3(WB), 0, s, sc, w, gbuf, reservoir);
     else
-        hipLaunchKernelGGL(winit_step, dim3(w.nseg), dim3(WB), 0, s, sc, w, (uint32_t)round, reservoir);
+        hipLaunchKernelGGL(winit_step, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, reservoir);
     return hipGetLastError();
 }
 
 hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, const uint4 *reservoir,
                             float4 *accum, hipStream_t s) {
     if (round == 0)
-        hipLaunchKernelGGL(wfinal_start, dim3(w.nseg), dim3(WB), 0, s, sc, w, gbuf, reservoir, accum);
+        hipLaunchKernelGGL(wfinal_start, dim3(w.seg_count), dim3(WB), 0, s, sc, w, gbuf, reservoir, accum);
     else
-        hipLaunchKernelGGL(wfinal_step, dim3(w.nseg), dim3(WB), 0, s, sc, w, (uint32_t)round, reservoir, accum);
+        hipLaunchKernelGGL(wfinal_step, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, reservoir, accum);
     return hipGetLastError();
 }
 
 hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, hipStream_t s) {
     if (round == 0)
-        hipLaunchKernelGGL(wmcpt_start, dim3(w.nseg), dim3(WB), 0, s, sc, w);
+        hipLaunchKernelGGL(wmcpt_start, dim3(w.seg_count), dim3(WB), 0, s, sc, w);
     else if (round == 1)
-        hipLaunchKernelGGL(wmcpt_step<1>, dim3(w.nseg), dim3(WB), 0, s, sc, w, (uint32_t)round, accum);
+        hipLaunchKernelGGL(wmcpt_step<1>, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, accum);
     else
-        hipLaunchKernelGGL(wmcpt_step<0>, dim3(w.nseg), dim3(WB), 0, s, sc, w, (uint32_t)round, accum);
+        hipLaunchKernelGGL(wmcpt_step<0>, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, accum);
     return hipGetLastError();
 }
 

@@ -159,7 +159,8 @@ def test_restir_pipeline_4_frames(scene1, oracle_mod):
     assert err <= 1e-3
     np.testing.assert_array_equal(img.view(np.uint32), fr.accum.view(np.uint32))
     st = r.stats()
-    assert st["frames"] == 4 and st["kernel_launches"][:3] == [4, 4, 4]
+    # the default wavefront path overlaps the three passes and times whole frames (slot 7)
+    assert st["frames"] == 4 and st["kernel_launches"][7] == 4
 
 
 def test_band_split_is_bit_identical(scene1, oracle_mod):
