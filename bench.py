@@ -125,11 +125,14 @@ def main():
 
     # Second timed region, same K steps, with HIP events around every wavefront launch
     # (PTX_FLAG_TIME_LAUNCHES costs ~5% of a frame, so the headline region above runs
-    # without them): per-launch durations of the dominant kernel for the roofline.
+    # without them): per-launch durations of the dominant kernel for the roofline.  It runs
+    # as ONE launch sequence (PTX_FLAG_SINGLE_STREAM): in the two-stream production frame
+    # two kernels share the GPU and a launch's duration measures the share, not the kernel;
+    # the overlap's gain is in `value` and in roofline.frame.
     st_k = None
     if args.variant == "wave":
         rk = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
-                      variant=args.variant, time_launches=True)
+                      variant=args.variant, time_launches=True, single_stream=True)
         rk.Initialize(cs)
         for _ in range(max(1, args.warmup)):
             rk.Update()

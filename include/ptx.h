@@ -73,6 +73,8 @@ extern "C" {
 #define PTX_FLAG_TILED_EXCHANGE 8u   /* A/B: 16x16 tiles with an LDS ray exchange             */
 #define PTX_FLAG_TIME_LAUNCHES 16u   /* HIP events around every wavefront launch (stats slots
                                         PTX_STAT_WAVE_*); costs ~5% of frame time            */
+#define PTX_FLAG_SINGLE_STREAM 32u   /* run the wavefront passes as one launch sequence (no
+                                        two-stream overlap): isolated per-kernel timings     */
 /* no variant flag: the wavefront pipeline (compacted ray queues, one trace round per
    path vertex) -- the default */
 

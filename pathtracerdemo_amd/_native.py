@@ -22,6 +22,7 @@ PTX_FLAG_SIMPLE_KERNELS = 2
 PTX_FLAG_PERSISTENT_LANES = 4
 PTX_FLAG_TILED_EXCHANGE = 8
 PTX_FLAG_TIME_LAUNCHES = 16
+PTX_FLAG_SINGLE_STREAM = 32
 VARIANT_FLAGS = {"wave": 0, "tiled": PTX_FLAG_TILED_EXCHANGE, "persistent": PTX_FLAG_PERSISTENT_LANES,
                  "simple": PTX_FLAG_SIMPLE_KERNELS}
 

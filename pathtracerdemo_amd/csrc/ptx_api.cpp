@@ -375,6 +375,7 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
                                    int npasses) {
     static const int env_k = getenv("PTX_WAVE_STREAMS") ? atoi(getenv("PTX_WAVE_STREAMS")) : 0;
     int k = env_k > 0 ? env_k : 2;
+    if (h->cfg.flags & PTX_FLAG_SINGLE_STREAM) k = 1;
     k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
     if ((uint32_t)k > w.nseg) k = (int)w.nseg;
     hipError_t e = hipSuccess;

@@ -20,7 +20,7 @@ from .scene.world import CompiledScene, World, serialize_world
 class Renderer:
     def __init__(self, width: int, height: int, device: int = -1, pipeline: str = "restir",
                  row_begin: int = 0, row_end: int = 0, count_work: bool = False, variant: str = "wave",
-                 time_launches: bool = False):
+                 time_launches: bool = False, single_stream: bool = False):
         self._lib = N.load()
         self.width, self.height = int(width), int(height)
         self.pipeline = pipeline
@@ -28,7 +28,8 @@ class Renderer:
                           device=device,
                           pipeline=N.PTX_PIPELINE_MCPT if pipeline == "mcpt" else N.PTX_PIPELINE_RESTIR,
                           flags=(N.PTX_FLAG_COUNT_WORK if count_work else 0) | N.VARIANT_FLAGS[variant]
-                          | (N.PTX_FLAG_TIME_LAUNCHES if time_launches else 0))
+                          | (N.PTX_FLAG_TIME_LAUNCHES if time_launches else 0)
+                          | (N.PTX_FLAG_SINGLE_STREAM if single_stream else 0))
         self._h = ctypes.c_void_p()
         rc = self._lib.ptx_create(ctypes.byref(cfg), ctypes.byref(self._h))
         if rc != N.PTX_OK:

@@ -5,6 +5,10 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=${TAG:-r1}
 ARGS=${BENCH_ARGS:-}
 cd /tmp && export TMPDIR=/tmp
+# one launch sequence per pass: per-kernel durations then match bench.py's launch-timing
+# region (PTX_FLAG_SINGLE_STREAM); the two-stream production overlap is measured by the
+# bench's headline value, not by per-kernel averages
+export PTX_WAVE_STREAMS=${PTX_WAVE_STREAMS:-1}
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
