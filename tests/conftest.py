@@ -20,6 +20,13 @@ def scene1():
 
 
 @pytest.fixture(scope="session")
+def scene3():
+    """Config C3: the build-defined many-light interior (scenes/make_c3.py, 32 rect lights)."""
+    from pathtracerdemo_amd.scene.world import compile_scene
+    return compile_scene("c3_interior_32")
+
+
+@pytest.fixture(scope="session")
 def oracle_mod():
     from oracle import oracle
     oracle.build()

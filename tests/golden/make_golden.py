@@ -24,6 +24,19 @@ from pathtracerdemo_amd.scene.world import compile_scene  # noqa: E402
 W, H = 24, 24
 
 
+# (scene, frames) -> fixture file; C3 is the build-defined many-light interior (scenes/make_c3.py)
+FIXTURES = {"c1_24x24_4frames.npz": ("dummy_scene_1", 4), "c3_24x24_2frames.npz": ("c3_interior_32", 2)}
+
+
+def scene_digest(cs) -> np.ndarray:
+    """sha256 of the three device arrays: pins the scene compiler's output too."""
+    import hashlib
+    h = hashlib.sha256()
+    for a in (cs.scene, cs.geometry, cs.accel):
+        h.update(np.ascontiguousarray(a, dtype="<u4").tobytes())
+    return np.frombuffer(h.digest(), dtype=np.uint8)
+
+
 def frame_fixture(cs, frames):
     fr = O.Frame(uniform_for(cs, W, H, 1), cs.scene, cs.geometry, cs.accel)
     for f in range(1, frames + 1):
@@ -32,7 +45,7 @@ def frame_fixture(cs, frames):
     mc = O.Frame(uniform_for(cs, W, H, 1), cs.scene, cs.geometry, cs.accel)
     mc.run(O.PASS_MCPT, threads=1)
     return dict(uniform=fr.uniform, gbuffer=fr.gbuffer, reservoir=fr.reservoir, accum_restir=fr.accum,
-                accum_mcpt=mc.accum)
+                accum_mcpt=mc.accum, frames=np.int32(frames), scene_sha256=scene_digest(cs))
 
 
 def kat_table():
@@ -54,8 +67,8 @@ def kat_table():
 
 def main():
     O.build()
-    cs = compile_scene("dummy_scene_1")
-    np.savez_compressed(os.path.join(HERE, "c1_24x24_4frames.npz"), **frame_fixture(cs, 4))
+    for fname, (scene, frames) in FIXTURES.items():
+        np.savez_compressed(os.path.join(HERE, fname), **frame_fixture(compile_scene(scene), frames))
     with open(os.path.join(HERE, "kat.json"), "w") as fh:
         json.dump(kat_table(), fh, indent=1, sort_keys=True)
     print("wrote", os.listdir(HERE))

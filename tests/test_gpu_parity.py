@@ -141,6 +141,39 @@ def test_alternate_variants(scene1, oracle_mod, native, variant):
     np.testing.assert_array_equal(m.read_image().view(np.uint32), fm.accum.view(np.uint32))
 
 
+def test_c3_many_lights_bit_exact(scene3, oracle_mod, native):
+    """Config C3 (3 instances incl. the chair, 37.8 k triangles, 32 rect lights): every pass
+    bit for bit, the ReSTIR pipeline over 2 frames, and TEST_MCPT (33 queries per bounce)."""
+    W, H = 128, 80
+    fr = oracle_frame(oracle_mod, scene3, W, H)
+    fr.run(oracle_mod.PASS_GBUFFER)
+    fr.run(oracle_mod.PASS_INIT)
+    fr.run(oracle_mod.PASS_FINAL)
+    r = make_renderer(scene3, W, H)
+    r.set_uniform(fr.uniform)
+    r.run_pass(native.PTX_PASS_GBUFFER)
+    np.testing.assert_array_equal(r.read_gbuffer(), fr.gbuffer)
+    r.run_pass(native.PTX_PASS_INIT)
+    np.testing.assert_array_equal(r.read_reservoir(), fr.reservoir)
+    r.reset_accumulation()
+    r.run_pass(native.PTX_PASS_FINAL)
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), fr.accum.view(np.uint32))
+    p = make_renderer(scene3, W, H)
+    fp = oracle_frame(oracle_mod, scene3, W, H)
+    for f in (1, 2):
+        p.Update()
+        p.Render()
+        fp.set_frame_index(f)
+        fp.run(oracle_mod.PASS_RESTIR)
+    np.testing.assert_array_equal(p.read_image().view(np.uint32), fp.accum.view(np.uint32))
+    fm = oracle_frame(oracle_mod, scene3, 64, 48)
+    fm.run(oracle_mod.PASS_MCPT)
+    m = make_renderer(scene3, 64, 48, pipeline="mcpt")
+    m.set_uniform(fm.uniform)
+    m.run_pass(native.PTX_PASS_MCPT)
+    np.testing.assert_array_equal(m.read_image().view(np.uint32), fm.accum.view(np.uint32))
+
+
 def test_restir_pipeline_4_frames(scene1, oracle_mod):
     """Config C1 shape: 256x256, FrameIndex 1..4 accumulated through the Renderer surface."""
     W = H = 256
