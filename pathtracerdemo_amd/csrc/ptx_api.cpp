@@ -293,12 +293,14 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const uint32_t nl = h->uniform[U_LIGHT_COUNT];
     const size_t per_px = std::max<size_t>(2u, (size_t)nl + 1u);
     const size_t padded = (size_t)((h->cfg.width + 7u) / 8u) * ((h->band_h + 7u) / 8u) * 64u;
-    const size_t nseg = (padded + kWaveSegPixels - 1u) / kWaveSegPixels;
-    const size_t cap = per_px * kWaveSegPixels * nseg;
+    static const uint32_t env_px = getenv("PTX_SEG_PX") ? (uint32_t)atoi(getenv("PTX_SEG_PX")) : 0u;  // A/B
+    const uint32_t seg_px = (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) ? env_px : kWaveSegPixels;
+    const size_t nseg = (padded + seg_px - 1u) / seg_px;
+    const size_t cap = per_px * seg_px * nseg;
     if (!h->d_wstate.p) {
         if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wact0, nseg * kWaveSegPixels * 4u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wact1, nseg * kWaveSegPixels * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wact0, nseg * seg_px * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wact1, nseg * seg_px * 4u)) return rc;
         if (int rc = alloc_buf(h, h->d_wctr, 2u * kWaveMaxRounds * nseg * 4u)) return rc;
     }
     if (cap > h->wave_ray_cap) {
@@ -313,9 +315,9 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     }
     w.state = (float4 *)h->d_wstate.p;
     w.npix = (uint32_t)npix;
-    w.seg_px = kWaveSegPixels;
+    w.seg_px = seg_px;
     w.nseg = (uint32_t)nseg;
-    w.ray_stride = (uint32_t)(per_px * kWaveSegPixels);
+    w.ray_stride = (uint32_t)(per_px * seg_px);
     w.rays = (float4 *)h->d_wrays.p;
     w.res[0] = (float4 *)h->d_wres0.p;
     w.res[1] = (float4 *)h->d_wres1.p;
@@ -324,6 +326,8 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     w.cnt = (uint32_t *)h->d_wctr.p;
     w.seg_base = 0;
     w.seg_count = w.nseg;
+    static const uint32_t cl = getenv("PTX_SEG_CLUSTER") ? (uint32_t)atoi(getenv("PTX_SEG_CLUSTER")) : 1u;  // A/B
+    w.cluster = (cl == 2u || cl == 4u || cl == 8u || cl == 16u) ? cl : 1u;
     return PTX_OK;
 }
 

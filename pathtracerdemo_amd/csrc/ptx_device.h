@@ -243,7 +243,10 @@ __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, Pa
 // (entry k at stack[k * stride]).  Also returns the hit position exactly as
 // GetSurface(hit).Position computes it (same world-space vertices and barycentrics).
 // `subs` / `insts` are the scene's sub-root and instance tables, or LDS copies of them.
-template <bool COUNT, bool PROF = false>
+// ROOTQ: sub-mesh roots of an instance go through one per-lane root queue (incoherent
+// secondary rays); otherwise one root at a time for the whole wave (coherent primary rays,
+// whose lanes mostly enter the same roots).  Same per-lane order and results either way.
+template <bool COUNT, bool PROF = false, bool ROOTQ = true>
 __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *subs, const Inst *insts, Ray ray,
                                               PassEps eps, uint32_t *stack, uint32_t stride, float t_max = 1e10f) {
     Prof pf{};
@@ -273,12 +276,20 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
             // reference tests root s against the best t after roots < s (never larger), so
             // this keeps every root it enters; the exact test is repeated when the root is
             // taken below, with the then-current best -- the reference's own test.
-            uint32_t mask = 0u;
 #pragma unroll 1
-            for (uint32_t k = 0; k < nc; ++k) {
+            for (uint32_t kk = 0; kk < (ROOTQ ? 1u : nc); ++kk) {
+            uint32_t mask = 0u;
+            if (ROOTQ) {
+#pragma unroll 1
+                for (uint32_t k = 0; k < nc; ++k) {
+                    float tn;
+                    if (PROF) pf.hit(PROF_ROOT);
+                    if (box_overlap(lo, inv, roots[s0 + k].bmin, roots[s0 + k].bmax, vx, vy, tn)) mask |= 1u << k;
+                }
+            } else {
                 float tn;
                 if (PROF) pf.hit(PROF_ROOT);
-                if (box_overlap(lo, inv, roots[s0 + k].bmin, roots[s0 + k].bmax, vx, vy, tn)) mask |= 1u << k;
+                if (box_overlap(lo, inv, roots[s0 + kk].bmin, roots[s0 + kk].bmax, vx, vy, tn)) mask = 1u << kk;
             }
             // while-while traversal over all of this lane's roots: lanes descend interior
             // nodes (taking their next root, in index order, when the stack runs dry) until
@@ -347,6 +358,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                     best.s.prim = first + k;
                 }
             }
+            }  // roots (ROOTQ: one queue per chunk of 32; else one root at a time)
         }
     }
     if (PROF) {

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(BLOCK) void gbuffer_kernel(Scene sc, uint4 *gbuf) {
     uint32_t x, y;
     if (!pixel_of(sc, x, y)) return;
     uint32_t *stack = lds_stack + threadIdx.x;
-    Hit h = trace_core_tab<COUNT>(sc, LDS_TABLES ? l_subs : sc.subs, LDS_TABLES ? l_insts : sc.insts,
+    Hit h = trace_core_tab<COUNT, false, false>(sc, LDS_TABLES ? l_subs : sc.subs, LDS_TABLES ? l_insts : sc.insts,
                                   camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);
     Compact s = h.s;
     s.valid = h.valid ? 1u : 0u;

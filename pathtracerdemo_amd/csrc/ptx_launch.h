@@ -44,7 +44,7 @@ hipError_t launch_mcpt_tiled(const Scene &sc, float4 *accum, uint32_t stack_dept
 // (cnt[(2r) * nseg + j] pixels of segment j active after logic round r, cnt[(2r+1) *
 // nseg + j] rays it emitted), so the host never synchronises inside a pass.
 constexpr uint32_t kWaveStateSlots = 9u;   // float4 per pixel (PT_1 needs the most)
-constexpr uint32_t kWaveSegPixels = 1024u; // padded pixels per segment (16 8x8 tiles)
+constexpr uint32_t kWaveSegPixels = 512u;  // padded pixels per segment (8 8x8 tiles); 512 > 1024 > 256
 constexpr int kWaveRoundsInit = 3, kWaveRoundsFinal = 3, kWaveRoundsMcpt = 4;
 constexpr int kWaveMaxRounds = 5;
 struct WaveBufs {
@@ -54,6 +54,7 @@ struct WaveBufs {
     uint32_t nseg;       // segments of the band
     uint32_t seg_base;   // first segment of this launch sequence (workgroup j -> segment
     uint32_t seg_count;  //   seg_base + j), and how many it covers
+    uint32_t cluster;    // segment layout: 16/cluster runs of `cluster` adjacent 8x8 tiles
     uint32_t ray_stride; // ray slots per segment (seg_px * max rays per pixel per round)
     float4 *rays;        // 2 float4 per ray: {o, remain}, {d, kind}
     float4 *res[2];      // 2 float4 per ray, ping-pong by round parity

@@ -93,13 +93,17 @@ __device__ __forceinline__ void seg_end(const WaveBufs &w, const Seg &g) {
         w.cnt[(2u * g.round + 1u) * w.nseg + g.j] = *g.l_ray;
     }
 }
-// Padded pixel handled by this thread at offset k of segment j.  A segment is 16 8x8
-// tiles spread over the whole band (tile j + t * nseg): each wave still shades one
-// coherent tile, while every segment -- and so every trace workgroup -- sees a sample of
-// the whole image, which keeps the per-segment trace cost even.
+// Padded pixel handled by this thread at offset k of segment j.  A segment is seg_px/64
+// 8x8 tiles spread over the whole band (tile j + t * nseg, cluster 1): each wave still
+// shades one coherent tile, while every segment -- and so every trace workgroup -- sees a
+// sample of the whole image, which keeps the per-segment trace cost even.  Measured at
+// 1080p: spreading beats clustering adjacent tiles (cluster 4: -5 %, 16: -33 %), and
+// 512-pixel segments beat 1024 (+1-3 %), 256 (-9 %) and 2048 (-11 %).
 __device__ __forceinline__ uint32_t seg_pixel(const WaveBufs &w, uint32_t j, uint32_t k) {
-    const uint32_t t = (k + threadIdx.x) >> 6;  // tile slot within the segment
-    return (j + t * w.nseg) * 64u + (threadIdx.x & 63u);
+    const uint32_t s = (k + threadIdx.x) >> 6;  // tile slot within the segment (seg_px / 64)
+    const uint32_t cl = w.cluster;              // runs of `cl` adjacent tiles
+    const uint32_t t = ((s / cl) * w.nseg + j) * cl + s % cl;
+    return t * 64u + (threadIdx.x & 63u);
 }
 // append the active pixel to this round's list (all lanes)
 __device__ __forceinline__ void seg_keep(const Seg &g, bool keep, uint32_t pix) {
@@ -384,14 +388,19 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
 // segment, one 8x8 tile per wave, so a frame can run G-buffer -> init -> final per segment
 // group with no dependency between groups.  Same ray, epsilons and traversal as
 // gbuffer_kernel (SH/PT_01_GBufferPass.wgsl:496-507,643-656).
+template <bool ROOTQ>
 __global__ __launch_bounds__(WB) void wgbuffer(Scene sc, WaveBufs w, uint4 *gbuf) {
     extern __shared__ uint32_t wstack[];
     uint32_t *stack = wstack + threadIdx.x;
     __shared__ SubRoot l_subs[kLdsSubs];
     __shared__ Inst l_insts[kLdsInsts];
     stage_tables(sc, l_subs, l_insts);
-    const uint32_t j = w.seg_base + blockIdx.x / 4u, k = (blockIdx.x % 4u) * WB;
-    const uint32_t q = seg_pixel(w, j, k);
+    // The group's pixels are the tiles t = m * nseg + r, r in [seg_base, seg_base + seg_count)
+    // (seg_pixel's layout, cluster 1); walking them in raster order gives each workgroup 4
+    // adjacent tiles (a 32x8 strip) -- primary rays of one CU then share BVH nodes in L1.
+    const uint32_t L = blockIdx.x * 4u + threadIdx.x / 64u, run = w.cluster * w.seg_count;
+    const uint32_t t = (L / run) * w.cluster * w.nseg + w.cluster * w.seg_base + L % run;
+    const uint32_t q = t * 64u + (threadIdx.x & 63u);
     uint32_t x, y;
     if (q >= padded_pixels(sc) || !tile_xy(sc, q, x, y)) return;
     const float *vpinv = reinterpret_cast<const float *>(sc.U + U_VPINV);
@@ -399,8 +408,8 @@ __global__ __launch_bounds__(WB) void wgbuffer(Scene sc, WaveBufs w, uint4 *gbuf
     const float v = ((float)y + 0.5f) / (float)sc.U[U_H];
     const f3 st = xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
     const f3 en = xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f + 1.0f));
-    const Hit h = trace_core_tab<false>(sc, l_subs, l_insts, Ray{st, normalize(en - st)}, PassEps{1e-8f, 1e-6f},
-                                        stack, WB);
+    const Hit h = trace_core_tab<false, false, ROOTQ>(sc, l_subs, l_insts, Ray{st, normalize(en - st)},
+                                                      PassEps{1e-8f, 1e-6f}, stack, WB);
     Compact c = h.s;
     c.valid = h.valid ? 1u : 0u;
     gbuf[(y - sc.row_begin) * sc.width + x] = gencode(c);
@@ -1043,7 +1052,13 @@ hipError_t launch_trace_rays_sm(const Scene &sc, const float4 *rays, float4 *hit
 
 hipError_t wave_gbuffer(const Scene &sc, const WaveBufs &w, uint4 *gbuf, uint32_t depth, hipStream_t s) {
     if (!tables_fit_lds(sc)) return hipErrorInvalidValue;  // caller falls back to gbuffer_kernel
-    hipLaunchKernelGGL(wgbuffer, dim3(4u * w.seg_count), dim3(WB), stack_lds_bytes(depth), s, sc, w, gbuf);
+    static const bool rootq = getenv("PTX_GBUF_ROOTQ") != nullptr;  // A/B
+    if (rootq)
+        hipLaunchKernelGGL(wgbuffer<true>, dim3(w.seg_px / WB * w.seg_count), dim3(WB), stack_lds_bytes(depth), s, sc,
+                           w, gbuf);
+    else
+        hipLaunchKernelGGL(wgbuffer<false>, dim3(w.seg_px / WB * w.seg_count), dim3(WB), stack_lds_bytes(depth), s,
+                           sc, w, gbuf);
     return hipGetLastError();
 }
 
