@@ -33,6 +33,9 @@
 namespace ptx {
 
 constexpr uint32_t WB = kBlock;
+#ifndef LOGIC_WAVES
+#define LOGIC_WAVES 4  // start/step kernels: <=128 VGPRs, 4 waves/SIMD, no spill (5 spills)
+#endif
 enum : uint32_t { Q_CLOSEST = 0u, Q_VIS = 1u };
 
 // ---------------------------------------------------------------- wave helpers
@@ -561,7 +564,7 @@ __device__ __forceinline__ void winit_finish(const WInit &s, uint4 *reservoir, u
     out[7] = make_uint4(asu(s.w_sum / s.p_hat_sel), s.C, 0u, 0u);
 }
 
-__global__ __launch_bounds__(WB) void winit_start(Scene sc, WaveBufs w, const uint4 *gbuf, uint4 *reservoir) {
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void winit_start(Scene sc, WaveBufs w, const uint4 *gbuf, uint4 *reservoir) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, 0u, lds);
     float4 *state = w.state;
@@ -599,7 +602,7 @@ __global__ __launch_bounds__(WB) void winit_start(Scene sc, WaveBufs w, const ui
     seg_end(w, g);
 }
 
-__global__ __launch_bounds__(WB) void winit_step(Scene sc, WaveBufs w, uint32_t round, uint4 *reservoir) {
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void winit_step(Scene sc, WaveBufs w, uint32_t round, uint4 *reservoir) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, round, lds);
     float4 *state = w.state;
@@ -743,7 +746,7 @@ __device__ __forceinline__ void wfinal_store(float4 *state, uint32_t npix, uint3
     state[FS_PREV * npix + pix] = make_float4(s.prev.x, s.prev.y, s.prev.z, 0.0f);
 }
 
-__global__ __launch_bounds__(WB) void wfinal_start(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir,
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wfinal_start(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir,
                                                    float4 *accum) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, 0u, lds);
@@ -784,7 +787,7 @@ __global__ __launch_bounds__(WB) void wfinal_start(Scene sc, WaveBufs w, const u
     seg_end(w, g);
 }
 
-__global__ __launch_bounds__(WB) void wfinal_step(Scene sc, WaveBufs w, uint32_t round, const uint4 *reservoir,
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wfinal_step(Scene sc, WaveBufs w, uint32_t round, const uint4 *reservoir,
                                                   float4 *accum) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, round, lds);
@@ -950,7 +953,7 @@ __global__ __launch_bounds__(WB) void wmcpt_start(Scene sc, WaveBufs w) {
 }
 
 template <int FIRST>
-__global__ __launch_bounds__(WB) void wmcpt_step(Scene sc, WaveBufs w, uint32_t round, float4 *accum) {
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wmcpt_step(Scene sc, WaveBufs w, uint32_t round, float4 *accum) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, round, lds);
     float4 *state = w.state;
