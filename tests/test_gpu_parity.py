@@ -174,6 +174,30 @@ def test_c3_many_lights_bit_exact(scene3, oracle_mod, native):
     np.testing.assert_array_equal(m.read_image().view(np.uint32), fm.accum.view(np.uint32))
 
 
+@pytest.mark.parametrize("W,H,rb,re_", [(1, 1, 0, 0), (37, 23, 0, 0), (8, 1, 0, 0), (130, 70, 13, 61),
+                                        (600, 450, 0, 0)])
+def test_odd_sizes_and_bands_bit_exact(scene1, oracle_mod, W, H, rb, re_):
+    """Edge shapes: 1x1, sizes that are not tile multiples (padded 8x8 tiles, partial segments),
+    a band starting and ending mid-tile, and the reference's 600x450 canvas; ReSTIR (2 frames)
+    and MCPT through the default wavefront path, bit for bit against the oracle."""
+    rows = (rb, re_ or H)
+    r = make_renderer(scene1, W, H, row_begin=rb, row_end=re_)
+    fr = oracle_frame(oracle_mod, scene1, W, H)
+    for f in (1, 2):
+        r.Update()
+        r.Render()
+        fr.set_frame_index(f)
+        fr.run(oracle_mod.PASS_RESTIR, rect=(0, rows[0], W, rows[1]))
+    np.testing.assert_array_equal(r.read_image().view(np.uint32),
+                                  fr.accum[rows[0]:rows[1]].view(np.uint32))
+    m = make_renderer(scene1, W, H, pipeline="mcpt", row_begin=rb, row_end=re_)
+    fm = oracle_frame(oracle_mod, scene1, W, H)
+    m.Update()
+    m.Render()
+    fm.run(oracle_mod.PASS_MCPT, rect=(0, rows[0], W, rows[1]))
+    np.testing.assert_array_equal(m.read_image().view(np.uint32), fm.accum[rows[0]:rows[1]].view(np.uint32))
+
+
 def test_restir_pipeline_4_frames(scene1, oracle_mod):
     """Config C1 shape: 256x256, FrameIndex 1..4 accumulated through the Renderer surface."""
     W = H = 256
