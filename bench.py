@@ -2,15 +2,19 @@
 """Benchmark: Msamples/s of the reference's per-pixel path on MI355X.
 
 Workload (BASELINE.json configs):
-  * restir (default): Renderer_TEST's live pipeline -- PT_01 G-buffer -> PT_1 initial
-    RIS candidates -> PT_4 final shading -- 1920x1080, 1 spp per frame, DUMMY_SCENE_1
-    (Cornell-style room, 22 294 triangles, 3 lights).  Temporal/spatial reuse are not
-    in the reference code and are not run here.
-  * mcpt: TEST_MCPT brute-force path tracer, same frame (configs[1]).
+  * reuse (default): configs[2], the metric's "ReSTIR DI (temporal + spatial reuse)" --
+    PT_01 G-buffer -> PT_1 initial RIS -> temporal reuse -> spatial reuse -> PT_4 final
+    shading, 1920x1080, 1 spp per frame, on C3 (the build-defined 32-rect-light interior,
+    scenes/c3_interior_32.json).  The reuse passes are build-defined.
+  * restir: Renderer_TEST's live pipeline (PT_01 -> PT_1 -> PT_4, no reuse), 1080p.
+  * mcpt: TEST_MCPT brute-force path tracer (configs[1]).
+  restir / mcpt default to DUMMY_SCENE_1 (Cornell-style room, 22 294 triangles, 3 lights).
 A step = one frame (all passes) over the whole band; inputs (scene, uniform) are resident
 in HBM before the timed region.  Multi-GPU (torchrun): weak scaling, rank r renders rows
-[r*H, (r+1)*H) of a W x (H*N) frame with global pixel coordinates (no collective on the
-data path; only the timing barrier and a max-reduce of the elapsed time).
+[r*H, (r+1)*H) of a W x (H*N) frame with global pixel coordinates.  restir / mcpt have no
+collective on the data path; reuse swaps reuse_radius halo rows (G-buffer + reservoirs)
+with the neighbouring bands every frame over RCCL (pathtracerdemo_amd/bands.py).  Timing:
+barrier + max-reduce of the elapsed time.
 """
 from __future__ import annotations
 
@@ -29,7 +33,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.
 # algorithmic bytes: 32 per slab test, 36 per triangle test, 48 per
 # instance transform, 48 per hit reconstruction; per-pixel pass IO below.
 B_AABB, B_TRI, B_INST, B_HIT = 32, 36, 48, 48
-PASS_IO = {"gbuffer": 16, "init": 16 + 128, "final": 16 + 128 + 16 + 16, "mcpt": 16 + 16}
+PASS_IO = {"gbuffer": 16, "init": 16 + 128, "final": 16 + 128 + 16 + 16, "mcpt": 16 + 16,
+           # temporal: G-buffer, PT_1 reservoir, history in; reservoir out.  spatial: G-buffer +
+           # reservoir of the pixel and its 3 neighbours in, PT_4's reservoir out
+           "temporal": 16 + 128 + 128 + 128, "spatial": 4 * (16 + 128) + 128}
+PASSES = {"restir": ["gbuffer", "init", "final"], "mcpt": ["mcpt"],
+          "reuse": ["gbuffer", "init", "temporal", "spatial", "final"]}
+DEFAULT_SCENE = {"reuse": "c3_interior_32", "restir": "dummy_scene_1", "mcpt": "dummy_scene_1"}
 
 
 def ray_bytes(c: dict) -> int:
@@ -41,10 +51,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["restir", "mcpt"], default="restir")
+    ap.add_argument("--workload", choices=["reuse", "restir", "mcpt"], default="reuse")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--scene", default="dummy_scene_1")
+    ap.add_argument("--scene", default=None, help="default: c3_interior_32 (reuse), dummy_scene_1 (others)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", choices=["wave", "tiled", "persistent", "simple"], default="wave",
@@ -54,6 +64,7 @@ def parse():
 
 def main():
     args = parse()
+    args.scene = args.scene or DEFAULT_SCENE[args.workload]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -76,17 +87,28 @@ def main():
     r = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
                  variant=args.variant)
     r.Initialize(cs)
+    band_drv = None
+    if pipeline == "reuse" and world > 1:
+        from pathtracerdemo_amd.bands import ReuseBand
+        band_drv = ReuseBand(r, rank, world, device=f"cuda:{local_rank}")
+
+    def frame(rr, drv):
+        rr.Update()
+        if drv is None:
+            rr.Render()
+        else:
+            drv.render_frame()
 
     # work census of the exact frame (counting build, untimed): algorithmic bytes
     rc = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
                   count_work=True, variant=args.variant)
     rc.Initialize(cs)
     rc.Update()
-    passes = ["gbuffer", "init", "final"] if pipeline == "restir" else ["mcpt"]
+    passes = PASSES[pipeline]
     counts = {}
     from pathtracerdemo_amd import _native as N
     pid = {"gbuffer": N.PTX_PASS_GBUFFER, "init": N.PTX_PASS_INIT, "final": N.PTX_PASS_FINAL,
-           "mcpt": N.PTX_PASS_MCPT}
+           "mcpt": N.PTX_PASS_MCPT, "temporal": N.PTX_PASS_TEMPORAL, "spatial": N.PTX_PASS_SPATIAL}
     for p in passes:
         rc.reset_stats()
         rc.run_pass(pid[p])
@@ -101,16 +123,14 @@ def main():
             dist.barrier()
 
     for _ in range(args.warmup):
-        r.Update()
-        r.Render()
+        frame(r, band_drv)
     r.synchronize()
     r.reset_stats()
     barrier()
     r.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        r.Update()
-        r.Render()
+        frame(r, band_drv)
     r.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -134,15 +154,17 @@ def main():
         rk = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
                       variant=args.variant, time_launches=True, single_stream=True)
         rk.Initialize(cs)
+        drv_k = None
+        if band_drv is not None:
+            from pathtracerdemo_amd.bands import ReuseBand
+            drv_k = ReuseBand(rk, rank, world, device=f"cuda:{local_rank}")
         for _ in range(max(1, args.warmup)):
-            rk.Update()
-            rk.Render()
+            frame(rk, drv_k)
         rk.synchronize()
         rk.reset_stats()
         barrier()
         for _ in range(args.steps):
-            rk.Update()
-            rk.Render()
+            frame(rk, drv_k)
         rk.synchronize()
         barrier()
         st_k = rk.stats()
@@ -158,6 +180,9 @@ def main():
     if st["kernel_launches"][N.PTX_STAT_FRAME]:
         # the wavefront ReSTIR frame overlaps its passes on two streams: timed as a whole
         kms = {"frame": st["kernel_ms_total"][N.PTX_STAT_FRAME] / st["kernel_launches"][N.PTX_STAT_FRAME]}
+    elif st["kernel_launches"][N.PTX_STAT_PASS_GROUP]:
+        # a reuse band: two pass groups around the halo exchange, per frame
+        kms = {"pass_groups": st["kernel_ms_total"][N.PTX_STAT_PASS_GROUP] / args.steps}
     else:
         kms = {p: st["kernel_ms_total"][pid[p]] / max(1, st["kernel_launches"][pid[p]]) for p in passes}
     # frame-level figure of SURVEY.md §8d: algorithmic bytes of the frame / kernel time
@@ -202,8 +227,11 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"{args.scene} {pipeline} {W}x{Hb} per GPU, 1 spp/frame",
-                   "pipeline": "PT_01 gbuffer -> PT_1 init -> PT_4 final" if pipeline == "restir"
-                   else "TEST_MCPT brute force", "frame": f"{W}x{H}", "band_rows_per_gpu": Hb,
+                   "pipeline": {"restir": "PT_01 gbuffer -> PT_1 init -> PT_4 final",
+                                "reuse": "PT_01 gbuffer -> PT_1 init -> temporal -> spatial (3 neighbours, "
+                                         "radius 30, pairwise MIS) -> PT_4 final",
+                                "mcpt": "TEST_MCPT brute force"}[pipeline],
+                   "frame": f"{W}x{H}", "band_rows_per_gpu": Hb,
                    "parallelism": f"row-bands x{world}"},
         "kernel_ms": {p: round(v, 4) for p, v in kms.items()},
         "nonfinite_px": nonfinite,
@@ -222,7 +250,8 @@ def main():
 
 
 def cpu_baseline(cs, W, H, pipeline, threads):
-    """The C oracle (a port of the WGSL) on the host cores: one full frame, timed."""
+    """The C oracle (a port of the WGSL + the reuse passes) on the host cores, timed over
+    whole frames: one frame (restir / mcpt), two for reuse (the second with its history)."""
     from oracle import oracle as O
     from pathtracerdemo_amd.scene.camera import Camera
     threads = max(1, min(threads, os.cpu_count() or 1))
@@ -230,11 +259,17 @@ def cpu_baseline(cs, W, H, pipeline, threads):
     cam.set_location(0, 0, 6)
     u = cs.uniform(W, H, cam.view_projection_inverse(), cam.location, 1)
     fr = O.Frame(u, cs.scene, cs.geometry, cs.accel)
+    nf = 2 if pipeline == "reuse" else 1
     t0 = time.perf_counter()
-    fr.run(O.PASS_RESTIR if pipeline == "restir" else O.PASS_MCPT, threads=threads)
+    for f in range(1, nf + 1):
+        fr.set_frame_index(f)
+        if pipeline == "reuse":
+            fr.run_reuse_frame(threads=threads)
+        else:
+            fr.run(O.PASS_RESTIR if pipeline == "restir" else O.PASS_MCPT, threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": round(W * H / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"one full {W}x{H} frame ({pipeline}, FrameIndex 1), C oracle, {threads} pthreads",
+    return {"value": round(nf * W * H / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{nf} full {W}x{H} frame(s) ({pipeline}, FrameIndex 1..{nf}), C oracle, {threads} pthreads",
             "seconds": round(dt, 2)}
 
 

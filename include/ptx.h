@@ -14,6 +14,9 @@
  *   ptx_reset_accumulation <- texture re-creation on Initialize             GC/Renderer_TEST.ts:445-476
  *   ptx_destroy          <- DestroyGPUResources                             GC/Renderer_TEST.ts:462-476
  *   ptx_run_pass         <- ComputePass.Dispatch of one pass                GC/ComputePass.ts:66-78
+ *   ptx_run_passes       <- a run of ComputePass.Dispatch calls (Render, :208-261)
+ *   PTX_PASS_TEMPORAL / PTX_PASS_SPATIAL and ptx_halo_* <- the reuse passes the reference
+ *                           only specifies (docs/theory/ReSTIR_Pipeline.md:259-462; no code)
  *
  * Conventions: every function returns 0 (PTX_OK) or a negative PTX_E* code and never
  * throws; ptx_last_error() holds the handle's last message.  Input arrays are borrowed
@@ -32,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PTX_ABI_VERSION 1
+#define PTX_ABI_VERSION 2
 
 #define PTX_OK 0
 #define PTX_E_INVALID (-1)  /* bad argument / state                  */
@@ -47,6 +50,9 @@ extern "C" {
 /* pipelines */
 #define PTX_PIPELINE_RESTIR 0  /* PT_01 G-buffer -> PT_1 Init -> PT_4 Final (Renderer_TEST) */
 #define PTX_PIPELINE_MCPT 1    /* TEST_MCPT brute force (legacy Renderer)                 */
+#define PTX_PIPELINE_RESTIR_REUSE 2 /* G-buffer -> Init -> temporal -> spatial -> Final: the
+                                       build-defined reuse passes; wavefront
+                                       kernels only                                        */
 
 /* passes for ptx_run_pass */
 #define PTX_PASS_GBUFFER 0
@@ -54,18 +60,23 @@ extern "C" {
 #define PTX_PASS_FINAL 2
 #define PTX_PASS_MCPT 3
 #define PTX_PASS_TRACE 4  /* ptx_trace / ptx_trace_device (stats slot only) */
+#define PTX_PASS_TEMPORAL 8  /* reuse: PT_1 reservoir <- previous frame's output (same pixel) */
+#define PTX_PASS_SPATIAL 9   /* reuse: pairwise-MIS resampling over neighbours -> Final's input */
 /* stats-only slots: every launch of the wavefront pipeline's kernels, by kind */
 #define PTX_STAT_WAVE_TRACE 5  /* trace_queue launches (ray-segment traversal)      */
 #define PTX_STAT_WAVE_LOGIC 6  /* start/step launches (shading, RIS, queue appends) */
 #define PTX_STAT_FRAME 7       /* whole ptx_render frames of the wavefront ReSTIR path, which
                                   overlaps its passes: slots 0..2 then only get the per-part
                                   G-buffer launches, with PTX_FLAG_TIME_LAUNCHES          */
+#define PTX_STAT_PASS_GROUP 10 /* ptx_run_passes calls of the wavefront kernels          */
 
 /* buffers for ptx_read_buffer / ptx_write_buffer / ptx_device_pointer */
 #define PTX_BUF_GBUFFER 0    /* band_h * W * 4 u32   */
 #define PTX_BUF_RESERVOIR 1  /* band_h * W * 32 u32  */
 #define PTX_BUF_ACCUM 2      /* band_h * W * 4 f32 (Scene texture: accumulated radiance) */
 #define PTX_BUF_COUNTERS 3   /* 32 u64: work counters [0..4] (PTX_FLAG_COUNT builds), diagnostics [8..) */
+#define PTX_BUF_RESERVOIR_HIST 4 /* band_h * W * 32 u32: spatial output = Final's input and the
+                                    next frame's temporal history (reuse pipeline)           */
 
 #define PTX_FLAG_COUNT_WORK 1u     /* count rays / AABB / triangle tests on device (slower)   */
 #define PTX_FLAG_SIMPLE_KERNELS 2u   /* A/B: one thread per pixel, no ray exchange            */
@@ -84,13 +95,17 @@ typedef struct ptx_config {
     int32_t device;               /* HIP device ordinal; -1 = current device        */
     uint32_t pipeline;            /* PTX_PIPELINE_*                                  */
     uint32_t flags;               /* PTX_FLAG_*                                      */
-    uint32_t reserved[5];
+    /* reuse pipeline (0 = default): spatial neighbours lie in [-radius, radius]^2 (30),
+     * `neighbors` per pixel (3, at most 16), history confidence capped at temporal_cap (20).
+     * A band handle keeps min(radius, rows available) halo rows above and below its band. */
+    uint32_t reuse_radius, reuse_neighbors, temporal_cap;
+    uint32_t reserved[2];
 } ptx_config;
 
 typedef struct ptx_stats {
     uint64_t frames;              /* ptx_render calls since the last stats reset    */
-    double kernel_ms_total[8];    /* summed device time per PTX_PASS_* (HIP events) */
-    uint64_t kernel_launches[8];  /* launches per PTX_PASS_*                        */
+    double kernel_ms_total[16];   /* summed device time per PTX_PASS_* / PTX_STAT_* slot */
+    uint64_t kernel_launches[16]; /* launches per slot                              */
     uint32_t triangles, bvh_nodes, instances, max_bvh_depth;
     uint64_t device_bytes;        /* device memory held by the handle               */
 } ptx_stats;
@@ -105,7 +120,22 @@ int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]);
 /* Run the configured pipeline for the current frame; if rgba_out != NULL copy the band's
  * accumulated RGBA f32 image (band_h * W * 4) into it (blocking). Otherwise asynchronous. */
 int ptx_render(ptx_handle *h, float *rgba_out);
+/* (reuse pipeline: whole-image handles only -- a band needs the halo exchange between its
+ *  passes, see ptx_halo_*) */
 int ptx_run_pass(ptx_handle *h, int pass);
+/* Passes in order as one launch sequence per segment group (overlapped on two streams).
+ * Every pass must read only its own pixel's results of the earlier passes, except that
+ * PTX_PASS_SPATIAL may come first (it reads neighbours of the previous passes' output). */
+int ptx_run_passes(ptx_handle *h, const int *passes, int n);
+/* Spatial-reuse halo of a band handle.  Between TEMPORAL and SPATIAL a band needs the
+ * G-buffer and reservoir rows of its neighbours: rows_top rows from the band above (its
+ * last rows), rows_bottom from the band below.  A message is rows x W x bytes_per_row
+ * (G-buffer rows, then reservoir rows).  pack copies THIS band's first rows_top / last
+ * rows_bottom rows (what the neighbours need) into device buffers; unpack copies received
+ * messages into the halo rows.  Both are async on the handle's stream. */
+int ptx_halo_rows(ptx_handle *h, uint32_t *rows_top, uint32_t *rows_bottom, size_t *bytes_per_row);
+int ptx_halo_pack(ptx_handle *h, void *dev_top, void *dev_bottom);
+int ptx_halo_unpack(ptx_handle *h, const void *dev_top, const void *dev_bottom);
 int ptx_reset_accumulation(ptx_handle *h);
 int ptx_synchronize(ptx_handle *h);
 int ptx_get_stats(ptx_handle *h, ptx_stats *out);

@@ -15,6 +15,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 PASS_GBUFFER, PASS_INIT, PASS_FINAL, PASS_MCPT, PASS_RESTIR = 0, 1, 2, 3, 4
+PASS_TEMPORAL, PASS_SPATIAL = 5, 6
+# build-defined reuse defaults (same as include/ptx.h)
+REUSE_RADIUS, REUSE_NEIGHBORS, TEMPORAL_CAP = 30, 3, 20
 
 
 class Counters(ctypes.Structure):
@@ -23,6 +26,11 @@ class Counters(ctypes.Structure):
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class ReuseParams(ctypes.Structure):
+    _fields_ = [("radius", ctypes.c_uint32), ("neighbors", ctypes.c_uint32), ("temporal_cap", ctypes.c_uint32),
+                ("hist_valid", ctypes.c_uint32)]
 
 
 class Inputs(ctypes.Structure):
@@ -48,6 +56,10 @@ def lib():
         _lib.pto_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Inputs), ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, P, P, P, ctypes.POINTER(Counters)]
         _lib.pto_run.restype = ctypes.c_int
+        _lib.pto_run_reuse.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Inputs), ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P,
+                                       ctypes.POINTER(ReuseParams), ctypes.POINTER(Counters)]
+        _lib.pto_run_reuse.restype = ctypes.c_int
         _lib.pto_pcg.argtypes = [ctypes.c_uint32]
         _lib.pto_pcg.restype = ctypes.c_uint32
         _lib.pto_random.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
@@ -83,6 +95,9 @@ class Frame:
         self.gbuffer = np.zeros((self.H, self.W, 4), dtype=np.uint32)
         self.reservoir = np.zeros((self.H, self.W, 32), dtype=np.uint32)
         self.accum = np.zeros((self.H, self.W, 4), dtype=np.float32)
+        self.res_hist = np.zeros((self.H, self.W, 32), dtype=np.uint32)  # spatial output / history
+        self.hist_valid = False
+        self.reuse = (REUSE_RADIUS, REUSE_NEIGHBORS, TEMPORAL_CAP)
         self.counters = {}
 
     def set_frame_index(self, f: int):
@@ -99,18 +114,42 @@ class Frame:
         self.counters["trace"] = cnt.as_dict()
         return (hits, self.counters["trace"]) if return_counters else hits
 
-    def run(self, pass_id: int, threads: int = 0, rect=None) -> dict:
+    def run(self, pass_id: int, threads: int = 0, rect=None, reservoir: np.ndarray | None = None) -> dict:
+        """One pass over `rect` (x0, y0, x1, y1).  PASS_TEMPORAL updates `reservoir` from
+        `res_hist`; PASS_SPATIAL reads `reservoir` and writes `res_hist`; PASS_FINAL reads
+        `reservoir` (pass `reservoir=self.res_hist` for the reuse pipeline)."""
         threads = threads or os.cpu_count() or 1
         x0, y0, x1, y1 = rect if rect is not None else (0, 0, self.W, self.H)
         inp = Inputs(self.uniform.ctypes.data, self.scene.ctypes.data, self.geometry.ctypes.data,
                      self.accel.ctypes.data)
         cnt = Counters()
+        if pass_id in (PASS_TEMPORAL, PASS_SPATIAL):
+            r, m, cap = self.reuse
+            prm = ReuseParams(r, m, cap, 1 if self.hist_valid else 0)
+            rc = lib().pto_run_reuse(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
+                                     _ptr(self.reservoir), _ptr(self.res_hist), ctypes.byref(prm),
+                                     ctypes.byref(cnt))
+            if rc != 0:
+                raise RuntimeError(f"oracle pass {pass_id} failed ({rc})")
+            self.counters[pass_id] = cnt.as_dict()
+            return self.counters[pass_id]
+        res = self.reservoir if reservoir is None else np.ascontiguousarray(reservoir)
+        assert res.dtype == np.uint32 and res.shape == self.reservoir.shape
         rc = lib().pto_run(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
-                           _ptr(self.reservoir), _ptr(self.accum), ctypes.byref(cnt))
+                           _ptr(res), _ptr(self.accum), ctypes.byref(cnt))
         if rc != 0:
             raise RuntimeError(f"oracle pass {pass_id} failed ({rc})")
         self.counters[pass_id] = cnt.as_dict()
         return self.counters[pass_id]
+
+    def run_reuse_frame(self, threads: int = 0, rect=None) -> None:
+        """One frame of the reuse pipeline: G-buffer -> PT_1 -> temporal -> spatial -> PT_4.
+        The caller keeps the camera fixed between frames (history stays valid) or clears
+        `hist_valid` (ptx_set_frame does the same on a camera change)."""
+        for p in (PASS_GBUFFER, PASS_INIT, PASS_TEMPORAL, PASS_SPATIAL):
+            self.run(p, threads, rect)
+        self.run(PASS_FINAL, threads, rect, reservoir=self.res_hist)
+        self.hist_valid = True
 
 
 def pcg(seed: int) -> int:

@@ -983,6 +983,269 @@ void pto_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *re
         }
 }
 
+/* ================================================================== reuse passes
+ * Temporal and spatial reuse are NOT in the reference code: only specified in
+ * docs/theory/ReSTIR_Pipeline.md:259-462 (pass 2 temporal, pass 3 spatial: generalized
+ * balance heuristic with confidences, m_i = c_i p_i / sum_j c_j p_j, w_i = m_i p_hat W_i)
+ * and docs/theory/memo.md:166-231 (shifts with a Jacobian).  The build-defined rules
+ *  are restated here so that the HIP kernels can be checked bit for bit:
+ *
+ *  - sample = the reservoir's (rSeed, XL, length); PT_4 consumes exactly that, replaying
+ *    the BSDF draws from rSeed at ITS OWN pixel (PT_4:1357-1384).  The shift between pixels
+ *    is therefore random replay of rSeed from the target pixel's primary hit, with the
+ *    light endpoint XL kept (a reconnection on the light).
+ *  - target p_hat_d(x) = Luminance(PathContribution) of the sample replayed in domain d
+ *    (pixel d's camera point and G-buffer hit), PT_4's formulas: the integrand PT_4 weights.
+ *  - Jacobian of the shift x -> y: q(x) / q(y), q = prod_i pdf_bsdf(replayed vertex i) / g,
+ *    g = |n_light . l| / r^2 for a rect light (solid angle of the fixed light point), else 1.
+ *    q also divides by beta, PT_1's roulette factor on the path (rr_step): PT_1's
+ *    contribution weights integrate beta * f, so a sample moved between pixels is
+ *    re-weighted by beta_target / beta_source and reuse keeps PT_1 + PT_4's expectation.
+ *  - confidences (word 29 of a reused reservoir) depend on geometry and history only,
+ *    never on sample values (a sample-dependent MIS weight biases the estimate): a PT_1
+ *    reservoir counts 1; neighbours count iff inside the image with a G-buffer hit.
+ *  - temporal: same pixel of the previous frame's spatial output (static camera: same
+ *    domain, identity shift), history confidence capped at `cap`.
+ *  - spatial: M neighbours in a (2R+1)^2 square, pairwise MIS with confidences.
+ *  - every reservoir written by a reuse pass stores p_hat (word 24) and q (word 25) of its
+ *    sample in its own domain; RNG streams are salted per pass. */
+#define SALT_TEMPORAL 0x54454D50u
+#define SALT_SPATIAL 0x53504154u
+
+typedef struct eval_out { int valid; float phat, q; } eval_out;
+
+static inline uint32_t reuse_seed(const ctx *c, uint32_t x, uint32_t y, uint32_t salt) {
+    return pto_pcg(init_seed(c, x, y) ^ salt);
+}
+static inline int wrs_update(float *w_sum, float w, uint32_t *seed) { /* UpdateReservoir, PT_1:1298-1320 */
+    *w_sum += w;
+    return pto_random(seed) < w / *w_sum;
+}
+
+/* PT_1's throughput recursion and Russian roulette (PT_1:1427-1442) along a replayed
+ * vertex: the roulette multiplies p by p_survive even when p_survive > 1, so PT_1's
+ * weights carry beta = prod min(1, p_survive) / p_survive; the shift carries it along. */
+static void rr_step(const surface *X, v3 V, v3 L, float pdf, v3 *f, float *p, float *beta, int *ok) {
+    *f = vmul(*f, vscale(bsdf(X, V, L), fabsf(vdot(X->nrm, L))));
+    *p *= pdf;
+    const float ps = luminance(*f) / *p;
+    if (!(ps > 0.0f)) *ok = 0; /* PT_1 ends such a path: no sample of this shape here */
+    *p *= ps;
+    if (ps > 1.0f) *beta /= ps;
+}
+
+/* The reservoir sample `res` replayed in the domain of pixel (x, y) with G-buffer hit x1:
+ * RegeneratePath + PathContribution of PT_4:1306-1384 plus the shift's pdf product. */
+static eval_out eval_sample(const ctx *c, uint32_t x, uint32_t y, compact x1, const uint32_t *res) {
+    eval_out o = {0, 0.0f, 0.0f};
+    const uint32_t length = res[23];
+    if (!x1.valid || res[29] == 0u || length < 2u) return o;
+    light_sample XL;
+    XL.dir = V3(f32_of(res[4]), f32_of(res[5]), f32_of(res[6]));
+    XL.type = res[7];
+    XL.pos = V3(f32_of(res[8]), f32_of(res[9]), f32_of(res[10]));
+    XL.id = (int32_t)res[11];
+    XL.Le = V3(f32_of(res[12]), f32_of(res[13]), f32_of(res[14]));
+    XL.pdf = f32_of(res[15]);
+    surface S[8];
+    memset(S, 0, sizeof S);
+    S[0].pos = get_x0(c, x, y);
+    S[1] = get_surface(c, x1);
+    float prod = 1.0f, beta = 1.0f, rr_p = 1.0f;
+    v3 rr_f = V3(1.0f, 1.0f, 1.0f);
+    int rr_ok = 1;
+    for (uint32_t i = 1; i + 1u < length; ++i) {
+        v3 V = vnormalize(vsub(S[i - 1].pos, S[i].pos));
+        uint32_t seed = res[i - 1u], lobe;
+        v3 dir = sample_bsdf(&seed, &S[i], V, &lobe);
+        const float pdf = pdf_bsdf(&S[i], V, dir);
+        prod *= pdf;
+        rr_step(&S[i], V, dir, pdf, &rr_f, &rr_p, &beta, &rr_ok);
+        ray r = {S[i].pos, dir};
+        hit h = trace_ray(c, r);
+        if (!h.valid) return o; /* the replayed path escapes: no such path in this domain */
+        S[i + 1] = get_surface(c, h.s);
+    }
+    v3 f = V3(1.0f, 1.0f, 1.0f);
+    for (uint32_t i = 1; i + 1u < length; ++i) {
+        v3 V = vnormalize(vsub(S[i - 1].pos, S[i].pos));
+        v3 L = vnormalize(vsub(S[i + 1].pos, S[i].pos));
+        f = vmul(f, vscale(bsdf(&S[i], L, V), fabsf(vdot(S[i].nrm, L))));
+    }
+    const surface *P = &S[length - 2u], *Xc = &S[length - 1u];
+    v3 V = vnormalize(vsub(P->pos, Xc->pos));
+    v3 L = direction_to_light(Xc, &XL);
+    if (XL.type == LIGHT_ENV) /* the escape direction passed PT_1's roulette too */
+        rr_step(Xc, V, L, pdf_bsdf(Xc, V, L), &rr_f, &rr_p, &beta, &rr_ok);
+    f = vmul(f, vscale(bsdf(Xc, L, V), fabsf(vdot(Xc->nrm, L))));
+    float g = 1.0f;
+    if (XL.type == LIGHT_RECT) {
+        v3 r = vsub(XL.pos, Xc->pos);
+        v3 Ld = vnormalize(r);
+        g = fabsf(vdot(get_light(c, (uint32_t)XL.id).dir, Ld)) / vdot(r, r);
+    }
+    f = vmul(f, vscale(l_emit(c, &XL, Xc), visibility(c, Xc->pos, XL.pos)));
+    const float q = prod / (g * beta);
+    o.valid = rr_ok && q > 0.0f && q <= 3.402823466e38f;
+    o.phat = o.valid ? luminance(f) : 0.0f;
+    o.q = o.valid ? q : 0.0f;
+    return o;
+}
+
+static void write_reused(uint32_t *out, const uint32_t *src, float p_sel, float q_sel, float w_sum, uint32_t C) {
+    uint32_t tmp[24];
+    memcpy(tmp, src, sizeof tmp); /* src may alias out (temporal works in place) */
+    memset(out, 0, 4u * PTO_RESERVOIR_WORDS);
+    memcpy(out, tmp, sizeof tmp);
+    out[24] = u32_of(p_sel);
+    out[25] = u32_of(q_sel);
+    out[28] = u32_of(p_sel > 0.0f ? w_sum / p_sel : 0.0f);
+    out[29] = C;
+}
+
+/* Temporal reuse (ReSTIR_Pipeline.md:259-340) of pixel (x, y): canonical = this frame's
+ * PT_1 reservoir, history = the previous frame's spatial output at the same pixel. */
+static void temporal_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t *cur, const uint32_t *hist,
+                           const pto_reuse_params *prm, uint32_t x, uint32_t y) {
+    const uint32_t W = c->U[U_W];
+    compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
+    if (!x1.valid) return; /* PT_1 wrote the zero reservoir; PT_4 never reads it */
+    uint32_t seed = reuse_seed(c, x, y, SALT_TEMPORAL);
+    eval_out ec = eval_sample(c, x, y, x1, cur);
+    const int canon_ok = ec.valid && ec.phat > 0.0f;
+    /* confidences depend on geometry and history only, never on the samples: a PT_1
+     * reservoir counts 1, the history min(C_hist, cap) */
+    const uint32_t Cp = prm->hist_valid ? (hist[29] < prm->temporal_cap ? hist[29] : prm->temporal_cap) : 0u;
+    const float cp = (float)Cp, tot = 1.0f + cp;
+    const float pp = f32_of(hist[24]), qp = f32_of(hist[25]);
+    const int hist_ok = Cp != 0u && hist[23] >= 2u && pp > 0.0f;
+    const float wc = canon_ok ? (1.0f / tot) * ec.phat * f32_of(cur[28]) : 0.0f;
+    const float wp = hist_ok ? (cp / tot) * pp * f32_of(hist[28]) : 0.0f;
+    float w_sum = 0.0f;
+    const uint32_t *src = cur;
+    float p_sel = ec.phat, q_sel = ec.q;
+    if (wrs_update(&w_sum, wc, &seed)) { src = cur; p_sel = ec.phat; q_sel = ec.q; }
+    if (wrs_update(&w_sum, wp, &seed)) { src = hist; p_sel = pp; q_sel = qp; }
+    write_reused(cur, src, p_sel, q_sel, w_sum, 1u + Cp);
+}
+
+/* Spatial neighbour k of (x, y): two draws, offsets in [-R, R]^2. Returns 1 if inside the
+ * image and not the pixel itself. */
+static int spatial_neighbor(uint32_t *seed, uint32_t R, uint32_t x, uint32_t y, uint32_t W, uint32_t H,
+                            uint32_t *nx, uint32_t *ny) {
+    const float side = (float)(2u * R + 1u);
+    uint32_t ix = (uint32_t)(pto_random(seed) * side), iy = (uint32_t)(pto_random(seed) * side);
+    if (ix > 2u * R) ix = 2u * R; /* Random() can return exactly 1.0 */
+    if (iy > 2u * R) iy = 2u * R;
+    const int64_t X = (int64_t)x + (int64_t)ix - (int64_t)R, Y = (int64_t)y + (int64_t)iy - (int64_t)R;
+    if (X < 0 || Y < 0 || X >= (int64_t)W || Y >= (int64_t)H || (ix == R && iy == R)) return 0;
+    *nx = (uint32_t)X;
+    *ny = (uint32_t)Y;
+    return 1;
+}
+
+/* Spatial reuse (ReSTIR_Pipeline.md:342-462) with pairwise MIS: for neighbour n and shift
+ * y = T(x_n), m_n(y) = c_n p_n->c(y) / (c_c p_c(y) + M c_n p_n->c(y)); the canonical sample
+ * gets m_c = (1/M) sum_n c_c p_c / (c_c p_c + M c_n p_n->c(x_c)). */
+static void spatial_pixel(const ctx *c, const uint32_t *gbuffer, const uint32_t *cur, uint32_t *out,
+                          const pto_reuse_params *prm, uint32_t x, uint32_t y) {
+    const uint32_t W = c->U[U_W], H = c->U[U_H];
+    const uint32_t p = y * W + x;
+    compact x1 = decode_compact(gbuffer + 4u * p);
+    uint32_t *o = out + PTO_RESERVOIR_WORDS * p;
+    if (!x1.valid) { memset(o, 0, 4u * PTO_RESERVOIR_WORDS); return; }
+    const uint32_t *rc = cur + PTO_RESERVOIR_WORDS * p;
+    uint32_t seed = reuse_seed(c, x, y, SALT_SPATIAL);
+    const uint32_t M = prm->neighbors;
+    uint32_t nb[16];
+    int present[16];
+    for (uint32_t k = 0; k < M; ++k) {
+        uint32_t nx = 0, ny = 0;
+        present[k] = spatial_neighbor(&seed, prm->radius, x, y, W, H, &nx, &ny);
+        nb[k] = ny * W + nx;
+        if (present[k]) present[k] = decode_compact(gbuffer + 4u * nb[k]).valid; /* geometry only */
+    }
+    const float Mf = (float)M, cc = (float)rc[29];
+    const float pc = f32_of(rc[24]), qc = f32_of(rc[25]), Wc = f32_of(rc[28]);
+    const int canon_ok = rc[29] != 0u && rc[23] >= 2u && pc > 0.0f;
+    float wn[16], pf[16], qf[16], sumQ = 0.0f;
+    uint32_t Csum = rc[29];
+    for (uint32_t k = 0; k < M; ++k) {
+        wn[k] = 0.0f; pf[k] = 0.0f; qf[k] = 0.0f;
+        float Q = 1.0f;
+        if (present[k]) {
+            const uint32_t *rn = cur + PTO_RESERVOIR_WORDS * nb[k];
+            const uint32_t nx = nb[k] % W, ny = nb[k] / W;
+            const float cn = (float)rn[29], pn = f32_of(rn[24]), qn = f32_of(rn[25]), Wn = f32_of(rn[28]);
+            Csum += rn[29];
+            if (rn[23] >= 2u && pn > 0.0f) { /* forward: the neighbour's sample in this pixel's domain */
+                eval_out F = eval_sample(c, x, y, x1, rn);
+                if (F.valid) {
+                    const float J = qn / F.q;
+                    const float pb = pn / J;
+                    const float den = cc * F.phat + Mf * cn * pb;
+                    const float m = den > 0.0f ? (cn * pb) / den : 0.0f;
+                    wn[k] = m * F.phat * Wn * J;
+                    pf[k] = F.phat;
+                    qf[k] = F.q;
+                }
+            }
+            if (canon_ok) { /* backward: this pixel's sample in the neighbour's domain */
+                eval_out B = eval_sample(c, nx, ny, decode_compact(gbuffer + 4u * nb[k]), rc);
+                if (B.valid) {
+                    const float pbc = B.phat * qc / B.q;
+                    const float den = cc * pc + Mf * cn * pbc;
+                    Q = den > 0.0f ? (cc * pc) / den : 1.0f;
+                }
+            }
+        }
+        sumQ += Q;
+    }
+    const float wc = canon_ok ? (sumQ / Mf) * pc * Wc : 0.0f;
+    float w_sum = 0.0f, p_sel = pc, q_sel = qc;
+    const uint32_t *src = rc;
+    if (wrs_update(&w_sum, wc, &seed)) { src = rc; p_sel = pc; q_sel = qc; }
+    for (uint32_t k = 0; k < M; ++k)
+        if (wrs_update(&w_sum, wn[k], &seed)) {
+            src = cur + PTO_RESERVOIR_WORDS * nb[k];
+            p_sel = pf[k];
+            q_sel = qf[k];
+        }
+    write_reused(o, src, p_sel, q_sel, w_sum, Csum);
+}
+
+/* Test helper: eval_sample of reservoir `res` in the domain of pixel (x, y). out = {valid, p_hat, q}. */
+void pto_eval_sample(const pto_inputs *in, const uint32_t *gbuffer, uint32_t x, uint32_t y, const uint32_t *res,
+                     float out[3]) {
+    ctx c;
+    ctx_init(&c, in, EPS_FINAL, NULL);
+    eval_out o = eval_sample(&c, x, y, decode_compact(gbuffer + 4u * (y * c.U[U_W] + x)), res);
+    out[0] = (float)o.valid;
+    out[1] = o.phat;
+    out[2] = o.q;
+}
+
+void pto_temporal(const pto_inputs *in, const uint32_t *gbuffer, uint32_t *res_cur, const uint32_t *res_hist,
+                  const pto_reuse_params *prm, int x0, int y0, int x1, int y1, pto_counters *cnt) {
+    ctx c;
+    ctx_init(&c, in, EPS_FINAL, cnt);
+    const uint32_t W = c.U[U_W];
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            const uint32_t p = (uint32_t)y * W + (uint32_t)x;
+            temporal_pixel(&c, gbuffer, res_cur + PTO_RESERVOIR_WORDS * p, res_hist + PTO_RESERVOIR_WORDS * p, prm,
+                           (uint32_t)x, (uint32_t)y);
+        }
+}
+
+void pto_spatial(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *res_cur, uint32_t *res_out,
+                 const pto_reuse_params *prm, int x0, int y0, int x1, int y1, pto_counters *cnt) {
+    ctx c;
+    ctx_init(&c, in, EPS_FINAL, cnt);
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) spatial_pixel(&c, gbuffer, res_cur, res_out, prm, (uint32_t)x, (uint32_t)y);
+}
+
 /* ================================================================== TEST_MCPT */
 /* GetLightColor, SH/TEST_MCPT.wgsl:1261-1309 */
 static v3 light_color(const ctx *c, uint32_t *seed, const surface *X, v3 V, uint32_t id) {
@@ -1114,8 +1377,9 @@ float pto_ray_triangle(const float o[3], const float d[3], const float p0[3], co
 typedef struct job {
     int pass, tid, nthreads, x0, y0, x1, y1;
     const pto_inputs *in;
-    uint32_t *gbuffer, *reservoir;
+    uint32_t *gbuffer, *reservoir, *res_hist;
     float *accum;
+    const pto_reuse_params *prm;
     pto_counters cnt;
 } job;
 
@@ -1127,6 +1391,8 @@ static void *worker(void *arg) {
         case 1: pto_init(j->in, j->gbuffer, j->x0, y, j->x1, y + 1, j->reservoir, &j->cnt); break;
         case 2: pto_final(j->in, j->gbuffer, j->reservoir, j->x0, y, j->x1, y + 1, j->accum, &j->cnt); break;
         case 3: pto_mcpt(j->in, j->x0, y, j->x1, y + 1, j->accum, &j->cnt); break;
+        case 5: pto_temporal(j->in, j->gbuffer, j->reservoir, j->res_hist, j->prm, j->x0, y, j->x1, y + 1, &j->cnt); break;
+        case 6: pto_spatial(j->in, j->gbuffer, j->reservoir, j->res_hist, j->prm, j->x0, y, j->x1, y + 1, &j->cnt); break;
         default: break;
         }
     }
@@ -1134,13 +1400,14 @@ static void *worker(void *arg) {
 }
 
 static int run_pass(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
-                    uint32_t *gbuffer, uint32_t *reservoir, float *accum, pto_counters *cnt) {
+                    uint32_t *gbuffer, uint32_t *reservoir, uint32_t *res_hist, const pto_reuse_params *prm,
+                    float *accum, pto_counters *cnt) {
     if (nthreads < 1) nthreads = 1;
     job *jobs = (job *)calloc((size_t)nthreads, sizeof(job));
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     if (!jobs || !th) { free(jobs); free(th); return -1; }
     for (int t = 0; t < nthreads; ++t) {
-        job j = {pass, t, nthreads, x0, y0, x1, y1, in, gbuffer, reservoir, accum, {0, 0, 0, 0, 0}};
+        job j = {pass, t, nthreads, x0, y0, x1, y1, in, gbuffer, reservoir, res_hist, accum, prm, {0, 0, 0, 0, 0}};
         jobs[t] = j;
         if (nthreads > 1) pthread_create(&th[t], NULL, worker, &jobs[t]);
     }
@@ -1163,10 +1430,18 @@ static int run_pass(int pass, int nthreads, const pto_inputs *in, int x0, int y0
 int pto_run(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, uint32_t *gbuffer,
             uint32_t *reservoir, float *accum, pto_counters *cnt) {
     if (pass == 4) {
-        int rc = run_pass(0, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, accum, cnt);
-        if (!rc) rc = run_pass(1, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, accum, cnt);
-        if (!rc) rc = run_pass(2, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, accum, cnt);
+        int rc = run_pass(0, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, NULL, NULL, accum, cnt);
+        if (!rc) rc = run_pass(1, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, NULL, NULL, accum, cnt);
+        if (!rc) rc = run_pass(2, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, NULL, NULL, accum, cnt);
         return rc;
     }
-    return run_pass(pass, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, accum, cnt);
+    if (pass < 0 || pass > 3) return -2;
+    return run_pass(pass, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, NULL, NULL, accum, cnt);
+}
+
+int pto_run_reuse(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                  const uint32_t *gbuffer, uint32_t *res_cur, uint32_t *res_hist, const pto_reuse_params *prm,
+                  pto_counters *cnt) {
+    if ((pass != 5 && pass != 6) || !prm || prm->neighbors > 16u) return -2;
+    return run_pass(pass, nthreads, in, x0, y0, x1, y1, (uint32_t *)gbuffer, res_cur, res_hist, prm, NULL, cnt);
 }

@@ -10,6 +10,8 @@
  *   pto_init     <- SH/PT_1_InitPass.wgsl:1361-1486
  *   pto_final    <- SH/PT_4_FinalShadingPass.wgsl:1392-1428
  *   pto_mcpt     <- SH/TEST_MCPT.wgsl:1315-1372
+ *   pto_temporal, pto_spatial <- build-defined reuse passes (no reference code; spec
+ *                   docs/theory/ReSTIR_Pipeline.md:259-462, docs/theory/memo.md:166-231)
  * over the reference's own device inputs (uniform block, SceneBuffer, GeometryBuffer,
  * AccelBuffer; Renderer_TEST.ts:165-206,267-420).  Implementation-defined WGSL details
  * are fixed as documented in DESIGN.md §Numerics (left-to-right dot/mat-vec sums, no
@@ -63,6 +65,30 @@ void pto_mcpt(const pto_inputs *in, int x0, int y0, int x1, int y1, float *accum
  * Rows [y0,y1) are interleaved over nthreads pthreads.  Returns 0 on success. */
 int pto_run(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, uint32_t *gbuffer,
             uint32_t *reservoir, float *accum, pto_counters *cnt);
+
+/* Reuse passes (build-defined; docs/theory/ReSTIR_Pipeline.md:259-462).
+ * Reservoirs are full-frame W*H*32 words; words 24/25 of a reused reservoir hold p_hat and
+ * the shift pdf product q of its sample in its own pixel's domain. */
+typedef struct pto_reuse_params {
+    uint32_t radius;        /* spatial neighbours in [-radius, radius]^2             */
+    uint32_t neighbors;     /* spatial neighbours per pixel (<= 16)                   */
+    uint32_t temporal_cap;  /* history confidence <= temporal_cap                    */
+    uint32_t hist_valid;    /* res_hist holds the previous frame (same camera/scene)  */
+} pto_reuse_params;
+/* temporal: res_cur (PT_1 output) updated in place from res_hist (previous spatial output) */
+void pto_temporal(const pto_inputs *in, const uint32_t *gbuffer, uint32_t *res_cur, const uint32_t *res_hist,
+                  const pto_reuse_params *prm, int x0, int y0, int x1, int y1, pto_counters *cnt);
+/* spatial: reads res_cur of the pixel and its neighbours, writes res_out (PT_4's input) */
+void pto_spatial(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *res_cur, uint32_t *res_out,
+                 const pto_reuse_params *prm, int x0, int y0, int x1, int y1, pto_counters *cnt);
+/* the shift of DESIGN.md §Reuse: reservoir sample `res` replayed in pixel (x, y)'s domain;
+ * out = {valid (0/1), p_hat, q} */
+void pto_eval_sample(const pto_inputs *in, const uint32_t *gbuffer, uint32_t x, uint32_t y, const uint32_t *res,
+                     float out[3]);
+/* threaded: pass 5 = temporal (res_cur in/out, res_hist in), 6 = spatial (res_cur in, res_hist out) */
+int pto_run_reuse(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                  const uint32_t *gbuffer, uint32_t *res_cur, uint32_t *res_hist, const pto_reuse_params *prm,
+                  pto_counters *cnt);
 
 /* Closest-hit queries, same record formats as ptx_trace (include/ptx.h):
  * rays n x 8 f32 {o, d.x | d.y, d.z, -, -}; hits n x 8 {t, flags|inst|mat, prim, bu, bv, pos}.

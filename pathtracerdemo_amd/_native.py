@@ -13,10 +13,14 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTX_LIB_PATH") or os.path.join(PKG_DIR, "libptx.so")
 
 PTX_OK = 0
-PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT = 0, 1
+PTX_ABI_VERSION = 2
+PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT, PTX_PIPELINE_RESTIR_REUSE = 0, 1, 2
+PIPELINES = {"restir": PTX_PIPELINE_RESTIR, "mcpt": PTX_PIPELINE_MCPT, "reuse": PTX_PIPELINE_RESTIR_REUSE}
 PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT, PTX_PASS_TRACE = 0, 1, 2, 3, 4
+PTX_PASS_TEMPORAL, PTX_PASS_SPATIAL = 8, 9
 PTX_STAT_WAVE_TRACE, PTX_STAT_WAVE_LOGIC, PTX_STAT_FRAME = 5, 6, 7  # stats-only slots (include/ptx.h)
-PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS = 0, 1, 2, 3
+PTX_STAT_PASS_GROUP = 10
+PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS, PTX_BUF_RESERVOIR_HIST = 0, 1, 2, 3, 4
 PTX_FLAG_COUNT_WORK = 1
 PTX_FLAG_SIMPLE_KERNELS = 2
 PTX_FLAG_PERSISTENT_LANES = 4
@@ -30,18 +34,20 @@ VARIANT_FLAGS = {"wave": 0, "tiled": PTX_FLAG_TILED_EXCHANGE, "persistent": PTX_
 EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame", "ptx_render", "ptx_run_pass",
             "ptx_reset_accumulation", "ptx_synchronize", "ptx_get_stats", "ptx_reset_stats", "ptx_read_buffer",
             "ptx_write_buffer", "ptx_device_pointer", "ptx_set_stream", "ptx_destroy", "ptx_last_error",
-            "ptx_trace", "ptx_trace_device"]
+            "ptx_trace", "ptx_trace_device", "ptx_run_passes", "ptx_halo_rows", "ptx_halo_pack",
+            "ptx_halo_unpack"]
 
 
 class PtxConfig(ctypes.Structure):
     _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("row_begin", ctypes.c_uint32),
                 ("row_end", ctypes.c_uint32), ("device", ctypes.c_int32), ("pipeline", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 5)]
+                ("flags", ctypes.c_uint32), ("reuse_radius", ctypes.c_uint32), ("reuse_neighbors", ctypes.c_uint32),
+                ("temporal_cap", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 2)]
 
 
 class PtxStats(ctypes.Structure):
-    _fields_ = [("frames", ctypes.c_uint64), ("kernel_ms_total", ctypes.c_double * 8),
-                ("kernel_launches", ctypes.c_uint64 * 8), ("triangles", ctypes.c_uint32),
+    _fields_ = [("frames", ctypes.c_uint64), ("kernel_ms_total", ctypes.c_double * 16),
+                ("kernel_launches", ctypes.c_uint64 * 16), ("triangles", ctypes.c_uint32),
                 ("bvh_nodes", ctypes.c_uint32), ("instances", ctypes.c_uint32), ("max_bvh_depth", ctypes.c_uint32),
                 ("device_bytes", ctypes.c_uint64)]
 
@@ -53,6 +59,23 @@ class PtxError(RuntimeError):
 _lib = None
 
 
+def share_torch_runtime() -> None:
+    """Load torch (when installed) BEFORE libptx.so so the process has ONE HIP runtime.
+
+    torch bundles its own libamdhip64 / libhsa-runtime64 (soname .so.7 / .so.1) but links
+    them by the bare name libamdhip64.so: if libptx.so loads /opt/rocm's copy first, torch
+    then loads a second runtime and sees no GPU.  The other way round the dynamic linker
+    hands libptx.so torch's (already loaded, same soname) runtime -- measured: same frame
+    times, and torch tensors / RCCL work beside the handles (halo exchange).  Set
+    PTX_STANDALONE_RUNTIME=1 to skip it."""
+    if os.environ.get("PTX_STANDALONE_RUNTIME") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load(path: str = LIB_PATH):
     """Load libptx.so; raises PtxError when the HIP extension is not built."""
     global _lib
@@ -61,6 +84,7 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise PtxError(f"{path} is missing: build it with `make -C pathtracerdemo_amd/csrc` "
                        "(or __graft_entry__.build()); there is no CPU fallback")
+    share_torch_runtime()
     lib = ctypes.CDLL(path)
     P, H = ctypes.c_void_p, ctypes.c_void_p
     lib.ptx_abi_version.restype = ctypes.c_int
@@ -79,12 +103,19 @@ def load(path: str = LIB_PATH):
     lib.ptx_set_stream.argtypes = [H, P]
     lib.ptx_trace.argtypes = [H, P, P, ctypes.c_size_t, ctypes.c_int]
     lib.ptx_trace_device.argtypes = [H, P, P, ctypes.c_size_t, ctypes.c_int]
+    lib.ptx_run_passes.argtypes = [H, P, ctypes.c_int]
+    lib.ptx_halo_rows.argtypes = [H, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                  ctypes.POINTER(ctypes.c_size_t)]
+    lib.ptx_halo_pack.argtypes = [H, P, P]
+    lib.ptx_halo_unpack.argtypes = [H, P, P]
     lib.ptx_destroy.argtypes = [H]
     lib.ptx_last_error.argtypes = [H]
     lib.ptx_last_error.restype = ctypes.c_char_p
     for name in EXPORTED:
         if name not in ("ptx_last_error", "ptx_abi_version"):
             getattr(lib, name).restype = ctypes.c_int
+    if lib.ptx_abi_version() != PTX_ABI_VERSION:
+        raise PtxError(f"{path}: ABI {lib.ptx_abi_version()} != {PTX_ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 

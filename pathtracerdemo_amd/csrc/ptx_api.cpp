@@ -23,7 +23,7 @@ using namespace ptx;
 
 namespace {
 
-constexpr int kPasses = 8;
+constexpr int kPasses = 16;
 constexpr int kEventRing = 256;  // ~15 event pairs per wavefront frame
 
 struct DevBuf {
@@ -58,9 +58,15 @@ struct ptx_handle {
     // frame
     uint32_t uniform[PTX_UNIFORM_WORDS] = {0};
     bool frame_set = false;
-    // band buffers
-    uint32_t band_h = 0;
+    // band buffers; the G-buffer and PT_1 reservoirs carry halo_top / halo_bot extra rows
+    // (reuse pipeline on a band: the spatial pass reads neighbours up to reuse_radius away)
+    uint32_t band_h = 0, halo_top = 0, halo_bot = 0;
     DevBuf d_gbuf, d_res, d_accum, d_counters, d_queue;
+    // reuse pipeline: spatial output / history, shift-job state and results
+    DevBuf d_hist, d_jstate, d_jres;
+    uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
+    bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
+    uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
     DevBuf d_qrays, d_qhits;  // staging for ptx_trace (host arrays)
     // wavefront variant: pixel state, ray queue + ping-pong results / active lists, counters
     DevBuf d_wstate, d_wrays, d_wres0, d_wres1, d_wact0, d_wact1, d_wctr;
@@ -73,8 +79,8 @@ struct ptx_handle {
     // stats
     TimedLaunch ring[kEventRing];
     int ring_pos = 0;
-    double ms_total[kPasses] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t launches[kPasses] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double ms_total[kPasses] = {};
+    uint64_t launches[kPasses] = {};
     uint64_t frames = 0;
 };
 
@@ -116,6 +122,10 @@ static int upload(ptx_handle *h, DevBuf &b, const void *src, size_t bytes) {
     if (bytes) HIP_CHECK(h, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
     return PTX_OK;
 }
+
+// first band row of the halo-extended G-buffer / reservoir allocations
+static uint4 *gbuf_band(ptx_handle *h) { return (uint4 *)h->d_gbuf.p + (size_t)h->halo_top * h->cfg.width; }
+static uint4 *res_band(ptx_handle *h) { return (uint4 *)h->d_res.p + 8u * (size_t)h->halo_top * h->cfg.width; }
 
 static inline float as_f32(uint32_t u) {
     float f;
@@ -291,7 +301,8 @@ static void resolve_event(TimedLaunch &t, ptx_handle *h) {
 static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t npix = (size_t)h->band_h * h->cfg.width;
     const uint32_t nl = h->uniform[U_LIGHT_COUNT];
-    const size_t per_px = std::max<size_t>(2u, (size_t)nl + 1u);
+    const size_t jpp = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? 2u * h->reuse_neighbors : 1u;
+    const size_t per_px = std::max<size_t>(std::max<size_t>(2u, (size_t)nl + 1u), jpp);
     const size_t padded = (size_t)((h->cfg.width + 7u) / 8u) * ((h->band_h + 7u) / 8u) * 64u;
     static const uint32_t env_px = getenv("PTX_SEG_PX") ? (uint32_t)atoi(getenv("PTX_SEG_PX")) : 0u;  // A/B
     const uint32_t seg_px = (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) ? env_px : kWaveSegPixels;
@@ -299,8 +310,8 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t cap = per_px * seg_px * nseg;
     if (!h->d_wstate.p) {
         if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wact0, nseg * seg_px * 4u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wact1, nseg * seg_px * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wact0, nseg * seg_px * jpp * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wact1, nseg * seg_px * jpp * 4u)) return rc;
         if (int rc = alloc_buf(h, h->d_wctr, 2u * kWaveMaxRounds * nseg * 4u)) return rc;
     }
     if (cap > h->wave_ray_cap) {
@@ -323,6 +334,9 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     w.res[1] = (float4 *)h->d_wres1.p;
     w.act[0] = (uint32_t *)h->d_wact0.p;
     w.act[1] = (uint32_t *)h->d_wact1.p;
+    // one stride for every pass: passes of different kinds run concurrently on the two
+    // streams (e.g. one half's spatial pass beside the other half's PT_4)
+    w.act_stride = (uint32_t)(seg_px * jpp);
     w.cnt = (uint32_t *)h->d_wctr.p;
     w.seg_base = 0;
     w.seg_count = w.nseg;
@@ -346,12 +360,51 @@ static void event_end(TimedLaunch *t, hipStream_t st) {
     if (t && hipEventRecord(t->stop, st) == hipSuccess) t->pending = true;
 }
 
+static int reuse_buffers(ptx_handle *h) {
+    const size_t njobs = (size_t)h->band_h * h->cfg.width * 2u * h->reuse_neighbors;
+    if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
+    return alloc_buf(h, h->d_jres, njobs * 8u);
+}
+static ReuseArgs reuse_args(ptx_handle *h, int pass) {
+    ReuseArgs A{};
+    A.gbuf = gbuf_band(h);
+    A.cur = res_band(h);
+    A.hist = (uint4 *)h->d_hist.p;
+    A.jstate = (float4 *)h->d_jstate.p;
+    A.jres = (float2 *)h->d_jres.p;
+    A.jpp = pass == PTX_PASS_TEMPORAL ? 1u : 2u * h->reuse_neighbors;
+    A.njobs = h->band_h * h->cfg.width * A.jpp;
+    A.radius = h->reuse_radius;
+    A.neighbors = h->reuse_neighbors;
+    A.cap = h->temporal_cap;
+    A.hist_valid = h->hist_valid ? 1u : 0u;
+    return A;
+}
+
 // One pass over the segments [w.seg_base, w.seg_base + w.seg_count) on stream `st`.
 static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass, hipStream_t st) {
-    const uint4 *gb = (const uint4 *)h->d_gbuf.p;
-    uint4 *res = (uint4 *)h->d_res.p;
+    const uint4 *gb = gbuf_band(h);
+    uint4 *res = res_band(h);
     float4 *acc = (float4 *)h->d_accum.p;
     hipError_t e = hipSuccess;  // every round rewrites all of its segment counts: no memset
+    if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL) {
+        const ReuseArgs A = reuse_args(h, pass);
+        const WaveBufs &wj = w;
+        for (int r = 0; e == hipSuccess && r <= kWaveRoundsReuse + 1; ++r) {
+            if (r > 0 && r <= kWaveRoundsReuse) {
+                TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
+                e = wave_trace(sc, wj, r - 1, 1, h->stack_depth, st);
+                event_end(t, st);
+            }
+            if (e != hipSuccess) break;
+            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
+            e = wave_reuse_round(sc, wj, pass == PTX_PASS_TEMPORAL, r, A, st);
+            event_end(t, st);
+        }
+        return e;
+    }
+    // the reuse pipeline's PT_4 reads the spatial output
+    const uint4 *fres = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? (const uint4 *)h->d_hist.p : res;
     const int rounds = pass == PTX_PASS_INIT ? kWaveRoundsInit : pass == PTX_PASS_FINAL ? kWaveRoundsFinal
                                                                                         : kWaveRoundsMcpt;
     for (int r = 0; e == hipSuccess && r <= rounds; ++r) {
@@ -363,7 +416,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         if (e != hipSuccess) break;
         TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
         e = pass == PTX_PASS_INIT    ? wave_init_round(sc, w, r, gb, res, st)
-            : pass == PTX_PASS_FINAL ? wave_final_round(sc, w, r, gb, res, acc, st)
+            : pass == PTX_PASS_FINAL ? wave_final_round(sc, w, r, gb, fres, acc, st)
                                      : wave_mcpt_round(sc, w, r, acc, st);
         event_end(t, st);
     }
@@ -404,7 +457,7 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
         for (int i = 0; i < npasses; ++i) {
             if (passes[i] == PTX_PASS_GBUFFER) {
                 TimedLaunch *t = event_begin(h, PTX_PASS_GBUFFER, st);
-                e = wave_gbuffer(sc, part, (uint4 *)h->d_gbuf.p, h->stack_depth, st);
+                e = wave_gbuffer(sc, part, gbuf_band(h), h->stack_depth, st);
                 event_end(t, st);
             } else {
                 e = launch_wave_seq(h, sc, part, passes[i], st);
@@ -420,6 +473,13 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
 }
 static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass) {
     return launch_wave_parts(h, sc, w, &pass, 1);
+}
+
+// The spatial pass just wrote d_hist for the current camera: the next frame's temporal
+// pass may use it (ptx_set_frame drops it when the camera moves).
+static void mark_history(ptx_handle *h) {
+    std::memcpy(h->hist_camera, h->uniform + 4, sizeof h->hist_camera);
+    h->hist_valid = true;
 }
 
 // A whole ReSTIR frame in wavefront form (G-buffer -> init -> final per segment group), timed
@@ -440,8 +500,20 @@ static int timed_wave_frame(ptx_handle *h) {
     h->ring_pos = (h->ring_pos + 1) % kEventRing;
     resolve_event(t, h);
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
-    static const int passes[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL};
-    hipError_t e = launch_wave_parts(h, sc, w, passes, 3);
+    hipError_t e;
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+        // per-pixel passes up to the temporal output, then (after every segment is done:
+        // the spatial pass reads neighbours) spatial + PT_4
+        if (int rc = reuse_buffers(h)) return rc;
+        static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_TEMPORAL};
+        static const int back[2] = {PTX_PASS_SPATIAL, PTX_PASS_FINAL};
+        e = launch_wave_parts(h, sc, w, front, 3);
+        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, back, 2);
+        if (e == hipSuccess) mark_history(h);
+    } else {
+        static const int passes[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL};
+        e = launch_wave_parts(h, sc, w, passes, 3);
+    }
     if (e != hipSuccess) return fail(h, PTX_E_HIP, "wavefront frame launch: %s", hipGetErrorString(e));
     HIP_CHECK(h, hipEventRecord(t.stop, h->stream));
     t.pass = PTX_STAT_FRAME;
@@ -469,25 +541,31 @@ static int timed_launch(ptx_handle *h, int pass) {
     if (variant == 1 && pass != PTX_PASS_GBUFFER)
         HIP_CHECK(h, hipMemsetAsync(ctr, 0, sizeof(unsigned int), h->stream));
     WaveBufs w{};
+    const bool reuse_pass = pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL;
+    if (reuse_pass && (variant != 3 || h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE))
+        return fail(h, PTX_E_INVALID, "pass %d needs the reuse pipeline (wavefront kernels)", pass);
     if (variant == 3 && pass != PTX_PASS_GBUFFER) {
         if (int rc = wave_buffers(h, w)) return rc;
+        if (reuse_pass)
+            if (int rc = reuse_buffers(h)) return rc;
     }
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
     hipError_t e = hipSuccess;
-    const uint4 *gb = (const uint4 *)h->d_gbuf.p;
-    uint4 *res = (uint4 *)h->d_res.p;
+    const uint4 *gb = gbuf_band(h);
+    uint4 *res = res_band(h);
     float4 *acc = (float4 *)h->d_accum.p;
     const uint32_t d = h->stack_depth;
-    if (variant == 3 && pass != PTX_PASS_GBUFFER && pass >= PTX_PASS_INIT && pass <= PTX_PASS_MCPT) {
+    if (variant == 3 && ((pass >= PTX_PASS_INIT && pass <= PTX_PASS_MCPT) || reuse_pass)) {
         e = launch_wave_pass(h, sc, w, pass);
         if (e != hipSuccess) return fail(h, PTX_E_HIP, "wavefront launch (pass %d): %s", pass, hipGetErrorString(e));
+        if (pass == PTX_PASS_SPATIAL) mark_history(h);
         HIP_CHECK(h, hipEventRecord(t.stop, h->stream));
         t.pass = pass;
         t.pending = true;
         return PTX_OK;
     }
     switch (pass) {
-    case PTX_PASS_GBUFFER: e = launch_gbuffer(sc, (uint4 *)h->d_gbuf.p, d, h->stream); break;
+    case PTX_PASS_GBUFFER: e = launch_gbuffer(sc, gbuf_band(h), d, h->stream); break;
     case PTX_PASS_INIT:
         e = variant == 0   ? launch_init_tiled(sc, gb, res, d, h->stream)
             : variant == 1 ? launch_init_persistent(sc, gb, res, ctr, d, h->stream)
@@ -512,13 +590,16 @@ static int timed_launch(ptx_handle *h, int pass) {
     return PTX_OK;
 }
 
-static DevBuf *buffer_of(ptx_handle *h, int which) {
+// The band part of a public buffer (the G-buffer / reservoir allocations carry halo rows).
+static bool buffer_view(ptx_handle *h, int which, DevBuf &v) {
+    const size_t px = (size_t)h->band_h * h->cfg.width;
     switch (which) {
-    case PTX_BUF_GBUFFER: return &h->d_gbuf;
-    case PTX_BUF_RESERVOIR: return &h->d_res;
-    case PTX_BUF_ACCUM: return &h->d_accum;
-    case PTX_BUF_COUNTERS: return &h->d_counters;
-    default: return nullptr;
+    case PTX_BUF_GBUFFER: v.p = gbuf_band(h); v.bytes = px * 16u; return true;
+    case PTX_BUF_RESERVOIR: v.p = res_band(h); v.bytes = px * 128u; return true;
+    case PTX_BUF_ACCUM: v = h->d_accum; return true;
+    case PTX_BUF_COUNTERS: v = h->d_counters; return true;
+    case PTX_BUF_RESERVOIR_HIST: v = h->d_hist; return v.p != nullptr;
+    default: return false;
     }
 }
 
@@ -530,7 +611,11 @@ int ptx_abi_version(void) { return PTX_ABI_VERSION; }
 int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!cfg || !out) return PTX_E_INVALID;
     *out = nullptr;
-    if (cfg->width == 0 || cfg->height == 0 || cfg->pipeline > PTX_PIPELINE_MCPT) return PTX_E_INVALID;
+    if (cfg->width == 0 || cfg->height == 0 || cfg->pipeline > PTX_PIPELINE_RESTIR_REUSE) return PTX_E_INVALID;
+    if (cfg->pipeline == PTX_PIPELINE_RESTIR_REUSE &&
+        (cfg->flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE)))
+        return PTX_E_INVALID;  // the reuse passes exist in wavefront form only
+    if (cfg->reuse_neighbors > 16u) return PTX_E_INVALID;
     ptx_handle *h = new (std::nothrow) ptx_handle();
     if (!h) return PTX_E_NOMEM;
     h->cfg = *cfg;
@@ -540,6 +625,17 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
         return PTX_E_INVALID;
     }
     h->band_h = h->cfg.row_end - h->cfg.row_begin;
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+        h->reuse_radius = h->cfg.reuse_radius ? h->cfg.reuse_radius : 30u;
+        h->reuse_neighbors = h->cfg.reuse_neighbors ? h->cfg.reuse_neighbors : 3u;
+        h->temporal_cap = h->cfg.temporal_cap ? h->cfg.temporal_cap : 20u;
+        h->halo_top = std::min(h->reuse_radius, h->cfg.row_begin);
+        h->halo_bot = std::min(h->reuse_radius, h->cfg.height - h->cfg.row_end);
+        if ((h->halo_top || h->halo_bot) && h->band_h < h->reuse_radius) {  // halos come from adjacent bands only
+            delete h;
+            return PTX_E_INVALID;
+        }
+    }
     int rc = PTX_OK;
     hipError_t e;
     if (cfg->device >= 0) {
@@ -553,8 +649,13 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     }
     h->stream = h->own_stream;
     const size_t px = (size_t)h->band_h * h->cfg.width;
-    if (!rc) rc = alloc_buf(h, h->d_gbuf, px * 16u);
-    if (!rc) rc = alloc_buf(h, h->d_res, px * 128u);
+    const size_t px_halo = (size_t)(h->halo_top + h->band_h + h->halo_bot) * h->cfg.width;
+    if (!rc) rc = alloc_buf(h, h->d_gbuf, px_halo * 16u);
+    if (!rc) rc = alloc_buf(h, h->d_res, px_halo * 128u);
+    if (!rc && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+        rc = alloc_buf(h, h->d_hist, px * 128u);
+        if (!rc && hipMemset(h->d_hist.p, 0, h->d_hist.bytes) != hipSuccess) rc = PTX_E_HIP;
+    }
     if (!rc) rc = alloc_buf(h, h->d_accum, px * 16u);
     if (!rc) rc = alloc_buf(h, h->d_counters, kCounterWords * 8u);
     if (!rc) rc = alloc_buf(h, h->d_queue, 64u);
@@ -581,6 +682,7 @@ int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const
     if (int rc = upload(h, h->d_geometry, geometry, n_geometry * 4u)) return rc;
     h->layout_valid = false;
     h->scene_loaded = true;
+    h->hist_valid = false;
     if (h->frame_set) return build_layout(h);
     return PTX_OK;
 }
@@ -598,6 +700,8 @@ int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]) {
     }
     std::memcpy(h->uniform, uniform, sizeof h->uniform);
     h->frame_set = true;
+    // temporal history is reusable only for the camera (and scene) that produced it
+    if (std::memcmp(h->hist_camera, uniform + 4, sizeof h->hist_camera) != 0) h->hist_valid = false;
     if (h->scene_loaded && !h->layout_valid) return build_layout(h);
     return PTX_OK;
 }
@@ -607,6 +711,96 @@ int ptx_run_pass(ptx_handle *h, int pass) {
     return timed_launch(h, pass);
 }
 
+int ptx_run_passes(ptx_handle *h, const int *passes, int n) {
+    if (!h || (!passes && n)) return PTX_E_INVALID;
+    if (n < 0 || n > 8) return fail(h, PTX_E_INVALID, "ptx_run_passes: %d passes", n);
+    for (int i = 0; i < n; ++i) {
+        const int p = passes[i];
+        const bool ok = p == PTX_PASS_GBUFFER || p == PTX_PASS_INIT || p == PTX_PASS_FINAL || p == PTX_PASS_MCPT ||
+                        p == PTX_PASS_TEMPORAL || (p == PTX_PASS_SPATIAL && i == 0);
+        if (!ok) return fail(h, PTX_E_INVALID, "ptx_run_passes: pass %d at position %d", p, i);
+        if ((p == PTX_PASS_TEMPORAL || p == PTX_PASS_SPATIAL) && h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE)
+            return fail(h, PTX_E_INVALID, "pass %d needs the reuse pipeline", p);
+    }
+    const uint32_t fl = h->cfg.flags;
+    if (fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE | PTX_FLAG_COUNT_WORK)) {
+        for (int i = 0; i < n; ++i)
+            if (int rc = timed_launch(h, passes[i])) return rc;
+        return PTX_OK;
+    }
+    if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before rendering");
+    if (!h->layout_valid) {
+        if (int rc = build_layout(h)) return rc;
+    }
+    Scene sc = make_scene(h);
+    bool gb = false, reuse = false;
+    for (int i = 0; i < n; ++i) {
+        gb |= passes[i] == PTX_PASS_GBUFFER;
+        reuse |= passes[i] == PTX_PASS_TEMPORAL || passes[i] == PTX_PASS_SPATIAL;
+    }
+    if (gb && !tables_fit_lds(sc)) {  // the segment-mapped G-buffer needs LDS tables
+        for (int i = 0; i < n; ++i)
+            if (int rc = timed_launch(h, passes[i])) return rc;
+        return PTX_OK;
+    }
+    WaveBufs w{};
+    if (int rc = wave_buffers(h, w)) return rc;
+    if (reuse)
+        if (int rc = reuse_buffers(h)) return rc;
+    TimedLaunch &t = h->ring[h->ring_pos];
+    h->ring_pos = (h->ring_pos + 1) % kEventRing;
+    resolve_event(t, h);
+    HIP_CHECK(h, hipEventRecord(t.start, h->stream));
+    const hipError_t e = launch_wave_parts(h, sc, w, passes, n);
+    if (e != hipSuccess) return fail(h, PTX_E_HIP, "ptx_run_passes: %s", hipGetErrorString(e));
+    HIP_CHECK(h, hipEventRecord(t.stop, h->stream));
+    t.pass = PTX_STAT_PASS_GROUP;
+    t.pending = true;
+    for (int i = 0; i < n; ++i)
+        if (passes[i] == PTX_PASS_SPATIAL) mark_history(h);
+    return PTX_OK;
+}
+
+int ptx_halo_rows(ptx_handle *h, uint32_t *rows_top, uint32_t *rows_bottom, size_t *bytes_per_row) {
+    if (!h) return PTX_E_INVALID;
+    if (rows_top) *rows_top = h->halo_top;
+    if (rows_bottom) *rows_bottom = h->halo_bot;
+    if (bytes_per_row) *bytes_per_row = (size_t)h->cfg.width * (16u + 128u);
+    return PTX_OK;
+}
+
+// Rows [r0, r0 + rows) of the halo-extended G-buffer / reservoir (row 0 = first halo row)
+// <-> one contiguous message (G-buffer rows, then reservoir rows).
+static int halo_copy(ptx_handle *h, uint32_t r0, uint32_t rows, void *msg, bool to_msg) {
+    if (!rows) return PTX_OK;
+    const size_t W = h->cfg.width, gb = rows * W * 16u, rb = rows * W * 128u;
+    char *g = (char *)h->d_gbuf.p + (size_t)r0 * W * 16u, *r = (char *)h->d_res.p + (size_t)r0 * W * 128u;
+    char *m = (char *)msg;
+    if (to_msg) {
+        HIP_CHECK(h, hipMemcpyAsync(m, g, gb, hipMemcpyDeviceToDevice, h->stream));
+        HIP_CHECK(h, hipMemcpyAsync(m + gb, r, rb, hipMemcpyDeviceToDevice, h->stream));
+    } else {
+        HIP_CHECK(h, hipMemcpyAsync(g, m, gb, hipMemcpyDeviceToDevice, h->stream));
+        HIP_CHECK(h, hipMemcpyAsync(r, m + gb, rb, hipMemcpyDeviceToDevice, h->stream));
+    }
+    return PTX_OK;
+}
+
+int ptx_halo_pack(ptx_handle *h, void *dev_top, void *dev_bottom) {
+    if (!h) return PTX_E_INVALID;
+    if ((h->halo_top && !dev_top) || (h->halo_bot && !dev_bottom)) return fail(h, PTX_E_INVALID, "ptx_halo_pack: null buffer");
+    // the band's first halo_top rows go up (the band above keeps them as its bottom halo)
+    if (int rc = halo_copy(h, h->halo_top, h->halo_top, dev_top, true)) return rc;
+    return halo_copy(h, h->halo_top + h->band_h - h->halo_bot, h->halo_bot, dev_bottom, true);
+}
+
+int ptx_halo_unpack(ptx_handle *h, const void *dev_top, const void *dev_bottom) {
+    if (!h) return PTX_E_INVALID;
+    if ((h->halo_top && !dev_top) || (h->halo_bot && !dev_bottom)) return fail(h, PTX_E_INVALID, "ptx_halo_unpack: null buffer");
+    if (int rc = halo_copy(h, 0u, h->halo_top, (void *)dev_top, false)) return rc;
+    return halo_copy(h, h->halo_top + h->band_h, h->halo_bot, (void *)dev_bottom, false);
+}
+
 int ptx_render(ptx_handle *h, float *rgba_out) {
     if (!h) return PTX_E_INVALID;
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR) {
@@ -614,6 +808,14 @@ int ptx_render(ptx_handle *h, float *rgba_out) {
         if (rc < 0) return rc;
         if (rc == 1)  // other variants / counting builds: pass by pass
             for (int p : {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL})
+                if ((rc = timed_launch(h, p))) return rc;
+    } else if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+        if (h->halo_top || h->halo_bot)
+            return fail(h, PTX_E_INVALID, "a band of the reuse pipeline renders through ptx_run_passes + ptx_halo_*");
+        int rc = timed_wave_frame(h);
+        if (rc < 0) return rc;
+        if (rc == 1)  // counting builds: pass by pass
+            for (int p : {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_TEMPORAL, PTX_PASS_SPATIAL, PTX_PASS_FINAL})
                 if ((rc = timed_launch(h, p))) return rc;
     } else {
         if (int rc = timed_launch(h, PTX_PASS_MCPT)) return rc;
@@ -629,6 +831,7 @@ int ptx_render(ptx_handle *h, float *rgba_out) {
 int ptx_reset_accumulation(ptx_handle *h) {
     if (!h) return PTX_E_INVALID;
     HIP_CHECK(h, hipMemsetAsync(h->d_accum.p, 0, h->d_accum.bytes, h->stream));
+    h->hist_valid = false;
     return PTX_OK;
 }
 
@@ -652,7 +855,8 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
     out->instances = h->n_inst;
     out->max_bvh_depth = h->max_depth;
     out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
-                        h->d_subs.bytes + h->d_insts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes;
+                        h->d_subs.bytes + h->d_insts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
+                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes;
     return PTX_OK;
 }
 
@@ -668,28 +872,30 @@ int ptx_reset_stats(ptx_handle *h) {
 
 int ptx_read_buffer(ptx_handle *h, int which, void *host_dst, size_t bytes) {
     if (!h || !host_dst) return PTX_E_INVALID;
-    DevBuf *b = buffer_of(h, which);
-    if (!b || bytes > b->bytes) return fail(h, PTX_E_INVALID, "read of %zu bytes from buffer %d", bytes, which);
+    DevBuf b;
+    if (!buffer_view(h, which, b) || bytes > b.bytes)
+        return fail(h, PTX_E_INVALID, "read of %zu bytes from buffer %d", bytes, which);
     HIP_CHECK(h, hipStreamSynchronize(h->stream));
-    HIP_CHECK(h, hipMemcpy(host_dst, b->p, bytes, hipMemcpyDeviceToHost));
+    HIP_CHECK(h, hipMemcpy(host_dst, b.p, bytes, hipMemcpyDeviceToHost));
     return PTX_OK;
 }
 
 int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t bytes) {
     if (!h || !host_src) return PTX_E_INVALID;
-    DevBuf *b = buffer_of(h, which);
-    if (!b || bytes > b->bytes) return fail(h, PTX_E_INVALID, "write of %zu bytes to buffer %d", bytes, which);
+    DevBuf b;
+    if (!buffer_view(h, which, b) || bytes > b.bytes)
+        return fail(h, PTX_E_INVALID, "write of %zu bytes to buffer %d", bytes, which);
     HIP_CHECK(h, hipStreamSynchronize(h->stream));
-    HIP_CHECK(h, hipMemcpy(b->p, host_src, bytes, hipMemcpyHostToDevice));
+    HIP_CHECK(h, hipMemcpy(b.p, host_src, bytes, hipMemcpyHostToDevice));
     return PTX_OK;
 }
 
 int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes) {
     if (!h || !dev_ptr) return PTX_E_INVALID;
-    DevBuf *b = buffer_of(h, which);
-    if (!b) return fail(h, PTX_E_INVALID, "unknown buffer %d", which);
-    *dev_ptr = b->p;
-    if (bytes) *bytes = b->bytes;
+    DevBuf b;
+    if (!buffer_view(h, which, b)) return fail(h, PTX_E_INVALID, "unknown buffer %d", which);
+    *dev_ptr = b.p;
+    if (bytes) *bytes = b.bytes;
     return PTX_OK;
 }
 
@@ -747,7 +953,8 @@ int ptx_destroy(ptx_handle *h) {
     }
     for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
-                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr})
+                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
+                      &h->d_hist, &h->d_jstate, &h->d_jres})
         free_buf(*b);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

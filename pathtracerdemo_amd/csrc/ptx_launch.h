@@ -58,7 +58,8 @@ struct WaveBufs {
     uint32_t ray_stride; // ray slots per segment (seg_px * max rays per pixel per round)
     float4 *rays;        // 2 float4 per ray: {o, remain}, {d, kind}
     float4 *res[2];      // 2 float4 per ray, ping-pong by round parity
-    uint32_t *act[2];    // active pixel lists (nseg * seg_px), ping-pong
+    uint32_t *act[2];    // active pixel / job lists (nseg * act_stride), ping-pong
+    uint32_t act_stride; // list entries per segment (seg_px; seg_px * jobs per pixel for reuse)
     uint32_t *cnt;       // 2 * kWaveMaxRounds * nseg counts
 };
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t stack_depth,
@@ -71,5 +72,19 @@ hipError_t wave_gbuffer(const Scene &sc, const WaveBufs &w, uint4 *gbuf, uint32_
 hipError_t launch_trace_rays_sm(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
                                 uint32_t stack_depth, hipStream_t s);
 hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, hipStream_t s);
+
+// reuse passes (ptx_reuse.hip): round 0 start, 1..kWaveRoundsReuse step, then combine
+constexpr int kWaveRoundsReuse = 3;
+struct ReuseArgs {
+    const uint4 *gbuf;  // G-buffer of the band's first row; halo rows at negative / >= npix indices
+    uint4 *cur;         // PT_1 reservoirs (temporal output in place), same addressing
+    uint4 *hist;        // spatial output = PT_4 input = next frame's history (band only)
+    float4 *jstate;     // shift-job state, 6 float4 slots x njobs (SoA)
+    float2 *jres;       // per job: {p_hat, q} (q = 0: invalid)
+    uint32_t njobs, jpp;  // jobs of the pass (npix * jpp), jobs per pixel
+    uint32_t radius, neighbors, cap, hist_valid;
+};
+hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,
+                            hipStream_t s);
 
 }  // namespace ptx

@@ -1,0 +1,428 @@
+// ptx_reuse.hip -- temporal and spatial reuse passes in wavefront form.
+//
+// Not in the reference code: specified only in docs/theory/ReSTIR_Pipeline.md:259-462
+// (pass 2 temporal, pass 3 spatial; confidence-weighted generalized balance heuristic) and
+// docs/theory/memo.md:166-231 (shift + Jacobian).  The build-defined rules are those of
+// oracle/pt_oracle.c (eval_sample, temporal_pixel, spatial_pixel), and
+// every reservoir these kernels write is bit-identical to the oracle's.
+//
+// Both passes are made of "shift jobs": evaluate a reservoir sample (rSeed, XL, length) in
+// the domain of some pixel (its camera point and G-buffer hit) -- PT_4's RegeneratePath +
+// PathContribution (SH/PT_4_FinalShadingPass.wgsl:1306-1384) plus the shift's pdf product
+// and PT_1's roulette factor -- giving (p_hat, q).  A job is <= 3 traces (two regenerated
+// BSDF rays, then the light's Visibility), so a pass is: start (create jobs, emit round 0),
+// {trace, step} x 3, combine (per pixel: MIS weights, resampling, reservoir out).
+//   temporal: 1 job per pixel (its PT_1 sample in its own domain)
+//   spatial:  2 per neighbour (neighbour sample -> this pixel, this sample -> neighbour)
+// Jobs live in the segment of their pixel; job id = pixel * jobs_per_pixel + slot.
+#include "ptx_wave_common.h"
+
+namespace ptx {
+
+constexpr uint32_t SALT_TEMPORAL = 0x54454D50u, SALT_SPATIAL = 0x53504154u;
+
+// Job state, SoA float4 slots (slot k of job j at jstate[k * njobs + j]):
+// HDR {i | length << 8 | phase << 16, rSeed[1], ray idx, sample ref}; F {f, prod | q};
+// CUR {pos, inst << 16 | mat}; NRM {nrm, beta}; PREV {prev pos, rr_p}; RRF {rr_f, -}
+enum : uint32_t { JS_HDR, JS_F, JS_CUR, JS_NRM, JS_PREV, JS_RRF, JS_COUNT };
+
+struct Job {
+    uint32_t i, length, phase, seed1, idx, matref;
+    int32_t ref;  // reservoir index of the sample (band-relative; halo rows are < 0 or >= npix)
+    f3 f;
+    float prod;   // pdf product of the regenerated directions; q once the light ray is out
+    Surface cur;
+    f3 prev;
+    float beta, rr_p;
+    f3 rr_f;
+};
+
+__device__ __forceinline__ const uint4 *res_at(const uint4 *base, int32_t idx) { return base + 8 * (ptrdiff_t)idx; }
+
+__device__ __forceinline__ void job_store(const ReuseArgs &A, uint32_t jid, const Job &s) {
+    const size_t n = A.njobs;
+    float4 *st = A.jstate;
+    st[JS_HDR * n + jid] = make_float4(asf(s.i | (s.length << 8) | (s.phase << 16)), asf(s.seed1), asf(s.idx),
+                                       asf((uint32_t)s.ref));
+    st[JS_F * n + jid] = make_float4(s.f.x, s.f.y, s.f.z, s.prod);
+    st[JS_CUR * n + jid] = make_float4(s.cur.pos.x, s.cur.pos.y, s.cur.pos.z, asf(s.matref));
+    st[JS_NRM * n + jid] = make_float4(s.cur.nrm.x, s.cur.nrm.y, s.cur.nrm.z, s.beta);
+    st[JS_PREV * n + jid] = make_float4(s.prev.x, s.prev.y, s.prev.z, s.rr_p);
+    st[JS_RRF * n + jid] = make_float4(s.rr_f.x, s.rr_f.y, s.rr_f.z, 0.0f);
+}
+__device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, uint32_t jid, Job &s) {
+    const size_t n = A.njobs;
+    const float4 *st = A.jstate;
+    const float4 hd = st[JS_HDR * n + jid], fv = st[JS_F * n + jid], cu = st[JS_CUR * n + jid];
+    const float4 nr = st[JS_NRM * n + jid], pv = st[JS_PREV * n + jid], rf = st[JS_RRF * n + jid];
+    const uint32_t hw = asu(hd.x);
+    s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = hw >> 16;
+    s.seed1 = asu(hd.y); s.idx = asu(hd.z); s.ref = (int32_t)asu(hd.w);
+    s.f = mk(fv.x, fv.y, fv.z); s.prod = fv.w;
+    s.matref = asu(cu.w);
+    s.cur.pos = mk(cu.x, cu.y, cu.z);
+    s.cur.nrm = mk(nr.x, nr.y, nr.z);
+    s.cur.mat = get_material(sc, desc_ptr(sc, sc.insts[s.matref >> 16].mesh), s.matref & 0xffffu);
+    s.beta = nr.w;
+    s.prev = mk(pv.x, pv.y, pv.z); s.rr_p = pv.w;
+    s.rr_f = mk(rf.x, rf.y, rf.z);
+}
+
+// PT_1's throughput recursion + Russian roulette at one replayed vertex (oracle rr_step).
+__device__ __forceinline__ bool rr_step(Job &s, const Surface &X, f3 V, f3 L, float pdf) {
+    s.rr_f = s.rr_f * (bsdf(X, V, L) * fabsf(dot(X.nrm, L)));
+    s.rr_p *= pdf;
+    const float ps = luminance(s.rr_f) / s.rr_p;
+    const bool ok = ps > 0.0f;
+    s.rr_p *= ps;
+    if (ps > 1.0f) s.beta /= ps;
+    return ok;
+}
+
+// Job at domain pixel (x, y) with G-buffer hit x1, sample `ref`: false if eval_sample's
+// preconditions fail (no job; its result is invalid).
+__device__ __forceinline__ bool job_begin(const Scene &sc, const ReuseArgs &A, Job &s, uint32_t x, uint32_t y,
+                                          const Compact &x1, int32_t ref) {
+    const uint4 *rv = res_at(A.cur, ref);
+    const uint32_t C = rv[7].y, length = rv[5].w;
+    if (!x1.valid || C == 0u || length < 2u) return false;
+    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = rv[0].y; s.idx = 0u; s.ref = ref;
+    s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
+    s.prev = x0_of(sc, x, y);
+    s.cur = get_surface(sc, x1);
+    s.matref = (x1.inst << 16) | x1.mat;
+    s.beta = 1.0f; s.rr_p = 1.0f; s.rr_f = mk(1.0f, 1.0f, 1.0f);
+    return true;
+}
+
+// The job's next ray: a regenerated BSDF direction (PT_4:1367-1381) or the light
+// segment's Visibility (PT_4:1323-1333).  Called by every lane of the wave; `emit` selects
+// the lanes with a live job.  Returns whether the job continues (else its result is out).
+__device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const ReuseArgs &A, bool emit, Job &s,
+                                         uint32_t jid) {
+    bool ray = false, vis = false;
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = o, Le = o;
+    float remain = -1.0f;
+    if (emit) {
+        const uint4 *rv = res_at(A.cur, s.ref);
+        const f3 V = normalize(s.prev - s.cur.pos);
+        bool ok = true;
+        if (s.i + 1u < s.length) {
+            uint32_t seed = s.i == 1u ? rv[0].x : s.seed1, lobe;
+            const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
+            const float pdf = pdf_bsdf(s.cur, V, dir);
+            s.prod *= pdf;
+            ok = rr_step(s, s.cur, V, dir, pdf);
+            s.phase = 0u;
+            o = s.cur.pos; d = dir;
+        } else {
+            const LightSample XL = load_xl(rv);
+            const f3 L = direction_to_light(s.cur, XL);
+            if (XL.type == LIGHT_ENV) ok = rr_step(s, s.cur, V, L, pdf_bsdf(s.cur, V, L));
+            s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+            float gl = 1.0f;
+            if (XL.type == LIGHT_RECT) {
+                const f3 r = XL.pos - s.cur.pos;
+                const f3 Ld = normalize(r);
+                gl = fabsf(dot(get_light(sc, (uint32_t)XL.id).dir, Ld)) / dot(r, r);
+            }
+            s.prod = s.prod / (gl * s.beta);  // q
+            Le = l_emit<true>(XL, s.cur);
+            s.phase = 1u;
+            const float dist = length(XL.pos - s.cur.pos);
+            o = s.cur.pos; d = (XL.pos - s.cur.pos) / dist; remain = dist;
+            vis = true;
+        }
+        if (ok) ray = true;
+        else A.jres[jid] = make_float2(0.0f, 0.0f);  // PT_1 would have ended such a path
+    }
+    const uint32_t idx = g.rbase + wave_alloc(g.l_ray, ray ? 1u : 0u);
+    if (ray) {
+        s.idx = idx;
+        put_ray(g.rays, idx, o, d, remain, vis ? Q_VIS : Q_CLOSEST);
+        if (vis) g.res_out[2u * idx] = make_float4(0.0f, Le.x, Le.y, Le.z);
+    }
+    return ray;
+}
+
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, round, lds);
+    const uint32_t n = g.n_in;
+    for (uint32_t base = 0; base < n; base += WB) {
+        const uint32_t q = base + threadIdx.x;
+        bool emit = false;
+        uint32_t jid = 0u;
+        Job s;
+        if (q < n) {
+            jid = g.act_in[q];
+            job_load(sc, A, jid, s);
+            if (s.phase == 0u) {  // regenerated vertex i+1 arrived (PT_4:1378-1380)
+                const Hit h = get_hit(g.res_in, s.idx);
+                if (!h.valid) {
+                    A.jres[jid] = make_float2(0.0f, 0.0f);  // the replayed path escapes here
+                } else {
+                    const Surface next = surface_at(sc, h.s, h.pos);
+                    const f3 V = normalize(s.prev - s.cur.pos);
+                    const f3 L = normalize(next.pos - s.cur.pos);
+                    s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+                    s.prev = s.cur.pos;
+                    s.cur = next;
+                    s.matref = (h.s.inst << 16) | h.s.mat;
+                    s.i += 1u;
+                    emit = true;
+                }
+            } else {  // the light segment's Visibility arrived
+                const float4 a = g.res_in[2u * s.idx];
+                s.f = s.f * (mk(a.y, a.z, a.w) * a.x);
+                const float qv = s.prod;
+                const bool valid = qv > 0.0f && qv <= 3.402823466e38f;
+                A.jres[jid] = valid ? make_float2(luminance(s.f), qv) : make_float2(0.0f, 0.0f);
+            }
+        }
+        const bool live = job_emit(sc, g, A, emit, s, jid);
+        if (live) job_store(A, jid, s);
+        seg_keep(g, live, jid);
+    }
+    seg_end(w, g);
+}
+
+__device__ __forceinline__ uint32_t reuse_seed(const Scene &sc, uint32_t x, uint32_t y, uint32_t salt) {
+    return pcg(pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u) ^ salt);
+}
+__device__ __forceinline__ bool wrs_update(float &w_sum, float wt, uint32_t &seed) {  // PT_1:1298-1320
+    w_sum += wt;
+    return rnd(seed) < wt / w_sum;
+}
+__device__ __forceinline__ void write_reused(uint4 *out, const uint4 *src, float p_sel, float q_sel, float w_sum,
+                                             uint32_t C) {
+    uint4 t[6];
+    for (int k = 0; k < 6; ++k) t[k] = src[k];  // src may be out itself (temporal)
+    for (int k = 0; k < 6; ++k) out[k] = t[k];
+    out[6] = make_uint4(asu(p_sel), asu(q_sel), 0u, 0u);
+    out[7] = make_uint4(asu(p_sel > 0.0f ? w_sum / p_sel : 0.0f), C, 0u, 0u);
+}
+
+// ---------------------------------------------------------------- temporal
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    const uint32_t np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, g.j, k);
+        uint32_t x, y, pix = 0u;
+        bool active = false;
+        Job s;
+        if (q < np && tile_xy(sc, q, x, y)) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            active = job_begin(sc, A, s, x, y, gdecode(A.gbuf[pix]), (int32_t)pix);
+        }
+        const bool live = job_emit(sc, g, A, active, s, pix);
+        if (live) job_store(A, pix, s);
+        seg_keep(g, live, pix);
+    }
+    seg_end(w, g);
+}
+
+// Temporal resampling of the pixel's PT_1 reservoir with the previous frame's output at
+// the same pixel (oracle temporal_pixel): static camera, identity shift.
+__global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, ReuseArgs A) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        if (!gdecode(A.gbuf[pix]).valid) continue;  // PT_1 wrote the zero reservoir
+        uint4 *rv = A.cur + 8u * (size_t)pix;
+        const uint4 *hv = A.hist + 8u * (size_t)pix;
+        uint32_t seed = reuse_seed(sc, x, y, SALT_TEMPORAL);
+        const uint4 r5 = rv[5], r7 = rv[7];
+        const float2 ec = (r7.y != 0u && r5.w >= 2u) ? A.jres[pix] : make_float2(0.0f, 0.0f);
+        const bool canon_ok = ec.y > 0.0f && ec.x > 0.0f;
+        const uint4 h5 = hv[5], h6 = hv[6], h7 = hv[7];
+        const uint32_t Cp = A.hist_valid ? min(h7.y, A.cap) : 0u;
+        const float cp = (float)Cp, tot = 1.0f + cp;
+        const float pp = asf(h6.x), qp = asf(h6.y);
+        const bool hist_ok = Cp != 0u && h5.w >= 2u && pp > 0.0f;
+        const float wc = canon_ok ? (1.0f / tot) * ec.x * asf(r7.x) : 0.0f;
+        const float wp = hist_ok ? (cp / tot) * pp * asf(h7.x) : 0.0f;
+        float w_sum = 0.0f, p_sel = ec.x, q_sel = ec.y;
+        bool from_hist = false;
+        if (wrs_update(w_sum, wc, seed)) { from_hist = false; p_sel = ec.x; q_sel = ec.y; }
+        if (wrs_update(w_sum, wp, seed)) { from_hist = true; p_sel = pp; q_sel = qp; }
+        write_reused(rv, from_hist ? hv : rv, p_sel, q_sel, w_sum, 1u + Cp);
+    }
+}
+
+// ---------------------------------------------------------------- spatial
+// Spatial neighbour of (x, y): two draws, offsets in [-R, R]^2 (oracle spatial_neighbor).
+__device__ __forceinline__ bool spatial_neighbor(uint32_t &seed, uint32_t R, uint32_t x, uint32_t y, uint32_t W,
+                                                 uint32_t H, uint32_t &nx, uint32_t &ny) {
+    const float side = (float)(2u * R + 1u);
+    uint32_t ix = (uint32_t)(rnd(seed) * side);
+    uint32_t iy = (uint32_t)(rnd(seed) * side);
+    ix = min(ix, 2u * R);  // Random() can return exactly 1.0
+    iy = min(iy, 2u * R);
+    const int X = (int)x + (int)ix - (int)R, Y = (int)y + (int)iy - (int)R;
+    if (X < 0 || Y < 0 || X >= (int)W || Y >= (int)H || (ix == R && iy == R)) return false;
+    nx = (uint32_t)X;
+    ny = (uint32_t)Y;
+    return true;
+}
+__device__ __forceinline__ int32_t band_index(const Scene &sc, uint32_t x, uint32_t y) {
+    return ((int32_t)y - (int32_t)sc.row_begin) * (int32_t)sc.width + (int32_t)x;
+}
+
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    const uint32_t np = padded_pixels(sc), M = A.neighbors;
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, g.j, k);
+        uint32_t x = 0u, y = 0u, pix = 0u, seed = 0u;
+        bool center = false, canon_ok = false;
+        Compact x1{};
+        if (q < np && tile_xy(sc, q, x, y)) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            x1 = gdecode(A.gbuf[pix]);
+            center = x1.valid != 0u;
+            if (center) {
+                seed = reuse_seed(sc, x, y, SALT_SPATIAL);
+                const uint4 *rc = A.cur + 8u * (size_t)pix;
+                canon_ok = rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
+            }
+        }
+        for (uint32_t m = 0; m < M; ++m) {  // workgroup-uniform
+            uint32_t nx = 0u, ny = 0u;
+            bool present = center && spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+            const int32_t nidx = present ? band_index(sc, nx, ny) : 0;
+            Compact xn{};
+            if (present) {
+                xn = gdecode(A.gbuf[nidx]);
+                present = xn.valid != 0u;
+            }
+            bool fwd = false, bwd = false;
+            if (present) {
+                const uint4 *rn = res_at(A.cur, nidx);
+                fwd = rn[5].w >= 2u && asf(rn[6].x) > 0.0f;
+                bwd = canon_ok;
+            }
+            const uint32_t jf = pix * A.jpp + 2u * m, jb = jf + 1u;
+            Job s;
+            // forward: the neighbour's sample in this pixel's domain
+            bool act = fwd && job_begin(sc, A, s, x, y, x1, nidx);
+            if (fwd && !act) A.jres[jf] = make_float2(0.0f, 0.0f);
+            bool live = job_emit(sc, g, A, act, s, jf);
+            if (live) job_store(A, jf, s);
+            seg_keep(g, live, jf);
+            // backward: this pixel's sample in the neighbour's domain
+            act = bwd && job_begin(sc, A, s, nx, ny, xn, (int32_t)pix);
+            if (bwd && !act) A.jres[jb] = make_float2(0.0f, 0.0f);
+            live = job_emit(sc, g, A, act, s, jb);
+            if (live) job_store(A, jb, s);
+            seg_keep(g, live, jb);
+        }
+    }
+    seg_end(w, g);
+}
+
+// Pairwise-MIS resampling of the pixel's temporal reservoir and its neighbours' shifted
+// samples (oracle spatial_pixel); writes the reservoir PT_4 reads.
+__global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, ReuseArgs A) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc), M = A.neighbors;
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        uint4 *out = A.hist + 8u * (size_t)pix;
+        if (!gdecode(A.gbuf[pix]).valid) {
+            for (int t = 0; t < 8; ++t) out[t] = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
+        const uint4 *rc = A.cur + 8u * (size_t)pix;
+        const uint4 c5 = rc[5], c6 = rc[6], c7 = rc[7];
+        const float Mf = (float)M, cc = (float)c7.y;
+        const float pc = asf(c6.x), qc = asf(c6.y), Wc = asf(c7.x);
+        const bool canon_ok = c7.y != 0u && c5.w >= 2u && pc > 0.0f;
+        const uint32_t seed0 = reuse_seed(sc, x, y, SALT_SPATIAL);
+        // pass 1: neighbours' confidences and the canonical sample's MIS weight
+        uint32_t seed = seed0, Csum = c7.y;
+        float sumQ = 0.0f;
+        for (uint32_t m = 0; m < M; ++m) {
+            uint32_t nx = 0u, ny = 0u;
+            float Q = 1.0f;
+            if (spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
+                const int32_t nidx = band_index(sc, nx, ny);
+                if (gdecode(A.gbuf[nidx]).valid) {
+                    const uint32_t Cn = res_at(A.cur, nidx)[7].y;
+                    Csum += Cn;
+                    if (canon_ok) {
+                        const float2 B = A.jres[pix * A.jpp + 2u * m + 1u];
+                        if (B.y > 0.0f) {
+                            const float pbc = B.x * qc / B.y;
+                            const float den = cc * pc + Mf * (float)Cn * pbc;
+                            Q = den > 0.0f ? (cc * pc) / den : 1.0f;
+                        }
+                    }
+                }
+            }
+            sumQ += Q;
+        }
+        // pass 2: resampling, canonical first (the selection draws follow the offsets)
+        const float wc = canon_ok ? (sumQ / Mf) * pc * Wc : 0.0f;
+        float w_sum = 0.0f, p_sel = pc, q_sel = qc;
+        int32_t src = (int32_t)pix;
+        uint32_t nseed = seed0;
+        if (wrs_update(w_sum, wc, seed)) { src = (int32_t)pix; p_sel = pc; q_sel = qc; }
+        for (uint32_t m = 0; m < M; ++m) {
+            uint32_t nx = 0u, ny = 0u;
+            float wn = 0.0f, pf = 0.0f, qf = 0.0f;
+            int32_t nidx = 0;
+            if (spatial_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
+                nidx = band_index(sc, nx, ny);
+                const uint4 *rn = res_at(A.cur, nidx);
+                const float pn = asf(rn[6].x);
+                if (gdecode(A.gbuf[nidx]).valid && rn[5].w >= 2u && pn > 0.0f) {
+                    const float2 F = A.jres[pix * A.jpp + 2u * m];
+                    if (F.y > 0.0f) {
+                        const float cn = (float)rn[7].y, qn = asf(rn[6].y), Wn = asf(rn[7].x);
+                        const float J = qn / F.y;
+                        const float pb = pn / J;
+                        const float den = cc * F.x + Mf * cn * pb;
+                        const float mw = den > 0.0f ? (cn * pb) / den : 0.0f;
+                        wn = mw * F.x * Wn * J;
+                        pf = F.x;
+                        qf = F.y;
+                    }
+                }
+            }
+            if (wrs_update(w_sum, wn, seed)) { src = nidx; p_sel = pf; q_sel = qf; }
+        }
+        write_reused(out, res_at(A.cur, src), p_sel, q_sel, w_sum, Csum);
+    }
+}
+
+// ---------------------------------------------------------------- host side
+// Logic round 0 creates the jobs, rounds 1..kWaveRoundsReuse step them, the last round
+// combines (so round r > 0 consumes trace round r-1).
+hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,
+                            hipStream_t s) {
+    const dim3 grid(w.seg_count), blk(WB);
+    if (round == 0) {
+        if (pass_temporal) hipLaunchKernelGGL(wtemporal_start, grid, blk, 0, s, sc, w, A);
+        else hipLaunchKernelGGL(wspatial_start, grid, blk, 0, s, sc, w, A);
+    } else if (round <= kWaveRoundsReuse) {
+        hipLaunchKernelGGL(wjob_step, grid, blk, 0, s, sc, w, (uint32_t)round, A);
+    } else {
+        if (pass_temporal) hipLaunchKernelGGL(wtemporal_combine, grid, blk, 0, s, sc, w, A);
+        else hipLaunchKernelGGL(wspatial_combine, grid, blk, 0, s, sc, w, A);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace ptx

@@ -25,136 +25,11 @@
 //                   emits the next round.  Pixel state lives in HBM (SoA float4 slots).
 // Rounds: init <= 3 traces (vertices 1..3), final <= 3 (two regenerated BSDF rays + the
 // light visibility), MCPT <= 4 (primary + 3 bounces with all lights' shadow rays).
-#include "ptx_launch.h"
-#include "ptx_shading.h"
+#include "ptx_wave_common.h"
 
 #include <cstdlib>
 
 namespace ptx {
-
-constexpr uint32_t WB = kBlock;
-#ifndef LOGIC_WAVES
-#define LOGIC_WAVES 4  // start/step kernels: <=128 VGPRs, 4 waves/SIMD, no spill (5 spills)
-#endif
-enum : uint32_t { Q_CLOSEST = 0u, Q_VIS = 1u };
-
-// ---------------------------------------------------------------- wave helpers
-// Exclusive prefix sum of `v` over the wave and the wave total.
-__device__ __forceinline__ uint32_t wave_scan(uint32_t v, uint32_t &total) {
-    const uint32_t lane = __lane_id();
-    uint32_t incl = v;
-    for (uint32_t o = 1u; o < 64u; o <<= 1) {
-        uint32_t t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
-    total = __shfl(incl, 63);
-    return incl - v;
-}
-// Reserve `n` consecutive slots of this workgroup's segment (one LDS atomic per wave).
-// Must be reached by every lane of the wave.
-__device__ __forceinline__ uint32_t wave_alloc(uint32_t *lds_ctr, uint32_t n) {
-    uint32_t total;
-    const uint32_t excl = wave_scan(n, total);
-    uint32_t base = 0u;
-    if (__lane_id() == 0u && total) base = atomicAdd(lds_ctr, total);
-    base = __shfl(base, 0);
-    return base + excl;
-}
-
-// This workgroup's view of one logic round: its segments of the queues and LDS counters.
-struct Seg {
-    uint32_t j, round;
-    uint32_t rbase;            // first ray slot of the segment
-    float4 *rays, *res_out;    // rays emitted this round + their result/payload slots
-    const float4 *res_in;      // results of the previous trace round
-    uint32_t *act_out;         // active list written this round (segment-local)
-    const uint32_t *act_in;    // active list of the previous round
-    uint32_t n_in;             // its length
-    uint32_t *l_ray, *l_act;   // LDS counters
-};
-__device__ __forceinline__ Seg seg_begin(const WaveBufs &w, uint32_t round, uint32_t *lds) {
-    Seg g;
-    g.j = w.seg_base + blockIdx.x;
-    g.round = round;
-    g.rbase = g.j * w.ray_stride;
-    g.rays = w.rays;
-    g.res_out = w.res[round & 1u];
-    g.res_in = w.res[(round + 1u) & 1u];
-    g.act_out = w.act[round & 1u] + (size_t)g.j * w.seg_px;
-    g.act_in = w.act[(round + 1u) & 1u] + (size_t)g.j * w.seg_px;
-    g.n_in = round ? w.cnt[(2u * (round - 1u)) * w.nseg + g.j] : 0u;
-    g.l_ray = lds;
-    g.l_act = lds + 1;
-    if (threadIdx.x == 0) { lds[0] = 0u; lds[1] = 0u; }
-    __syncthreads();
-    return g;
-}
-__device__ __forceinline__ void seg_end(const WaveBufs &w, const Seg &g) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        w.cnt[(2u * g.round) * w.nseg + g.j] = *g.l_act;
-        w.cnt[(2u * g.round + 1u) * w.nseg + g.j] = *g.l_ray;
-    }
-}
-// Padded pixel handled by this thread at offset k of segment j.  A segment is seg_px/64
-// 8x8 tiles spread over the whole band (tile j + t * nseg, cluster 1): each wave still
-// shades one coherent tile, while every segment -- and so every trace workgroup -- sees a
-// sample of the whole image, which keeps the per-segment trace cost even.  Measured at
-// 1080p: spreading beats clustering adjacent tiles (cluster 4: -5 %, 16: -33 %), and
-// 512-pixel segments beat 1024 (+1-3 %), 256 (-9 %) and 2048 (-11 %).
-__device__ __forceinline__ uint32_t seg_pixel(const WaveBufs &w, uint32_t j, uint32_t k) {
-    const uint32_t s = (k + threadIdx.x) >> 6;  // tile slot within the segment (seg_px / 64)
-    const uint32_t cl = w.cluster;              // runs of `cl` adjacent tiles
-    const uint32_t t = ((s / cl) * w.nseg + j) * cl + s % cl;
-    return t * 64u + (threadIdx.x & 63u);
-}
-// append the active pixel to this round's list (all lanes)
-__device__ __forceinline__ void seg_keep(const Seg &g, bool keep, uint32_t pix) {
-    const uint32_t slot = wave_alloc(g.l_act, keep ? 1u : 0u);
-    if (keep) g.act_out[slot] = pix;
-}
-
-__device__ __forceinline__ void put_ray(float4 *rays, uint32_t idx, f3 o, f3 d, float remain, uint32_t kind) {
-    rays[2u * idx] = make_float4(o.x, o.y, o.z, remain);
-    rays[2u * idx + 1u] = make_float4(d.x, d.y, d.z, asf(kind));
-}
-__device__ __forceinline__ Hit get_hit(const float4 *res, uint32_t idx) {
-    const float4 a = res[2u * idx], b = res[2u * idx + 1u];
-    const uint32_t enc = asu(a.y);
-    Hit h;
-    h.valid = (enc >> 31) != 0u;
-    h.t = a.x;
-    h.s = Compact{enc >> 31, (enc >> 16) & 0x7fffu, enc & 0xffffu, asu(a.z), a.w, b.x};
-    h.pos = mk(b.y, b.z, b.w);
-    return h;
-}
-__device__ __forceinline__ f3 x0_of(const Scene &sc, uint32_t x, uint32_t y) {  // Get_X0, PT_1:732-738
-    const float *vpinv = reinterpret_cast<const float *>(sc.U + U_VPINV);
-    float u = ((float)x + 0.5f) / (float)sc.U[U_W];
-    float v = ((float)y + 0.5f) / (float)sc.U[U_H];
-    return xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
-}
-__device__ __forceinline__ Compact gdecode(uint4 g) {
-    return Compact{(g.x & 0x80000000u) ? 1u : 0u, (g.x & 0x7fff0000u) >> 16, g.x & 0xffffu, g.y, asf(g.z), asf(g.w)};
-}
-__device__ __forceinline__ uint4 gencode(const Compact &s) {
-    return make_uint4((s.valid << 31) | (s.inst << 16) | s.mat, s.prim, asu(s.bu), asu(s.bv));
-}
-__device__ __forceinline__ void mix_color(const Scene &sc, float4 *accum, uint32_t i, f3 c) {
-    float t = 1.0f / (float)(sc.U[U_FRAME] + 1u);  // WriteColor, PT_4:599-606
-    float4 a = accum[i];
-    accum[i] = make_float4(mixf(a.x, c.x, t), mixf(a.y, c.y, t), mixf(a.z, c.z, t), 1.0f);
-}
-// pixel -> (x, y) for the start kernels: 8x8 tiles so a wave's first rays are coherent
-__device__ __forceinline__ bool tile_xy(const Scene &sc, uint32_t p, uint32_t &x, uint32_t &y) {
-    const uint32_t tiles_x = (sc.width + 7u) / 8u, t = p >> 6, l = p & 63u;
-    x = (t % tiles_x) * 8u + (l & 7u);
-    y = sc.row_begin + (t / tiles_x) * 8u + (l >> 3);
-    return x < sc.width && y < sc.row_end;
-}
-__device__ __forceinline__ uint32_t padded_pixels(const Scene &sc) {
-    return ((sc.width + 7u) / 8u) * ((sc.row_end - sc.row_begin + 7u) / 8u) * 64u;
-}
 
 // ---------------------------------------------------------------- trace queue
 // Workgroup j traces ray segment j of `round`.  A Visibility query is traced with its
@@ -700,17 +575,6 @@ struct WFinal {
     Surface cur;
     f3 prev;
 };
-__device__ __forceinline__ LightSample load_xl(const uint4 *res) {
-    const uint4 r1 = res[1], r2 = res[2], r3 = res[3];
-    LightSample XL;
-    XL.dir = mk(asf(r1.x), asf(r1.y), asf(r1.z));
-    XL.type = r1.w;
-    XL.pos = mk(asf(r2.x), asf(r2.y), asf(r2.z));
-    XL.id = (int32_t)r2.w;
-    XL.Le = mk(asf(r3.x), asf(r3.y), asf(r3.z));
-    XL.pdf = asf(r3.w);
-    return XL;
-}
 // Either the next RegeneratePath BSDF ray or the light segment's Visibility ray.
 // Called by every lane of the wave; `emit` selects the lanes with a ray.
 __device__ __forceinline__ void wfinal_emit(const Scene &sc, const Seg &g, bool emit, WFinal &s, const uint4 *resv) {

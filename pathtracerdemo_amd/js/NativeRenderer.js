@@ -20,9 +20,10 @@ const { mat4 } = require('./wgpu_math');
 
 const addon = require(path.join(__dirname, '..', 'ptx_node.node'));
 
-const PIPELINE = { restir: 0, mcpt: 1 };
-const PASS = { GBUFFER: 0, INIT: 1, FINAL: 2, MCPT: 3, TRACE: 4, WAVE_TRACE: 5, WAVE_LOGIC: 6 };
-const BUF = { GBUFFER: 0, RESERVOIR: 1, ACCUM: 2, COUNTERS: 3 };
+const PIPELINE = { restir: 0, mcpt: 1, reuse: 2 };
+const PASS = { GBUFFER: 0, INIT: 1, FINAL: 2, MCPT: 3, TRACE: 4, WAVE_TRACE: 5, WAVE_LOGIC: 6, FRAME: 7,
+  TEMPORAL: 8, SPATIAL: 9, PASS_GROUP: 10 };
+const BUF = { GBUFFER: 0, RESERVOIR: 1, ACCUM: 2, COUNTERS: 3, RESERVOIR_HIST: 4 };
 const FLAGS = { COUNT_WORK: 1, SIMPLE_KERNELS: 2, PERSISTENT_LANES: 4, TILED_EXCHANGE: 8, TIME_LAUNCHES: 16 };
 const UNIFORM_WORDS = 33;
 
@@ -52,7 +53,8 @@ class NativeRenderer {
   /**
    * @param {number} width  image width (Canvas.width in the reference)
    * @param {number} height image height
-   * @param {object} [options] {pipeline: 'restir'|'mcpt', device, rowBegin, rowEnd, flags}
+   * @param {object} [options] {pipeline: 'restir'|'mcpt'|'reuse', device, rowBegin, rowEnd, flags,
+   *   reuseRadius, reuseNeighbors, temporalCap}
    */
   constructor(width, height, options = {}) {
     this.Width = width;
@@ -65,6 +67,8 @@ class NativeRenderer {
       width, height, rowBegin: this.RowBegin, rowEnd: this.RowEnd,
       device: options.device === undefined ? -1 : options.device,
       pipeline: PIPELINE[this.Pipeline], flags: options.flags || 0,
+      reuseRadius: options.reuseRadius || 0, reuseNeighbors: options.reuseNeighbors || 0,
+      temporalCap: options.temporalCap || 0,
     });
     this.World = null;
     this.Camera = null;

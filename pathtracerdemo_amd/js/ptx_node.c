@@ -115,7 +115,8 @@ static napi_value js_abi_version(napi_env env, napi_callback_info info) {
     return r;
 }
 
-/* create({width, height, rowBegin, rowEnd, device, pipeline, flags}) -> handle */
+/* create({width, height, rowBegin, rowEnd, device, pipeline, flags, reuseRadius, reuseNeighbors,
+ *         temporalCap}) -> handle */
 static napi_value js_create(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1];
@@ -131,7 +132,10 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
         get_u32_prop(env, argv[0], "rowBegin", 0, &cfg.row_begin) ||
         get_u32_prop(env, argv[0], "rowEnd", 0, &cfg.row_end) || get_u32_prop(env, argv[0], "device", dev, &dev) ||
         get_u32_prop(env, argv[0], "pipeline", PTX_PIPELINE_RESTIR, &cfg.pipeline) ||
-        get_u32_prop(env, argv[0], "flags", 0, &cfg.flags)) {
+        get_u32_prop(env, argv[0], "flags", 0, &cfg.flags) ||
+        get_u32_prop(env, argv[0], "reuseRadius", 0, &cfg.reuse_radius) ||
+        get_u32_prop(env, argv[0], "reuseNeighbors", 0, &cfg.reuse_neighbors) ||
+        get_u32_prop(env, argv[0], "temporalCap", 0, &cfg.temporal_cap)) {
         napi_throw_type_error(env, NULL, "create: config fields must be integers");
         return NULL;
     }
@@ -328,6 +332,35 @@ static napi_value js_run_pass(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
+/* runPasses(h, [pass, ...]) -- one overlapped launch sequence (ptx_run_passes) */
+static napi_value js_run_passes(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    bool is_array = false;
+    uint32_t n = 0;
+    if (argc < 2 || napi_is_array(env, argv[1], &is_array) != napi_ok || !is_array ||
+        napi_get_array_length(env, argv[1], &n) != napi_ok || n > 8) {
+        napi_throw_type_error(env, NULL, "runPasses(h, passes) needs an array of at most 8 passes");
+        return NULL;
+    }
+    int passes[8];
+    for (uint32_t i = 0; i < n; ++i) {
+        napi_value e;
+        int32_t p = -1;
+        if (napi_get_element(env, argv[1], i, &e) != napi_ok || napi_get_value_int32(env, e, &p) != napi_ok) {
+            napi_throw_type_error(env, NULL, "runPasses: passes must be integers");
+            return NULL;
+        }
+        passes[i] = p;
+    }
+    int rc = ptx_run_passes(H->h, passes, (int)n);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_run_passes");
+    return NULL;
+}
+
 /* read/writeBuffer(h, which, TypedArray) -- byte count = the array's byte length */
 static napi_value buffer_io(napi_env env, napi_callback_info info, int write) {
     size_t argc = 3;
@@ -372,7 +405,8 @@ static napi_value js_trace(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
-/* getStats(h) -> {frames, kernelMsTotal[8], kernelLaunches[8], triangles, bvhNodes, instances, maxBvhDepth, deviceBytes} */
+/* getStats(h) -> {frames, kernelMsTotal[16], kernelLaunches[16], triangles, bvhNodes, instances, maxBvhDepth,
+ *                 deviceBytes} */
 static napi_value js_get_stats(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1];
@@ -384,9 +418,10 @@ static napi_value js_get_stats(napi_env env, napi_callback_info info) {
     if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_get_stats");
     napi_value o, v, ms, la;
     CHECK_NAPI(env, napi_create_object(env, &o));
-    CHECK_NAPI(env, napi_create_array_with_length(env, 8, &ms));
-    CHECK_NAPI(env, napi_create_array_with_length(env, 8, &la));
-    for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t nslots = (uint32_t)(sizeof st.kernel_launches / sizeof st.kernel_launches[0]);
+    CHECK_NAPI(env, napi_create_array_with_length(env, nslots, &ms));
+    CHECK_NAPI(env, napi_create_array_with_length(env, nslots, &la));
+    for (uint32_t i = 0; i < nslots; ++i) {
         napi_create_double(env, st.kernel_ms_total[i], &v);
         napi_set_element(env, ms, i, v);
         napi_create_double(env, (double)st.kernel_launches[i], &v);
@@ -447,7 +482,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"abiVersion", js_abi_version},     {"create", js_create},
         {"uploadScene", js_upload_scene},   {"setFrame", js_set_frame},
         {"render", js_render},              {"renderAsync", js_render_async},
-        {"runPass", js_run_pass},           {"resetAccumulation", js_reset_accumulation},
+        {"runPass", js_run_pass},           {"runPasses", js_run_passes},           {"resetAccumulation", js_reset_accumulation},
         {"synchronize", js_synchronize},    {"getStats", js_get_stats},
         {"resetStats", js_reset_stats},     {"readBuffer", js_read_buffer},
         {"writeBuffer", js_write_buffer},   {"trace", js_trace},

@@ -4,7 +4,8 @@ Same surface and semantics as ``Renderer`` of apps/frontend/src/graphics-core/
 Renderer_TEST.ts (constructor :83-126, GetCamera :129-132, ResetFrameCount :134-137,
 Initialize :141-163, Update :165-206, Render :208-261), with the WebGPU device replaced
 by libptx.so on one MI355X.  ``pipeline="mcpt"`` mirrors the legacy Renderer.ts
-(TEST_MCPT.wgsl brute force, GC/Renderer.ts:536-647).
+(TEST_MCPT.wgsl brute force, GC/Renderer.ts:536-647); ``pipeline="reuse"`` adds the
+build-defined temporal + spatial reuse passes between PT_1 and PT_4.
 """
 from __future__ import annotations
 
@@ -20,13 +21,15 @@ from .scene.world import CompiledScene, World, serialize_world
 class Renderer:
     def __init__(self, width: int, height: int, device: int = -1, pipeline: str = "restir",
                  row_begin: int = 0, row_end: int = 0, count_work: bool = False, variant: str = "wave",
-                 time_launches: bool = False, single_stream: bool = False):
+                 time_launches: bool = False, single_stream: bool = False, reuse_radius: int = 0,
+                 reuse_neighbors: int = 0, temporal_cap: int = 0):
         self._lib = N.load()
         self.width, self.height = int(width), int(height)
         self.pipeline = pipeline
         cfg = N.PtxConfig(width=self.width, height=self.height, row_begin=row_begin, row_end=row_end,
                           device=device,
-                          pipeline=N.PTX_PIPELINE_MCPT if pipeline == "mcpt" else N.PTX_PIPELINE_RESTIR,
+                          pipeline=N.PIPELINES[pipeline], reuse_radius=reuse_radius,
+                          reuse_neighbors=reuse_neighbors, temporal_cap=temporal_cap,
                           flags=(N.PTX_FLAG_COUNT_WORK if count_work else 0) | N.VARIANT_FLAGS[variant]
                           | (N.PTX_FLAG_TIME_LAUNCHES if time_launches else 0)
                           | (N.PTX_FLAG_SINGLE_STREAM if single_stream else 0))
@@ -79,6 +82,27 @@ class Renderer:
 
     def run_pass(self, pass_id: int) -> None:
         self._call("ptx_run_pass", self._h, pass_id)
+
+    def run_passes(self, passes) -> None:
+        """Several passes as one overlapped launch sequence (include/ptx.h ptx_run_passes)."""
+        arr = (ctypes.c_int * len(passes))(*passes)
+        self._call("ptx_run_passes", self._h, arr, len(passes))
+
+    def halo_rows(self):
+        """(rows above, rows below, bytes per halo row) of a reuse band (ptx_halo_rows)."""
+        t, b, n = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_size_t()
+        self._call("ptx_halo_rows", self._h, ctypes.byref(t), ctypes.byref(b), ctypes.byref(n))
+        return int(t.value), int(b.value), int(n.value)
+
+    def halo_pack(self, dev_top: int | None, dev_bottom: int | None) -> None:
+        self._call("ptx_halo_pack", self._h, dev_top, dev_bottom)
+
+    def halo_unpack(self, dev_top: int | None, dev_bottom: int | None) -> None:
+        self._call("ptx_halo_unpack", self._h, dev_top, dev_bottom)
+
+    def read_history(self) -> np.ndarray:
+        """The reuse pipeline's spatial output (PT_4's input, next frame's history)."""
+        return self._read(N.PTX_BUF_RESERVOIR_HIST, np.uint32, 32)
 
     def synchronize(self) -> None:
         self._call("ptx_synchronize", self._h)

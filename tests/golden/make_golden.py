@@ -22,6 +22,7 @@ from oracle import oracle as O  # noqa: E402
 from pathtracerdemo_amd.scene.world import compile_scene  # noqa: E402
 
 W, H = 24, 24
+REUSE_FRAMES = 3
 
 
 # (scene, frames) -> fixture file; C3 is the build-defined many-light interior (scenes/make_c3.py)
@@ -44,8 +45,15 @@ def frame_fixture(cs, frames):
         fr.run(O.PASS_RESTIR, threads=1)
     mc = O.Frame(uniform_for(cs, W, H, 1), cs.scene, cs.geometry, cs.accel)
     mc.run(O.PASS_MCPT, threads=1)
+    # the build-defined reuse pipeline, default parameters, 3 frames
+    ru = O.Frame(uniform_for(cs, W, H, 1), cs.scene, cs.geometry, cs.accel)
+    for f in range(1, REUSE_FRAMES + 1):
+        ru.set_frame_index(f)
+        ru.run_reuse_frame(threads=1)
     return dict(uniform=fr.uniform, gbuffer=fr.gbuffer, reservoir=fr.reservoir, accum_restir=fr.accum,
-                accum_mcpt=mc.accum, frames=np.int32(frames), scene_sha256=scene_digest(cs))
+                accum_mcpt=mc.accum, frames=np.int32(frames), scene_sha256=scene_digest(cs),
+                accum_reuse=ru.accum, hist_reuse=ru.res_hist, reuse_frames=np.int32(REUSE_FRAMES),
+                reuse_params=np.array(ru.reuse, dtype=np.int32))
 
 
 def kat_table():

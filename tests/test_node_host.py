@@ -21,7 +21,7 @@ NODE = shutil.which("node")
 ADDON = os.path.join(ROOT, "pathtracerdemo_amd", "ptx_node.node")
 pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 
-EXPORTS = ["abiVersion", "create", "uploadScene", "setFrame", "render", "renderAsync", "runPass",
+EXPORTS = ["abiVersion", "create", "uploadScene", "setFrame", "render", "renderAsync", "runPass", "runPasses",
            "resetAccumulation", "synchronize", "getStats", "resetStats", "readBuffer", "writeBuffer",
            "trace", "destroy", "lastError"]
 
@@ -47,7 +47,7 @@ def test_addon_exports_the_abi():
     assert out.returncode == 0, out.stderr
     keys, abi = json.loads(out.stdout)
     assert sorted(keys) == sorted(EXPORTS)
-    assert abi == 1
+    assert abi == 2
 
 
 def test_js_uniform_matches_python_host(scene1, scene_dir):
