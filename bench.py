@@ -214,7 +214,7 @@ def main():
     prof = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(prof):
         try:
-            entry = json.load(open(prof)).get(f"{pipeline}:{dom}:{W}x{Hb}")
+            entry = json.load(open(prof)).get(f"{pipeline}:{args.scene}:{dom}:{W}x{Hb}")
             traffic = entry["bytes_per_launch"] if isinstance(entry, dict) else entry
         except Exception:
             traffic = None

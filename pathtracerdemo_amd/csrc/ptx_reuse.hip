@@ -197,9 +197,9 @@ __device__ __forceinline__ bool wrs_update(float &w_sum, float wt, uint32_t &see
 }
 __device__ __forceinline__ void write_reused(uint4 *out, const uint4 *src, float p_sel, float q_sel, float w_sum,
                                              uint32_t C) {
-    uint4 t[6];
-    for (int k = 0; k < 6; ++k) t[k] = src[k];  // src may be out itself (temporal)
-    for (int k = 0; k < 6; ++k) out[k] = t[k];
+    // all loads before the stores: src may be out itself (temporal)
+    const uint4 a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], a4 = src[4], a5 = src[5];
+    out[0] = a0; out[1] = a1; out[2] = a2; out[3] = a3; out[4] = a4; out[5] = a5;
     out[6] = make_uint4(asu(p_sel), asu(q_sel), 0u, 0u);
     out[7] = make_uint4(asu(p_sel > 0.0f ? w_sum / p_sel : 0.0f), C, 0u, 0u);
 }
@@ -276,56 +276,51 @@ __device__ __forceinline__ int32_t band_index(const Scene &sc, uint32_t x, uint3
     return ((int32_t)y - (int32_t)sc.row_begin) * (int32_t)sc.width + (int32_t)x;
 }
 
+// One thread per job: job slot 2m (+1) of a pixel = the forward (backward) shift with
+// neighbour m.  A workgroup walks its segment slot by slot, so a wave holds one 8x8 tile's
+// jobs of the same kind; the neighbour offsets are re-drawn per job (2 PCG draws each).
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
 void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, 0u, lds);
-    const uint32_t np = padded_pixels(sc), M = A.neighbors;
-    for (uint32_t k = 0; k < w.seg_px; k += WB) {
-        const uint32_t q = seg_pixel(w, g.j, k);
-        uint32_t x = 0u, y = 0u, pix = 0u, seed = 0u;
-        bool center = false, canon_ok = false;
-        Compact x1{};
+    const uint32_t np = padded_pixels(sc), jpp = A.jpp;
+    for (uint32_t base = 0; base < w.seg_px * jpp; base += WB) {  // workgroup-uniform
+        const uint32_t slot = base / w.seg_px, m = slot >> 1;
+        const bool backward = (slot & 1u) != 0u;
+        const uint32_t q = seg_pixel(w, g.j, base % w.seg_px);
+        uint32_t x, y, jid = 0u;
+        bool act = false;
+        Job s;
         if (q < np && tile_xy(sc, q, x, y)) {
-            pix = (y - sc.row_begin) * sc.width + x;
-            x1 = gdecode(A.gbuf[pix]);
-            center = x1.valid != 0u;
-            if (center) {
-                seed = reuse_seed(sc, x, y, SALT_SPATIAL);
-                const uint4 *rc = A.cur + 8u * (size_t)pix;
-                canon_ok = rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
+            const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+            jid = pix * jpp + slot;
+            const Compact x1 = gdecode(A.gbuf[pix]);
+            if (x1.valid) {
+                uint32_t seed = reuse_seed(sc, x, y, SALT_SPATIAL), nx = 0u, ny = 0u;
+                bool present = false;
+                for (uint32_t k = 0; k <= m; ++k) present = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+                const int32_t nidx = present ? band_index(sc, nx, ny) : 0;
+                Compact xn{};
+                if (present) {
+                    xn = gdecode(A.gbuf[nidx]);
+                    present = xn.valid != 0u;
+                }
+                bool want = false;
+                if (present && !backward) {  // the neighbour's sample in this pixel's domain
+                    const uint4 *rn = res_at(A.cur, nidx);
+                    want = rn[5].w >= 2u && asf(rn[6].x) > 0.0f;
+                    act = want && job_begin(sc, A, s, x, y, x1, nidx);
+                } else if (present) {  // this pixel's sample in the neighbour's domain
+                    const uint4 *rc = A.cur + 8u * (size_t)pix;
+                    want = rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
+                    act = want && job_begin(sc, A, s, nx, ny, xn, (int32_t)pix);
+                }
+                if (want && !act) A.jres[jid] = make_float2(0.0f, 0.0f);
             }
         }
-        for (uint32_t m = 0; m < M; ++m) {  // workgroup-uniform
-            uint32_t nx = 0u, ny = 0u;
-            bool present = center && spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
-            const int32_t nidx = present ? band_index(sc, nx, ny) : 0;
-            Compact xn{};
-            if (present) {
-                xn = gdecode(A.gbuf[nidx]);
-                present = xn.valid != 0u;
-            }
-            bool fwd = false, bwd = false;
-            if (present) {
-                const uint4 *rn = res_at(A.cur, nidx);
-                fwd = rn[5].w >= 2u && asf(rn[6].x) > 0.0f;
-                bwd = canon_ok;
-            }
-            const uint32_t jf = pix * A.jpp + 2u * m, jb = jf + 1u;
-            Job s;
-            // forward: the neighbour's sample in this pixel's domain
-            bool act = fwd && job_begin(sc, A, s, x, y, x1, nidx);
-            if (fwd && !act) A.jres[jf] = make_float2(0.0f, 0.0f);
-            bool live = job_emit(sc, g, A, act, s, jf);
-            if (live) job_store(A, jf, s);
-            seg_keep(g, live, jf);
-            // backward: this pixel's sample in the neighbour's domain
-            act = bwd && job_begin(sc, A, s, nx, ny, xn, (int32_t)pix);
-            if (bwd && !act) A.jres[jb] = make_float2(0.0f, 0.0f);
-            live = job_emit(sc, g, A, act, s, jb);
-            if (live) job_store(A, jb, s);
-            seg_keep(g, live, jb);
-        }
+        const bool live = job_emit(sc, g, A, act, s, jid);
+        if (live) job_store(A, jid, s);
+        seg_keep(g, live, jid);
     }
     seg_end(w, g);
 }
