@@ -69,11 +69,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal knobs for one-GPU boxes: PTX_DIST_BACKEND=gloo (host halo messages) and
+    # PTX_FORCE_DEVICE=0 (every rank on GPU 0); the real run is nccl (RCCL), one GPU per rank
+    backend = os.environ.get("PTX_DIST_BACKEND", "nccl")
+    device = int(os.environ.get("PTX_FORCE_DEVICE", local_rank))
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl")
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend=backend)
 
     from pathtracerdemo_amd.renderer import Renderer
     from pathtracerdemo_amd.scene.world import compile_scene
@@ -84,13 +88,13 @@ def main():
     cs = compile_scene(args.scene)
     row_begin, row_end = rank * Hb, (rank + 1) * Hb
     pipeline = args.workload
-    r = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
+    r = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
                  variant=args.variant)
     r.Initialize(cs)
     band_drv = None
     if pipeline == "reuse" and world > 1:
         from pathtracerdemo_amd.bands import ReuseBand
-        band_drv = ReuseBand(r, rank, world, device=f"cuda:{local_rank}")
+        band_drv = ReuseBand(r, rank, world, device=f"cuda:{device}" if backend == "nccl" else "cpu")
 
     def frame(rr, drv):
         rr.Update()
@@ -100,7 +104,7 @@ def main():
             drv.render_frame()
 
     # work census of the exact frame (counting build, untimed): algorithmic bytes
-    rc = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
+    rc = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
                   count_work=True, variant=args.variant)
     rc.Initialize(cs)
     rc.Update()
@@ -136,7 +140,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = r.stats()
@@ -151,13 +155,13 @@ def main():
     # the overlap's gain is in `value` and in roofline.frame.
     st_k = None
     if args.variant == "wave":
-        rk = Renderer(W, H, device=local_rank, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
+        rk = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
                       variant=args.variant, time_launches=True, single_stream=True)
         rk.Initialize(cs)
         drv_k = None
         if band_drv is not None:
             from pathtracerdemo_amd.bands import ReuseBand
-            drv_k = ReuseBand(rk, rank, world, device=f"cuda:{local_rank}")
+            drv_k = ReuseBand(rk, rank, world, device=f"cuda:{device}" if backend == "nccl" else "cpu")
         for _ in range(max(1, args.warmup)):
             frame(rk, drv_k)
         rk.synchronize()

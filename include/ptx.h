@@ -132,7 +132,8 @@ int ptx_run_passes(ptx_handle *h, const int *passes, int n);
  * last rows), rows_bottom from the band below.  A message is rows x W x bytes_per_row
  * (G-buffer rows, then reservoir rows).  pack copies THIS band's first rows_top / last
  * rows_bottom rows (what the neighbours need) into device buffers; unpack copies received
- * messages into the halo rows.  Both are async on the handle's stream. */
+ * messages into the halo rows.  Both are async on the handle's stream; the buffers may be
+ * device memory (RCCL) or host memory (then synchronize before reading a packed one). */
 int ptx_halo_rows(ptx_handle *h, uint32_t *rows_top, uint32_t *rows_bottom, size_t *bytes_per_row);
 int ptx_halo_pack(ptx_handle *h, void *dev_top, void *dev_bottom);
 int ptx_halo_unpack(ptx_handle *h, const void *dev_top, const void *dev_bottom);

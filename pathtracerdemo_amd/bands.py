@@ -60,7 +60,8 @@ class ReuseBand:
     def __init__(self, target, rank: int, world: int, device="cpu"):
         import torch
         self.t, self.rank, self.world = target, rank, world
-        if str(device).startswith("cuda"):  # pack -> RCCL -> unpack ordered on torch's stream
+        self.host_buffers = not str(device).startswith("cuda")
+        if not self.host_buffers:  # pack -> RCCL -> unpack ordered on torch's stream
             target.set_stream(torch.cuda.current_stream(device).cuda_stream)
         top, bottom, row_bytes = target.halo_rows()
         mk = lambda rows: torch.empty(rows * row_bytes, dtype=torch.uint8, device=device)
@@ -75,6 +76,8 @@ class ReuseBand:
         t = self.t
         t.run_passes(self.FRONT)
         t.halo_pack(self._ptr(self.send_top), self._ptr(self.send_bottom))
+        if self.host_buffers and hasattr(t, "synchronize"):
+            t.synchronize()  # host messages (gloo): the copies must land before sending
         halo_exchange(self.send_top, self.send_bottom, self.recv_top, self.recv_bottom, self.rank, self.world)
         t.halo_unpack(self._ptr(self.recv_top), self._ptr(self.recv_bottom))
         t.run_passes(self.BACK)

@@ -776,12 +776,13 @@ static int halo_copy(ptx_handle *h, uint32_t r0, uint32_t rows, void *msg, bool 
     const size_t W = h->cfg.width, gb = rows * W * 16u, rb = rows * W * 128u;
     char *g = (char *)h->d_gbuf.p + (size_t)r0 * W * 16u, *r = (char *)h->d_res.p + (size_t)r0 * W * 128u;
     char *m = (char *)msg;
+    // hipMemcpyDefault: the message may be device memory (RCCL) or host memory (gloo)
     if (to_msg) {
-        HIP_CHECK(h, hipMemcpyAsync(m, g, gb, hipMemcpyDeviceToDevice, h->stream));
-        HIP_CHECK(h, hipMemcpyAsync(m + gb, r, rb, hipMemcpyDeviceToDevice, h->stream));
+        HIP_CHECK(h, hipMemcpyAsync(m, g, gb, hipMemcpyDefault, h->stream));
+        HIP_CHECK(h, hipMemcpyAsync(m + gb, r, rb, hipMemcpyDefault, h->stream));
     } else {
-        HIP_CHECK(h, hipMemcpyAsync(g, m, gb, hipMemcpyDeviceToDevice, h->stream));
-        HIP_CHECK(h, hipMemcpyAsync(r, m + gb, rb, hipMemcpyDeviceToDevice, h->stream));
+        HIP_CHECK(h, hipMemcpyAsync(g, m, gb, hipMemcpyDefault, h->stream));
+        HIP_CHECK(h, hipMemcpyAsync(r, m + gb, rb, hipMemcpyDefault, h->stream));
     }
     return PTX_OK;
 }
