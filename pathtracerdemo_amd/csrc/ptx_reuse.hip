@@ -39,12 +39,14 @@ struct Job {
 
 __device__ __forceinline__ const uint4 *res_at(const uint4 *base, int32_t idx) { return base + 8 * (ptrdiff_t)idx; }
 
+// A job waiting for its light segment's Visibility (phase 1) only needs HDR and F.
 __device__ __forceinline__ void job_store(const ReuseArgs &A, uint32_t jid, const Job &s) {
     const size_t n = A.njobs;
     float4 *st = A.jstate;
     st[JS_HDR * n + jid] = make_float4(asf(s.i | (s.length << 8) | (s.phase << 16)), asf(s.seed1), asf(s.idx),
                                        asf((uint32_t)s.ref));
     st[JS_F * n + jid] = make_float4(s.f.x, s.f.y, s.f.z, s.prod);
+    if (s.phase != 0u) return;
     st[JS_CUR * n + jid] = make_float4(s.cur.pos.x, s.cur.pos.y, s.cur.pos.z, asf(s.matref));
     st[JS_NRM * n + jid] = make_float4(s.cur.nrm.x, s.cur.nrm.y, s.cur.nrm.z, s.beta);
     st[JS_PREV * n + jid] = make_float4(s.prev.x, s.prev.y, s.prev.z, s.rr_p);
@@ -53,12 +55,14 @@ __device__ __forceinline__ void job_store(const ReuseArgs &A, uint32_t jid, cons
 __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, uint32_t jid, Job &s) {
     const size_t n = A.njobs;
     const float4 *st = A.jstate;
-    const float4 hd = st[JS_HDR * n + jid], fv = st[JS_F * n + jid], cu = st[JS_CUR * n + jid];
-    const float4 nr = st[JS_NRM * n + jid], pv = st[JS_PREV * n + jid], rf = st[JS_RRF * n + jid];
+    const float4 hd = st[JS_HDR * n + jid], fv = st[JS_F * n + jid];
     const uint32_t hw = asu(hd.x);
     s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = hw >> 16;
     s.seed1 = asu(hd.y); s.idx = asu(hd.z); s.ref = (int32_t)asu(hd.w);
     s.f = mk(fv.x, fv.y, fv.z); s.prod = fv.w;
+    if (s.phase != 0u) return;
+    const float4 cu = st[JS_CUR * n + jid], nr = st[JS_NRM * n + jid];
+    const float4 pv = st[JS_PREV * n + jid], rf = st[JS_RRF * n + jid];
     s.matref = asu(cu.w);
     s.cur.pos = mk(cu.x, cu.y, cu.z);
     s.cur.nrm = mk(nr.x, nr.y, nr.z);

@@ -605,6 +605,7 @@ __device__ __forceinline__ void wfinal_store(float4 *state, uint32_t npix, uint3
     state[FS_HDR * npix + pix] = make_float4(asf(s.i | (s.length << 8) | (s.phase << 16)), asf(s.seed1),
                                              asf(s.idx), 0.0f);
     state[FS_F * npix + pix] = make_float4(s.f.x, s.f.y, s.f.z, s.ucw);
+    if (s.phase != 0u) return;  // waiting for the light segment: nothing else is read
     state[FS_CUR * npix + pix] = make_float4(s.cur.pos.x, s.cur.pos.y, s.cur.pos.z, asf(matref));
     state[FS_NRM * npix + pix] = make_float4(s.cur.nrm.x, s.cur.nrm.y, s.cur.nrm.z, 0.0f);
     state[FS_PREV * npix + pix] = make_float4(s.prev.x, s.prev.y, s.prev.z, 0.0f);
@@ -666,18 +667,20 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         if (q < n) {
             pix = g.act_in[q];
             const float4 hd = state[FS_HDR * npix + pix], fv = state[FS_F * npix + pix];
-            const float4 cu = state[FS_CUR * npix + pix], nr = state[FS_NRM * npix + pix];
-            const float4 pv = state[FS_PREV * npix + pix];
             const uint32_t hw = asu(hd.x);
             s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = hw >> 16;
             s.seed1 = asu(hd.y); s.idx = asu(hd.z);
             s.f = mk(fv.x, fv.y, fv.z); s.ucw = fv.w;
-            s.prev = mk(pv.x, pv.y, pv.z);
-            matref = asu(cu.w);
-            const Inst &I = sc.insts[matref >> 16];
-            s.cur.pos = mk(cu.x, cu.y, cu.z);
-            s.cur.nrm = mk(nr.x, nr.y, nr.z);
-            s.cur.mat = get_material(sc, desc_ptr(sc, I.mesh), matref & 0xffffu);
+            if (s.phase == 0u) {  // (the light-segment phase needs only HDR and F)
+                const float4 cu = state[FS_CUR * npix + pix], nr = state[FS_NRM * npix + pix];
+                const float4 pv = state[FS_PREV * npix + pix];
+                s.prev = mk(pv.x, pv.y, pv.z);
+                matref = asu(cu.w);
+                const Inst &I = sc.insts[matref >> 16];
+                s.cur.pos = mk(cu.x, cu.y, cu.z);
+                s.cur.nrm = mk(nr.x, nr.y, nr.z);
+                s.cur.mat = get_material(sc, desc_ptr(sc, I.mesh), matref & 0xffffu);
+            }
             if (s.phase == 0u) {  // regenerated vertex i+1 (PT_4:1378-1380) and f over vertex i
                 const Hit h = get_hit(res_in, s.idx);
                 const Surface next = h.valid ? surface_at(sc, h.s, h.pos) : get_surface(sc, h.s);
