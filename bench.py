@@ -222,9 +222,10 @@ def main():
             traffic = entry["bytes_per_launch"] if isinstance(entry, dict) else entry
         except Exception:
             traffic = None
-    cpu = None
+    cpu = ts_cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads)
+        ts_cpu = ts_cpu_baseline(cs, args.scene, W, Hb, args.cpu_threads)
     line = {
         "metric": "Msamples/sec at 1920x1080, 1 spp ReSTIR DI; per-pixel L2 vs WebGPU ref",
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
@@ -247,6 +248,7 @@ def main():
                                "kernel_ms": round(frame_kernel_s * 1e3, 4),
                                "frac": round(frame_bytes / frame_kernel_s / (HBM_PEAK_GBS * 1e9), 4)}},
         "cpu_baseline": cpu,
+        "ts_cpu_baseline": ts_cpu,
     }
     print(json.dumps(line))
     if dist is not None:
@@ -275,6 +277,39 @@ def cpu_baseline(cs, W, H, pipeline, threads):
     return {"value": round(nf * W * H / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{nf} full {W}x{H} frame(s) ({pipeline}, FrameIndex 1..{nf}), C oracle, {threads} pthreads",
             "seconds": round(dt, 2)}
+
+
+def ts_cpu_baseline(cs, scene, W, H, threads, rows=256):
+    """SURVEY.md §8(d)'s JS CPU tracer (pathtracerdemo_amd/js/cpu: the reference's live
+    pipeline PT_01 -> PT_1 -> PT_4 restated in JavaScript, bit-identical to the oracle) on
+    Node worker_threads: a band of `rows` rows in the middle of the frame, wall clock."""
+    import shutil
+    import subprocess
+    import tempfile
+    node = shutil.which("node")
+    if node is None:
+        return None
+    from pathtracerdemo_amd.scene.camera import Camera
+    from pathtracerdemo_amd.scene.export import export_compiled
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    cam = Camera(W, H)
+    cam.set_location(0, 0, 6)
+    u = cs.uniform(W, H, cam.view_projection_inverse(), cam.location, 1)
+    y0 = max(0, H // 2 - rows // 2)
+    y1 = min(H, y0 + rows)
+    with tempfile.TemporaryDirectory() as tmp:
+        d = export_compiled(cs, os.path.join(tmp, "scene"), scene)
+        uf = os.path.join(tmp, "u.bin")
+        np.asarray(u, dtype="<u4").tofile(uf)
+        out = subprocess.run([node, os.path.join(ROOT, "pathtracerdemo_amd", "js", "cpu", "bench_cpu.js"), d, uf,
+                              str(threads), str(y0), str(y1)], capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        return {"error": out.stderr[-300:]}
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    return {"value": round(r["msamples_per_s"], 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "language": "JavaScript (Node worker_threads, pathtracerdemo_amd/js/cpu/pt_cpu.js)",
+            "sample": f"rows {y0}..{y1} of the {W}x{H} {scene} frame, PT_01 -> PT_1 -> PT_4 (the reference's "
+                      f"live pipeline; no reuse passes), FrameIndex 1", "seconds": round(r["seconds"], 2)}
 
 
 if __name__ == "__main__":
