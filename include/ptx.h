@@ -17,6 +17,8 @@
  *   ptx_run_passes       <- a run of ComputePass.Dispatch calls (Render, :208-261)
  *   PTX_PASS_TEMPORAL / PTX_PASS_SPATIAL and ptx_halo_* <- the reuse passes the reference
  *                           only specifies (docs/theory/ReSTIR_Pipeline.md:259-462; no code)
+ *   PTX_PIPELINE_RESTIR_GI <- BASELINE configs[4], ReSTIR GI: build-defined on the reference's
+ *                           shading functions with memo.md:166-231's reconnection shift
  *
  * Conventions: every function returns 0 (PTX_OK) or a negative PTX_E* code and never
  * throws; ptx_last_error() holds the handle's last message.  Input arrays are borrowed
@@ -35,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PTX_ABI_VERSION 2
+#define PTX_ABI_VERSION 3
 
 #define PTX_OK 0
 #define PTX_E_INVALID (-1)  /* bad argument / state                  */
@@ -53,6 +55,10 @@ extern "C" {
 #define PTX_PIPELINE_RESTIR_REUSE 2 /* G-buffer -> Init -> temporal -> spatial -> Final: the
                                        build-defined reuse passes; wavefront
                                        kernels only                                        */
+#define PTX_PIPELINE_RESTIR_GI 3    /* G-buffer -> GI init (direct light + 1-bounce indirect
+                                       candidate) -> temporal -> spatial -> GI shade, on 64-byte
+                                       GI reservoirs; passes keep their
+                                       PTX_PASS_* ids (INIT, TEMPORAL, SPATIAL, FINAL)        */
 
 /* passes for ptx_run_pass */
 #define PTX_PASS_GBUFFER 0
@@ -72,11 +78,12 @@ extern "C" {
 
 /* buffers for ptx_read_buffer / ptx_write_buffer / ptx_device_pointer */
 #define PTX_BUF_GBUFFER 0    /* band_h * W * 4 u32   */
-#define PTX_BUF_RESERVOIR 1  /* band_h * W * 32 u32  */
+#define PTX_BUF_RESERVOIR 1  /* band_h * W * 32 u32 (GI pipeline: 16 u32) */
 #define PTX_BUF_ACCUM 2      /* band_h * W * 4 f32 (Scene texture: accumulated radiance) */
 #define PTX_BUF_COUNTERS 3   /* 32 u64: work counters [0..4] (PTX_FLAG_COUNT builds), diagnostics [8..) */
 #define PTX_BUF_RESERVOIR_HIST 4 /* band_h * W * 32 u32: spatial output = Final's input and the
                                     next frame's temporal history (reuse pipeline)           */
+#define PTX_BUF_DIRECT 5     /* band_h * W * 4 f32: direct light of the GI init pass (GI pipeline) */
 
 #define PTX_FLAG_COUNT_WORK 1u     /* count rays / AABB / triangle tests on device (slower)   */
 #define PTX_FLAG_SIMPLE_KERNELS 2u   /* A/B: one thread per pixel, no ray exchange            */

@@ -16,6 +16,9 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 PASS_GBUFFER, PASS_INIT, PASS_FINAL, PASS_MCPT, PASS_RESTIR = 0, 1, 2, 3, 4
 PASS_TEMPORAL, PASS_SPATIAL = 5, 6
+# ReSTIR GI passes (build-defined; pt_oracle_gi.c)
+GI_PASS_INIT, GI_PASS_TEMPORAL, GI_PASS_SPATIAL, GI_PASS_FINAL = 7, 8, 9, 10
+GI_WORDS = 16
 # build-defined reuse defaults (same as include/ptx.h)
 REUSE_RADIUS, REUSE_NEIGHBORS, TEMPORAL_CAP = 30, 3, 20
 
@@ -39,8 +42,8 @@ class Inputs(ctypes.Structure):
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "pt_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("pt_oracle.c", "pt_oracle_gi.c", "pt_oracle.h")]
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, srcs)):
         subprocess.run(["make", "-C", HERE, "liboracle.so"], check=True, capture_output=True)
     return LIB_PATH
 
@@ -60,6 +63,13 @@ def lib():
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P,
                                        ctypes.POINTER(ReuseParams), ctypes.POINTER(Counters)]
         _lib.pto_run_reuse.restype = ctypes.c_int
+        _lib.pto_run_gi.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Inputs), ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int, P, P, P, P, P, ctypes.POINTER(ReuseParams),
+                                    ctypes.POINTER(Counters)]
+        _lib.pto_run_gi.restype = ctypes.c_int
+        _lib.pto_gi_shift.argtypes = [ctypes.POINTER(Inputs), P, ctypes.c_uint32, ctypes.c_uint32, P, P]
+        _lib.pto_gi_sample_dir.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_uint32), P]
+        _lib.pto_gi_sample_dir.restype = ctypes.c_float
         _lib.pto_pcg.argtypes = [ctypes.c_uint32]
         _lib.pto_pcg.restype = ctypes.c_uint32
         _lib.pto_random.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
@@ -98,6 +108,10 @@ class Frame:
         self.res_hist = np.zeros((self.H, self.W, 32), dtype=np.uint32)  # spatial output / history
         self.hist_valid = False
         self.reuse = (REUSE_RADIUS, REUSE_NEIGHBORS, TEMPORAL_CAP)
+        # ReSTIR GI buffers: candidate / temporal reservoirs, spatial output (= history), direct light
+        self.gi_res = np.zeros((self.H, self.W, GI_WORDS), dtype=np.uint32)
+        self.gi_hist = np.zeros((self.H, self.W, GI_WORDS), dtype=np.uint32)
+        self.direct = np.zeros((self.H, self.W, 4), dtype=np.float32)
         self.counters = {}
 
     def set_frame_index(self, f: int):
@@ -152,6 +166,44 @@ class Frame:
         self.hist_valid = True
 
 
+    def _inputs(self):
+        return Inputs(self.uniform.ctypes.data, self.scene.ctypes.data, self.geometry.ctypes.data,
+                      self.accel.ctypes.data)
+
+    def run_gi(self, pass_id: int, threads: int = 0, rect=None) -> dict:
+        """One ReSTIR GI pass (GI_PASS_*) over `rect`: init writes gi_res + direct, temporal
+        updates gi_res from gi_hist, spatial writes gi_hist, final accumulates into accum."""
+        threads = threads or os.cpu_count() or 1
+        x0, y0, x1, y1 = rect if rect is not None else (0, 0, self.W, self.H)
+        r, m, cap = self.reuse
+        prm = ReuseParams(r, m, cap, 1 if self.hist_valid else 0)
+        cnt = Counters()
+        inp = self._inputs()
+        rc = lib().pto_run_gi(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
+                              _ptr(self.gi_res), _ptr(self.gi_hist), _ptr(self.direct), _ptr(self.accum),
+                              ctypes.byref(prm), ctypes.byref(cnt))
+        if rc != 0:
+            raise RuntimeError(f"oracle GI pass {pass_id} failed ({rc})")
+        self.counters[("gi", pass_id)] = cnt.as_dict()
+        return self.counters[("gi", pass_id)]
+
+    def run_gi_frame(self, threads: int = 0, rect=None) -> None:
+        """One ReSTIR GI frame: G-buffer -> GI init -> temporal -> spatial -> shade."""
+        self.run(PASS_GBUFFER, threads, rect)
+        for p in (GI_PASS_INIT, GI_PASS_TEMPORAL, GI_PASS_SPATIAL, GI_PASS_FINAL):
+            self.run_gi(p, threads, rect)
+        self.hist_valid = True
+
+    def gi_shift(self, x: int, y: int, s: np.ndarray):
+        """The GI reconnection shift of reservoir `s` (16 words) into pixel (x, y):
+        (valid, f rgb, q)."""
+        s = np.ascontiguousarray(s, dtype=np.uint32)
+        out = np.zeros(5, dtype=np.float32)
+        inp = self._inputs()
+        lib().pto_gi_shift(ctypes.byref(inp), _ptr(self.gbuffer), x, y, _ptr(s), _ptr(out))
+        return bool(out[0]), out[1:4].copy(), float(out[4])
+
+
 def pcg(seed: int) -> int:
     return int(lib().pto_pcg(seed & 0xFFFFFFFF))
 
@@ -188,6 +240,15 @@ def sample_bsdf(n, mat, v, seed: int):
     out = np.zeros(3, dtype=np.float32)
     lib().pto_sample_bsdf(*[_ptr(a) for a in args], ctypes.byref(s), _ptr(out), ctypes.byref(lobe))
     return out, int(lobe.value), int(s.value)
+
+
+def gi_sample_dir(n, mat, v, seed: int):
+    """The GI candidate sampler: (direction, pdf, next seed)."""
+    args = [np.asarray(a, dtype=np.float32) for a in (n, mat, v)]
+    s = ctypes.c_uint32(seed)
+    out = np.zeros(3, dtype=np.float32)
+    pdf = float(lib().pto_gi_sample_dir(*[_ptr(a) for a in args], ctypes.byref(s), _ptr(out)))
+    return out, pdf, int(s.value)
 
 
 def ray_triangle(o, d, p0, p1, p2, det_eps: float) -> float:

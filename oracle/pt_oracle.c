@@ -1445,3 +1445,4 @@ int pto_run_reuse(int pass, int nthreads, const pto_inputs *in, int x0, int y0, 
     if ((pass != 5 && pass != 6) || !prm || prm->neighbors > 16u) return -2;
     return run_pass(pass, nthreads, in, x0, y0, x1, y1, (uint32_t *)gbuffer, res_cur, res_hist, prm, NULL, cnt);
 }
+#include "pt_oracle_gi.c"

@@ -90,6 +90,33 @@ int pto_run_reuse(int pass, int nthreads, const pto_inputs *in, int x0, int y0, 
                   const uint32_t *gbuffer, uint32_t *res_cur, uint32_t *res_hist, const pto_reuse_params *prm,
                   pto_counters *cnt);
 
+/* ReSTIR GI (build-defined; pt_oracle_gi.c): 16-word GI reservoirs
+ * (W*H*16), per-pixel direct light (W*H*4 f32).  init writes res_cur + direct; temporal
+ * updates res_cur from res_hist; spatial reads res_cur, writes res_hist; final reads
+ * res_hist + direct and accumulates into accum. */
+#define PTO_GI_WORDS 16
+#define PTO_GI_PASS_INIT 7
+#define PTO_GI_PASS_TEMPORAL 8
+#define PTO_GI_PASS_SPATIAL 9
+#define PTO_GI_PASS_FINAL 10
+void pto_gi_init(const pto_inputs *in, const uint32_t *gbuffer, int x0, int y0, int x1, int y1, uint32_t *res,
+                 float *direct, pto_counters *cnt);
+void pto_gi_temporal(const pto_inputs *in, const uint32_t *gbuffer, uint32_t *res_cur, const uint32_t *res_hist,
+                     const pto_reuse_params *prm, int x0, int y0, int x1, int y1);
+void pto_gi_spatial(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *res_cur, uint32_t *res_out,
+                    const pto_reuse_params *prm, int x0, int y0, int x1, int y1, pto_counters *cnt);
+void pto_gi_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *res, const float *direct, int x0,
+                  int y0, int x1, int y1, float *accum);
+/* the GI reconnection shift of reservoir s into pixel (x, y): out = {valid, f.rgb, q} */
+void pto_gi_shift(const pto_inputs *in, const uint32_t *gbuffer, uint32_t x, uint32_t y, const uint32_t *s,
+                  float out[5]);
+/* the GI candidate direction (two-sided cosine lobe) on an explicit surface; returns its pdf */
+float pto_gi_sample_dir(const float n[3], const float mat[7], const float v[3], uint32_t *seed, float out_dir[3]);
+/* threaded: pass = PTO_GI_PASS_* */
+int pto_run_gi(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, const uint32_t *gbuffer,
+               uint32_t *res_cur, uint32_t *res_hist, float *direct, float *accum, const pto_reuse_params *prm,
+               pto_counters *cnt);
+
 /* Closest-hit queries, same record formats as ptx_trace (include/ptx.h):
  * rays n x 8 f32 {o, d.x | d.y, d.z, -, -}; hits n x 8 {t, flags|inst|mat, prim, bu, bv, pos}.
  * eps_mode 0 = PT_01 epsilons, 1 = PT_1/PT_4/MCPT epsilons. */

@@ -13,14 +13,16 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTX_LIB_PATH") or os.path.join(PKG_DIR, "libptx.so")
 
 PTX_OK = 0
-PTX_ABI_VERSION = 2
-PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT, PTX_PIPELINE_RESTIR_REUSE = 0, 1, 2
-PIPELINES = {"restir": PTX_PIPELINE_RESTIR, "mcpt": PTX_PIPELINE_MCPT, "reuse": PTX_PIPELINE_RESTIR_REUSE}
+PTX_ABI_VERSION = 3
+PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT, PTX_PIPELINE_RESTIR_REUSE, PTX_PIPELINE_RESTIR_GI = 0, 1, 2, 3
+PIPELINES = {"restir": PTX_PIPELINE_RESTIR, "mcpt": PTX_PIPELINE_MCPT, "reuse": PTX_PIPELINE_RESTIR_REUSE,
+             "gi": PTX_PIPELINE_RESTIR_GI}
 PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT, PTX_PASS_TRACE = 0, 1, 2, 3, 4
 PTX_PASS_TEMPORAL, PTX_PASS_SPATIAL = 8, 9
 PTX_STAT_WAVE_TRACE, PTX_STAT_WAVE_LOGIC, PTX_STAT_FRAME = 5, 6, 7  # stats-only slots (include/ptx.h)
 PTX_STAT_PASS_GROUP = 10
 PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS, PTX_BUF_RESERVOIR_HIST = 0, 1, 2, 3, 4
+PTX_BUF_DIRECT = 5
 PTX_FLAG_COUNT_WORK = 1
 PTX_FLAG_SIMPLE_KERNELS = 2
 PTX_FLAG_PERSISTENT_LANES = 4

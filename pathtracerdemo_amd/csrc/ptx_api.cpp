@@ -64,6 +64,10 @@ struct ptx_handle {
     DevBuf d_gbuf, d_res, d_accum, d_counters, d_queue;
     // reuse pipeline: spatial output / history, shift-job state and results
     DevBuf d_hist, d_jstate, d_jres;
+    // reservoir size in uint4 (8: the reference's 128-byte Reservoir; 4: the GI reservoir)
+    // and the GI pipeline's per-pixel direct light
+    uint32_t res_u4 = 8;
+    DevBuf d_direct;
     uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
     bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
     uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
@@ -125,7 +129,11 @@ static int upload(ptx_handle *h, DevBuf &b, const void *src, size_t bytes) {
 
 // first band row of the halo-extended G-buffer / reservoir allocations
 static uint4 *gbuf_band(ptx_handle *h) { return (uint4 *)h->d_gbuf.p + (size_t)h->halo_top * h->cfg.width; }
-static uint4 *res_band(ptx_handle *h) { return (uint4 *)h->d_res.p + 8u * (size_t)h->halo_top * h->cfg.width; }
+static uint4 *res_band(ptx_handle *h) { return (uint4 *)h->d_res.p + h->res_u4 * (size_t)h->halo_top * h->cfg.width; }
+// pipelines with the build-defined temporal / spatial passes (DI reuse, GI)
+static bool has_reuse(const ptx_handle *h) {
+    return h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE || h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI;
+}
 
 static inline float as_f32(uint32_t u) {
     float f;
@@ -301,7 +309,7 @@ static void resolve_event(TimedLaunch &t, ptx_handle *h) {
 static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t npix = (size_t)h->band_h * h->cfg.width;
     const uint32_t nl = h->uniform[U_LIGHT_COUNT];
-    const size_t jpp = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? 2u * h->reuse_neighbors : 1u;
+    const size_t jpp = has_reuse(h) ? 2u * h->reuse_neighbors : 1u;
     const size_t per_px = std::max<size_t>(std::max<size_t>(2u, (size_t)nl + 1u), jpp);
     const size_t padded = (size_t)((h->cfg.width + 7u) / 8u) * ((h->band_h + 7u) / 8u) * 64u;
     static const uint32_t env_px = getenv("PTX_SEG_PX") ? (uint32_t)atoi(getenv("PTX_SEG_PX")) : 0u;  // A/B
@@ -362,6 +370,7 @@ static void event_end(TimedLaunch *t, hipStream_t st) {
 
 static int reuse_buffers(ptx_handle *h) {
     const size_t njobs = (size_t)h->band_h * h->cfg.width * 2u * h->reuse_neighbors;
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) return alloc_buf(h, h->d_jres, njobs * 4u);  // ray index per job
     if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
     return alloc_buf(h, h->d_jres, njobs * 8u);
 }
@@ -381,12 +390,47 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     return A;
 }
 
+static GiArgs gi_args(ptx_handle *h) {
+    GiArgs A{};
+    A.gbuf = gbuf_band(h);
+    A.cur = res_band(h);
+    A.hist = (uint4 *)h->d_hist.p;
+    A.direct = (float4 *)h->d_direct.p;
+    A.accum = (float4 *)h->d_accum.p;
+    A.jray = (uint32_t *)h->d_jres.p;
+    A.jpp = 2u * h->reuse_neighbors;
+    A.radius = h->reuse_radius;
+    A.neighbors = h->reuse_neighbors;
+    A.cap = h->temporal_cap;
+    A.hist_valid = h->hist_valid ? 1u : 0u;
+    return A;
+}
+
 // One pass over the segments [w.seg_base, w.seg_base + w.seg_count) on stream `st`.
 static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass, hipStream_t st) {
     const uint4 *gb = gbuf_band(h);
     uint4 *res = res_band(h);
     float4 *acc = (float4 *)h->d_accum.p;
     hipError_t e = hipSuccess;  // every round rewrites all of its segment counts: no memset
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {
+        // GI passes: init = 3 logic rounds around 2 traces, spatial = start, trace, combine,
+        // temporal / final = one per-pixel launch
+        const GiArgs A = gi_args(h);
+        const int gp = pass == PTX_PASS_INIT ? 0 : pass == PTX_PASS_TEMPORAL ? 1 : pass == PTX_PASS_SPATIAL ? 2 : 3;
+        const int rounds = gp == 0 ? kWaveRoundsGiInit : gp == 2 ? kWaveRoundsGiSpatial : 0;
+        for (int r = 0; e == hipSuccess && r <= rounds; ++r) {
+            if (r > 0) {
+                TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
+                e = wave_trace(sc, w, r - 1, 1, h->stack_depth, st);
+                event_end(t, st);
+                if (e != hipSuccess) break;
+            }
+            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
+            e = wave_gi_round(sc, w, gp, r, A, st);
+            event_end(t, st);
+        }
+        return e;
+    }
     if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL) {
         const ReuseArgs A = reuse_args(h, pass);
         const WaveBufs &wj = w;
@@ -501,7 +545,7 @@ static int timed_wave_frame(ptx_handle *h) {
     resolve_event(t, h);
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
     hipError_t e;
-    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+    if (has_reuse(h)) {
         // per-pixel passes up to the temporal output, then (after every segment is done:
         // the spatial pass reads neighbours) spatial + PT_4
         if (int rc = reuse_buffers(h)) return rc;
@@ -542,8 +586,10 @@ static int timed_launch(ptx_handle *h, int pass) {
         HIP_CHECK(h, hipMemsetAsync(ctr, 0, sizeof(unsigned int), h->stream));
     WaveBufs w{};
     const bool reuse_pass = pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL;
-    if (reuse_pass && (variant != 3 || h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE))
-        return fail(h, PTX_E_INVALID, "pass %d needs the reuse pipeline (wavefront kernels)", pass);
+    if (reuse_pass && (variant != 3 || !has_reuse(h)))
+        return fail(h, PTX_E_INVALID, "pass %d needs the reuse or GI pipeline (wavefront kernels)", pass);
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI && pass == PTX_PASS_MCPT)
+        return fail(h, PTX_E_INVALID, "the GI pipeline has no MCPT pass");
     if (variant == 3 && pass != PTX_PASS_GBUFFER) {
         if (int rc = wave_buffers(h, w)) return rc;
         if (reuse_pass)
@@ -595,7 +641,8 @@ static bool buffer_view(ptx_handle *h, int which, DevBuf &v) {
     const size_t px = (size_t)h->band_h * h->cfg.width;
     switch (which) {
     case PTX_BUF_GBUFFER: v.p = gbuf_band(h); v.bytes = px * 16u; return true;
-    case PTX_BUF_RESERVOIR: v.p = res_band(h); v.bytes = px * 128u; return true;
+    case PTX_BUF_RESERVOIR: v.p = res_band(h); v.bytes = px * 16u * h->res_u4; return true;
+    case PTX_BUF_DIRECT: v = h->d_direct; return v.p != nullptr;
     case PTX_BUF_ACCUM: v = h->d_accum; return true;
     case PTX_BUF_COUNTERS: v = h->d_counters; return true;
     case PTX_BUF_RESERVOIR_HIST: v = h->d_hist; return v.p != nullptr;
@@ -611,8 +658,8 @@ int ptx_abi_version(void) { return PTX_ABI_VERSION; }
 int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!cfg || !out) return PTX_E_INVALID;
     *out = nullptr;
-    if (cfg->width == 0 || cfg->height == 0 || cfg->pipeline > PTX_PIPELINE_RESTIR_REUSE) return PTX_E_INVALID;
-    if (cfg->pipeline == PTX_PIPELINE_RESTIR_REUSE &&
+    if (cfg->width == 0 || cfg->height == 0 || cfg->pipeline > PTX_PIPELINE_RESTIR_GI) return PTX_E_INVALID;
+    if ((cfg->pipeline == PTX_PIPELINE_RESTIR_REUSE || cfg->pipeline == PTX_PIPELINE_RESTIR_GI) &&
         (cfg->flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE)))
         return PTX_E_INVALID;  // the reuse passes exist in wavefront form only
     if (cfg->reuse_neighbors > 16u) return PTX_E_INVALID;
@@ -625,7 +672,8 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
         return PTX_E_INVALID;
     }
     h->band_h = h->cfg.row_end - h->cfg.row_begin;
-    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) h->res_u4 = kGiResU4;
+    if (has_reuse(h)) {
         h->reuse_radius = h->cfg.reuse_radius ? h->cfg.reuse_radius : 30u;
         h->reuse_neighbors = h->cfg.reuse_neighbors ? h->cfg.reuse_neighbors : 3u;
         h->temporal_cap = h->cfg.temporal_cap ? h->cfg.temporal_cap : 20u;
@@ -651,10 +699,14 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     const size_t px = (size_t)h->band_h * h->cfg.width;
     const size_t px_halo = (size_t)(h->halo_top + h->band_h + h->halo_bot) * h->cfg.width;
     if (!rc) rc = alloc_buf(h, h->d_gbuf, px_halo * 16u);
-    if (!rc) rc = alloc_buf(h, h->d_res, px_halo * 128u);
-    if (!rc && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
-        rc = alloc_buf(h, h->d_hist, px * 128u);
+    if (!rc) rc = alloc_buf(h, h->d_res, px_halo * 16u * h->res_u4);
+    if (!rc && has_reuse(h)) {
+        rc = alloc_buf(h, h->d_hist, px * 16u * h->res_u4);
         if (!rc && hipMemset(h->d_hist.p, 0, h->d_hist.bytes) != hipSuccess) rc = PTX_E_HIP;
+    }
+    if (!rc && h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {
+        rc = alloc_buf(h, h->d_direct, px * 16u);
+        if (!rc && hipMemset(h->d_direct.p, 0, h->d_direct.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
     if (!rc) rc = alloc_buf(h, h->d_accum, px * 16u);
     if (!rc) rc = alloc_buf(h, h->d_counters, kCounterWords * 8u);
@@ -719,8 +771,10 @@ int ptx_run_passes(ptx_handle *h, const int *passes, int n) {
         const bool ok = p == PTX_PASS_GBUFFER || p == PTX_PASS_INIT || p == PTX_PASS_FINAL || p == PTX_PASS_MCPT ||
                         p == PTX_PASS_TEMPORAL || (p == PTX_PASS_SPATIAL && i == 0);
         if (!ok) return fail(h, PTX_E_INVALID, "ptx_run_passes: pass %d at position %d", p, i);
-        if ((p == PTX_PASS_TEMPORAL || p == PTX_PASS_SPATIAL) && h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE)
-            return fail(h, PTX_E_INVALID, "pass %d needs the reuse pipeline", p);
+        if ((p == PTX_PASS_TEMPORAL || p == PTX_PASS_SPATIAL) && !has_reuse(h))
+            return fail(h, PTX_E_INVALID, "pass %d needs the reuse or GI pipeline", p);
+        if (p == PTX_PASS_MCPT && h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI)
+            return fail(h, PTX_E_INVALID, "the GI pipeline has no MCPT pass");
     }
     const uint32_t fl = h->cfg.flags;
     if (fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE | PTX_FLAG_COUNT_WORK)) {
@@ -765,7 +819,7 @@ int ptx_halo_rows(ptx_handle *h, uint32_t *rows_top, uint32_t *rows_bottom, size
     if (!h) return PTX_E_INVALID;
     if (rows_top) *rows_top = h->halo_top;
     if (rows_bottom) *rows_bottom = h->halo_bot;
-    if (bytes_per_row) *bytes_per_row = (size_t)h->cfg.width * (16u + 128u);
+    if (bytes_per_row) *bytes_per_row = (size_t)h->cfg.width * (16u + 16u * h->res_u4);
     return PTX_OK;
 }
 
@@ -773,8 +827,8 @@ int ptx_halo_rows(ptx_handle *h, uint32_t *rows_top, uint32_t *rows_bottom, size
 // <-> one contiguous message (G-buffer rows, then reservoir rows).
 static int halo_copy(ptx_handle *h, uint32_t r0, uint32_t rows, void *msg, bool to_msg) {
     if (!rows) return PTX_OK;
-    const size_t W = h->cfg.width, gb = rows * W * 16u, rb = rows * W * 128u;
-    char *g = (char *)h->d_gbuf.p + (size_t)r0 * W * 16u, *r = (char *)h->d_res.p + (size_t)r0 * W * 128u;
+    const size_t W = h->cfg.width, rpx = 16u * h->res_u4, gb = rows * W * 16u, rb = rows * W * rpx;
+    char *g = (char *)h->d_gbuf.p + (size_t)r0 * W * 16u, *r = (char *)h->d_res.p + (size_t)r0 * W * rpx;
     char *m = (char *)msg;
     // hipMemcpyDefault: the message may be device memory (RCCL) or host memory (gloo)
     if (to_msg) {
@@ -810,7 +864,7 @@ int ptx_render(ptx_handle *h, float *rgba_out) {
         if (rc == 1)  // other variants / counting builds: pass by pass
             for (int p : {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL})
                 if ((rc = timed_launch(h, p))) return rc;
-    } else if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+    } else if (has_reuse(h)) {
         if (h->halo_top || h->halo_bot)
             return fail(h, PTX_E_INVALID, "a band of the reuse pipeline renders through ptx_run_passes + ptx_halo_*");
         int rc = timed_wave_frame(h);
@@ -857,7 +911,7 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
     out->max_bvh_depth = h->max_depth;
     out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
                         h->d_subs.bytes + h->d_insts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
-                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes;
+                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_direct.bytes;
     return PTX_OK;
 }
 
@@ -955,7 +1009,7 @@ int ptx_destroy(ptx_handle *h) {
     for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
-                      &h->d_hist, &h->d_jstate, &h->d_jres})
+                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_direct})
         free_buf(*b);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

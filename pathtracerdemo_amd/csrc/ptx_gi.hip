@@ -1,0 +1,450 @@
+// ptx_gi.hip -- ReSTIR GI (BASELINE configs[4]: 1-bounce indirect reservoirs) in wavefront form.
+//
+// Build-defined (no reference code; the rules are oracle/pt_oracle_gi.c's):
+// the reconnection shift of docs/theory/memo.md:166-231 at x2 on top of the reference's
+// GetSurface / SampleNEE / L_emit / Visibility / BSDF (SH/PT_1_InitPass.wgsl:285-1260).
+// Every reservoir, direct-light texel and pixel these kernels write is bit-identical to
+// the oracle's.
+//
+//   init      wgi_start (NEE shadow ray + candidate ray per pixel) -> trace ->
+//             wgi_step<1> (direct light; x2: NEE shadow ray from x2) -> trace -> wgi_step<2>
+//   temporal  wgi_temporal: per pixel, no rays (identity shift, stored contributions)
+//   spatial   wgis_start (2 shift jobs per neighbour, ONE occlusion ray each, the job's
+//             contribution and q riding in the ray's result slot) -> trace -> wgis_combine
+//   final     wgi_final: direct + f * W, accumulated
+// Same segment queues and trace_queue as the other passes; the shift's binary visibility
+// is the Q_OCC query kind (closest hit, any surface occludes).
+#include "ptx_wave_common.h"
+
+namespace ptx {
+
+constexpr uint32_t SALT_GI = 0x47494E49u, SALT_GI_TEMPORAL = 0x47495450u, SALT_GI_SPATIAL = 0x47495350u;
+constexpr float GI_VIS_SHORTEN = 0.999f, FLT_MAX_F = 3.402823466e38f;
+constexpr uint32_t GI_NO_RAY = 0xffffffffu;
+
+// init pixel state (SoA float4 slots of w.state)
+enum : uint32_t { GS_B1, GS_X1, GS_L1, GS_X2, GS_L2, GS_COUNT };
+static_assert(GS_COUNT <= kWaveStateSlots, "GI init state exceeds the wavefront state slots");
+
+__device__ __forceinline__ float gi_q(f3 y, const Surface &X2) {
+    const f3 r = X2.pos - y;
+    return dot(r, r) / fabsf(dot(X2.nrm, normalize(r)));
+}
+__device__ __forceinline__ f3 gi_lo(const Surface &X2, f3 V2, f3 L2, f3 lt) {
+    return (bsdf(X2, V2, L2) * lt) * fabsf(dot(X2.nrm, L2));
+}
+__device__ __forceinline__ bool gi_q_ok(float q) { return q > 0.0f && q <= FLT_MAX_F; }
+// two-sided cosine candidate direction with its exact pdf (oracle gi_sample_dir)
+__device__ __forceinline__ f3 gi_sample_dir(uint32_t &seed, const Surface &X, f3 V, float &pdf) {
+    const float T = X.mat.trans;
+    f3 N = dot(V, X.nrm) >= 0.0f ? X.nrm : -X.nrm;
+    if (rnd(seed) < T) N = -N;
+    const f3 L = tbn_mul(tbn(N), sample_cosine(seed));
+    const bool same = dot(L, X.nrm) * dot(V, X.nrm) > 0.0f;
+    pdf = ((same ? 1.0f - T : T) * fabsf(dot(X.nrm, L))) / PI_F;
+    return L;
+}
+__device__ __forceinline__ f3 ld3(const uint4 &v) { return mk(asf(v.x), asf(v.y), asf(v.z)); }
+
+// the candidate reservoir (oracle gi_init_pixel's tail): one-candidate RIS, C = 1
+__device__ __forceinline__ void gi_store_candidate(uint4 *out, uint4 x2, f3 dir, f3 lt, f3 f, float q, float pdf1) {
+    const float p_hat = luminance(f);
+    const float w_sum = pdf1 > 0.0f ? p_hat / pdf1 : 0.0f;
+    const bool ok = p_hat > 0.0f && gi_q_ok(q) && w_sum > 0.0f && w_sum <= FLT_MAX_F;
+    out[0] = x2;
+    out[1] = make_uint4(asu(dir.x), asu(dir.y), asu(dir.z), asu(ok ? w_sum / p_hat : 0.0f));
+    out[2] = make_uint4(asu(lt.x), asu(lt.y), asu(lt.z), 1u);
+    out[3] = make_uint4(asu(f.x), asu(f.y), asu(f.z), asu(q));
+}
+
+// ---------------------------------------------------------------- init
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+void wgi_start(Scene sc, WaveBufs w, GiArgs A) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    const uint32_t npix = w.npix, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, g.j, k);
+        uint32_t x, y, pix = 0u;
+        bool active = false;
+        f3 xl_pos{}, u{}, L1{}, b1{};
+        Surface X1;
+        float pdf1 = 0.0f;
+        uint32_t seed = 0u;
+        if (q < np && tile_xy(sc, q, x, y)) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            const Compact x1 = gdecode(A.gbuf[pix]);
+            if (!x1.valid) {
+                uint4 *out = A.cur + 4u * (size_t)pix;
+                for (int t = 0; t < 4; ++t) out[t] = make_uint4(0u, 0u, 0u, 0u);
+                A.direct[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            } else {
+                active = true;
+                seed = pcg(pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u) ^ SALT_GI);
+                X1 = get_surface(sc, x1);
+                const f3 V1 = normalize(x0_of(sc, x, y) - X1.pos);
+                const LightSample XL = sample_nee(sc, seed, X1, V1);
+                const f3 L = direction_to_light(X1, XL);
+                u = (l_emit<false>(XL, X1) * bsdf(X1, V1, L)) * fabsf(dot(X1.nrm, L));
+                u = XL.pdf > 0.0f ? u / XL.pdf : mk(0.0f, 0.0f, 0.0f);
+                xl_pos = XL.pos;
+                L1 = gi_sample_dir(seed, X1, V1, pdf1);
+                b1 = bsdf(X1, V1, L1) * fabsf(dot(X1.nrm, L1));
+            }
+        }
+        // two rays per active pixel: [base] the direct light's Visibility, [base+1] the candidate
+        const uint32_t base = g.rbase + wave_alloc(g.l_ray, active ? 2u : 0u);
+        if (active) {
+            const float dist = length(xl_pos - X1.pos);
+            put_ray(g.rays, base, X1.pos, (xl_pos - X1.pos) / dist, dist, Q_VIS);
+            g.res_out[2u * base] = make_float4(0.0f, u.x, u.y, u.z);
+            put_ray(g.rays, base + 1u, X1.pos, L1, -1.0f, Q_CLOSEST);
+            float4 *st = w.state;
+            st[GS_B1 * npix + pix] = make_float4(b1.x, b1.y, b1.z, pdf1);
+            st[GS_X1 * npix + pix] = make_float4(X1.pos.x, X1.pos.y, X1.pos.z, asf(seed));
+            st[GS_L1 * npix + pix] = make_float4(asf(base), L1.x, L1.y, L1.z);
+        }
+        seg_keep(g, active, pix);
+    }
+    seg_end(w, g);
+}
+
+// ROUND 1: direct light + the candidate's hit (NEE from x2 or the environment);
+// ROUND 2: x2's light Visibility -> the candidate reservoir.
+template <int ROUND>
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+void wgi_step(Scene sc, WaveBufs w, GiArgs A) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, (uint32_t)ROUND, lds);
+    const uint32_t npix = w.npix, n = g.n_in;
+    float4 *st = w.state;
+    for (uint32_t b0 = 0; b0 < n; b0 += WB) {
+        const uint32_t qi = b0 + threadIdx.x;
+        bool emit = false;
+        uint32_t pix = 0u;
+        f3 o{}, xl_pos{}, lt{};
+        if (qi < n) {
+            pix = g.act_in[qi];
+            const float4 sb = st[GS_B1 * npix + pix], sx = st[GS_X1 * npix + pix];
+            const f3 b1 = mk(sb.x, sb.y, sb.z), x1pos = mk(sx.x, sx.y, sx.z);
+            uint4 *out = A.cur + 4u * (size_t)pix;
+            if (ROUND == 1) {
+                const float4 sl = st[GS_L1 * npix + pix];
+                const uint32_t base = asu(sl.x);
+                const float4 a = g.res_in[2u * base];
+                const f3 d = mk(a.y, a.z, a.w) * a.x;
+                A.direct[pix] = make_float4(d.x, d.y, d.z, 0.0f);
+                const Hit h = get_hit(g.res_in, base + 1u);
+                if (!h.valid) {  // escapes: the environment in direction L1
+                    const f3 L1 = mk(sl.y, sl.z, sl.w);
+                    gi_store_candidate(out, make_uint4(0u, 0u, 0u, 0u), L1, mk(0.0f, 0.0f, 0.0f), b1 * ENV_C, 1.0f,
+                                       sb.w);
+                } else {
+                    uint32_t seed = asu(sx.w);
+                    const Surface X2 = surface_at(sc, h.s, h.pos);
+                    const f3 V2 = normalize(x1pos - X2.pos);
+                    const LightSample XL2 = sample_nee(sc, seed, X2, V2);
+                    const f3 L2 = direction_to_light(X2, XL2);
+                    lt = l_emit<false>(XL2, X2);
+                    lt = XL2.pdf > 0.0f ? lt / XL2.pdf : mk(0.0f, 0.0f, 0.0f);
+                    o = X2.pos;
+                    xl_pos = XL2.pos;
+                    uint4 c = gencode(h.s);
+                    c.x |= 0x80000000u;
+                    st[GS_X2 * npix + pix] = make_float4(asf(c.x), asf(c.y), asf(c.z), asf(c.w));
+                    st[GS_L2 * npix + pix] = make_float4(L2.x, L2.y, L2.z, 0.0f);
+                    emit = true;
+                }
+            } else {
+                const float4 s2 = st[GS_X2 * npix + pix], sl2 = st[GS_L2 * npix + pix];
+                const uint4 c = make_uint4(asu(s2.x), asu(s2.y), asu(s2.z), asu(s2.w));
+                const float4 a = g.res_in[2u * asu(sl2.w)];
+                const f3 ltv = mk(a.y, a.z, a.w) * a.x;
+                const f3 L2 = mk(sl2.x, sl2.y, sl2.z);
+                const Surface X2 = get_surface(sc, gdecode(c));
+                const f3 V2 = normalize(x1pos - X2.pos);
+                const f3 f = b1 * gi_lo(X2, V2, L2, ltv);
+                gi_store_candidate(out, c, L2, ltv, f, gi_q(x1pos, X2), sb.w);
+            }
+        }
+        const uint32_t idx = g.rbase + wave_alloc(g.l_ray, emit ? 1u : 0u);
+        if (emit) {
+            const float dist = length(xl_pos - o);
+            put_ray(g.rays, idx, o, (xl_pos - o) / dist, dist, Q_VIS);
+            g.res_out[2u * idx] = make_float4(0.0f, lt.x, lt.y, lt.z);
+            st[GS_L2 * npix + pix].w = asf(idx);
+        }
+        seg_keep(g, emit, pix);
+    }
+    seg_end(w, g);
+}
+
+// ---------------------------------------------------------------- temporal
+__device__ __forceinline__ uint32_t gi_seed(const Scene &sc, uint32_t x, uint32_t y, uint32_t salt) {
+    return pcg(pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u) ^ salt);
+}
+// reservoir `src`'s sample (words 0..10) with contribution f, q, W = w_sum / p_hat(f), C
+__device__ __forceinline__ void gi_write(uint4 *out, const uint4 *src, f3 f, float q, float w_sum, uint32_t C) {
+    const uint4 s0 = src[0], s1 = src[1], s2 = src[2];  // src may be out itself
+    const float p = luminance(f);
+    out[0] = s0;
+    out[1] = make_uint4(s1.x, s1.y, s1.z, asu(p > 0.0f ? w_sum / p : 0.0f));
+    out[2] = make_uint4(s2.x, s2.y, s2.z, C);
+    out[3] = make_uint4(asu(f.x), asu(f.y), asu(f.z), asu(q));
+}
+
+__global__ __launch_bounds__(WB) void wgi_temporal(Scene sc, WaveBufs w, GiArgs A) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        if (!gdecode(A.gbuf[pix]).valid) continue;
+        uint4 *cur = A.cur + 4u * (size_t)pix;
+        const uint4 *hist = A.hist + 4u * (size_t)pix;
+        uint32_t seed = gi_seed(sc, x, y, SALT_GI_TEMPORAL);
+        const uint4 c1 = cur[1], c2 = cur[2], c3 = cur[3], h1 = hist[1], h2 = hist[2], h3 = hist[3];
+        const float pc = luminance(ld3(c3)), ph = luminance(ld3(h3));
+        const bool canon_ok = c2.w != 0u && pc > 0.0f;
+        const uint32_t Cp = A.hist_valid ? min(h2.w, A.cap) : 0u;
+        const float cp = (float)Cp, tot = 1.0f + cp;
+        const bool hist_ok = Cp != 0u && ph > 0.0f;
+        const float wc = canon_ok ? (1.0f / tot) * pc * asf(c1.w) : 0.0f;
+        const float wp = hist_ok ? (cp / tot) * ph * asf(h1.w) : 0.0f;
+        float w_sum = 0.0f;
+        bool from_hist = false;
+        w_sum += wc;
+        if (rnd(seed) < wc / w_sum) from_hist = false;
+        w_sum += wp;
+        if (rnd(seed) < wp / w_sum) from_hist = true;
+        const uint4 s3 = from_hist ? h3 : c3;
+        gi_write(cur, from_hist ? hist : cur, ld3(s3), asf(s3.w), w_sum, 1u + Cp);
+    }
+}
+
+// ---------------------------------------------------------------- spatial
+__device__ __forceinline__ bool gi_neighbor(uint32_t &seed, uint32_t R, uint32_t x, uint32_t y, uint32_t W, uint32_t H,
+                                            uint32_t &nx, uint32_t &ny) {  // oracle spatial_neighbor
+    const float side = (float)(2u * R + 1u);
+    uint32_t ix = (uint32_t)(rnd(seed) * side);
+    uint32_t iy = (uint32_t)(rnd(seed) * side);
+    ix = min(ix, 2u * R);
+    iy = min(iy, 2u * R);
+    const int X = (int)x + (int)ix - (int)R, Y = (int)y + (int)iy - (int)R;
+    if (X < 0 || Y < 0 || X >= (int)W || Y >= (int)H || (ix == R && iy == R)) return false;
+    nx = (uint32_t)X;
+    ny = (uint32_t)Y;
+    return true;
+}
+__device__ __forceinline__ int32_t gi_band_index(const Scene &sc, uint32_t x, uint32_t y) {
+    return ((int32_t)y - (int32_t)sc.row_begin) * (int32_t)sc.width + (int32_t)x;
+}
+
+// The shift of GI reservoir s into domain (x, y) with hit y1, up to its occlusion query
+// (oracle gi_shift): false when no such path exists (q invalid).
+__device__ __forceinline__ bool gi_shift_begin(const Scene &sc, uint32_t x, uint32_t y, const Compact &y1,
+                                               const uint4 *s, f3 &f, float &q, f3 &o, f3 &dir, float &remain) {
+    const uint4 s0 = s[0], s1 = s[1], s2 = s[2];
+    if (!y1.valid || s2.w == 0u) return false;
+    const Surface Y = get_surface(sc, y1);
+    const f3 Vy = normalize(x0_of(sc, x, y) - Y.pos);
+    if (!(s0.x & 0x80000000u)) {
+        dir = ld3(s1);
+        f = (bsdf(Y, Vy, dir) * fabsf(dot(Y.nrm, dir))) * ENV_C;
+        q = 1.0f;
+        remain = FLT_MAX_F;
+    } else {
+        const Surface X2 = get_surface(sc, gdecode(s0));
+        const f3 r = X2.pos - Y.pos;
+        const float dist = length(r);
+        dir = r / dist;
+        const f3 V2 = normalize(Y.pos - X2.pos);
+        f = (bsdf(Y, Vy, dir) * fabsf(dot(Y.nrm, dir))) * gi_lo(X2, V2, ld3(s1), ld3(s2));
+        q = gi_q(Y.pos, X2);
+        remain = dist * GI_VIS_SHORTEN;
+    }
+    o = Y.pos;
+    return gi_q_ok(q);
+}
+
+// One thread per job (slot 2m: neighbour m's sample -> this pixel, 2m+1: this pixel's
+// sample -> neighbour m); the job's contribution and q ride in its ray's result slot.
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+void wgis_start(Scene sc, WaveBufs w, GiArgs A) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    const uint32_t np = padded_pixels(sc), jpp = A.jpp;
+    for (uint32_t base = 0; base < w.seg_px * jpp; base += WB) {  // workgroup-uniform
+        const uint32_t slot = base / w.seg_px, m = slot >> 1;
+        const bool backward = (slot & 1u) != 0u;
+        const uint32_t q = seg_pixel(w, g.j, base % w.seg_px);
+        uint32_t x, y, jid = 0u;
+        bool ray = false, job = false;
+        f3 f{}, o{}, dir{};
+        float qv = 0.0f, remain = 0.0f;
+        if (q < np && tile_xy(sc, q, x, y)) {
+            const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+            jid = pix * jpp + slot;
+            const Compact x1 = gdecode(A.gbuf[pix]);
+            if (x1.valid) {
+                job = true;
+                uint32_t seed = gi_seed(sc, x, y, SALT_GI_SPATIAL), nx = 0u, ny = 0u;
+                bool present = false;
+                for (uint32_t kk = 0; kk <= m; ++kk) present = gi_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+                const int32_t nidx = present ? gi_band_index(sc, nx, ny) : 0;
+                Compact xn{};
+                if (present) {
+                    xn = gdecode(A.gbuf[nidx]);
+                    present = xn.valid != 0u;
+                }
+                if (present && !backward) {
+                    const uint4 *rn = A.cur + 4 * (ptrdiff_t)nidx;
+                    if (luminance(ld3(rn[3])) > 0.0f) ray = gi_shift_begin(sc, x, y, x1, rn, f, qv, o, dir, remain);
+                } else if (present) {
+                    const uint4 *rc = A.cur + 4u * (size_t)pix;
+                    if (rc[2].w != 0u && luminance(ld3(rc[3])) > 0.0f)
+                        ray = gi_shift_begin(sc, nx, ny, xn, rc, f, qv, o, dir, remain);
+                }
+            }
+        }
+        const uint32_t idx = g.rbase + wave_alloc(g.l_ray, ray ? 1u : 0u);
+        if (ray) {
+            put_ray(g.rays, idx, o, dir, remain, Q_OCC);
+            g.res_out[2u * idx] = make_float4(0.0f, f.x, f.y, f.z);
+            g.res_out[2u * idx + 1u] = make_float4(qv, 0.0f, 0.0f, 0.0f);
+        }
+        if (job) A.jray[jid] = ray ? idx : GI_NO_RAY;
+    }
+    seg_end(w, g);
+}
+
+// a job's result: valid, contribution (visibility applied), q
+__device__ __forceinline__ bool gi_job(const GiArgs &A, const float4 *res, uint32_t jid, f3 &f, float &q) {
+    const uint32_t idx = A.jray[jid];
+    if (idx == GI_NO_RAY) return false;
+    const float4 a = res[2u * idx], b = res[2u * idx + 1u];
+    f = mk(a.y, a.z, a.w) * a.x;
+    q = b.x;
+    return true;
+}
+
+// Pairwise-MIS resampling (oracle gi_spatial_pixel); res = trace round 0's results.
+__global__ __launch_bounds__(WB) void wgis_combine(Scene sc, WaveBufs w, GiArgs A) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc), M = A.neighbors;
+    const float4 *res = w.res[0];
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        uint4 *out = A.hist + 4u * (size_t)pix;
+        if (!gdecode(A.gbuf[pix]).valid) {
+            for (int t = 0; t < 4; ++t) out[t] = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
+        const uint4 *rc = A.cur + 4u * (size_t)pix;
+        const uint4 c1 = rc[1], c2 = rc[2], c3 = rc[3];
+        const float Mf = (float)M, cc = (float)c2.w;
+        const f3 fcv = ld3(c3);
+        const float pc = luminance(fcv), qc = asf(c3.w), Wc = asf(c1.w);
+        const bool canon_ok = c2.w != 0u && pc > 0.0f;
+        const uint32_t seed0 = gi_seed(sc, x, y, SALT_GI_SPATIAL);
+        uint32_t seed = seed0, Csum = c2.w;
+        float sumQ = 0.0f;
+        for (uint32_t m = 0; m < M; ++m) {  // confidences + the canonical MIS weight
+            uint32_t nx = 0u, ny = 0u;
+            float Q = 1.0f;
+            if (gi_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
+                const int32_t nidx = gi_band_index(sc, nx, ny);
+                if (gdecode(A.gbuf[nidx]).valid) {
+                    const uint32_t Cn = A.cur[4 * (ptrdiff_t)nidx + 2].w;
+                    Csum += Cn;
+                    f3 B;
+                    float qB;
+                    if (canon_ok && gi_job(A, res, pix * A.jpp + 2u * m + 1u, B, qB)) {
+                        const float pbc = luminance(B) * qc / qB;
+                        const float den = cc * pc + Mf * (float)Cn * pbc;
+                        Q = den > 0.0f ? (cc * pc) / den : 1.0f;
+                    }
+                }
+            }
+            sumQ += Q;
+        }
+        const float wc = canon_ok ? (sumQ / Mf) * pc * Wc : 0.0f;
+        float w_sum = 0.0f;
+        const uint4 *src = rc;
+        f3 fsel = fcv;
+        float qsel = qc;
+        w_sum += wc;
+        if (rnd(seed) < wc / w_sum) { src = rc; fsel = fcv; qsel = qc; }
+        uint32_t nseed = seed0;
+        for (uint32_t m = 0; m < M; ++m) {
+            uint32_t nx = 0u, ny = 0u;
+            float wn = 0.0f;
+            f3 F = mk(0.0f, 0.0f, 0.0f);
+            float qF = 0.0f;
+            int32_t nidx = 0;
+            if (gi_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
+                nidx = gi_band_index(sc, nx, ny);
+                const uint4 *rn = A.cur + 4 * (ptrdiff_t)nidx;
+                const uint4 n1 = rn[1], n2 = rn[2], n3 = rn[3];
+                const float pn = luminance(ld3(n3));
+                if (gdecode(A.gbuf[nidx]).valid && pn > 0.0f && gi_job(A, res, pix * A.jpp + 2u * m, F, qF)) {
+                    const float pF = luminance(F);
+                    const float J = asf(n3.w) / qF;
+                    const float pb = pn / J;
+                    const float den = cc * pF + Mf * (float)n2.w * pb;
+                    const float mw = den > 0.0f ? ((float)n2.w * pb) / den : 0.0f;
+                    wn = mw * pF * asf(n1.w) * J;
+                } else {
+                    F = mk(0.0f, 0.0f, 0.0f);
+                    qF = 0.0f;
+                }
+            }
+            w_sum += wn;
+            if (rnd(seed) < wn / w_sum) { src = A.cur + 4 * (ptrdiff_t)nidx; fsel = F; qsel = qF; }
+        }
+        gi_write(out, src, fsel, qsel, w_sum, Csum);
+    }
+}
+
+// ---------------------------------------------------------------- final
+__global__ __launch_bounds__(WB) void wgi_final(Scene sc, WaveBufs w, GiArgs A) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        if (!gdecode(A.gbuf[pix]).valid) {
+            A.accum[pix] = make_float4(ENV_C, ENV_C, ENV_C, 1.0f);
+            continue;
+        }
+        const uint4 *r = A.hist + 4u * (size_t)pix;
+        const float4 d = A.direct[pix];
+        const f3 col = mk(d.x, d.y, d.z) + ld3(r[3]) * asf(r[1].w);
+        mix_color(sc, A.accum, pix, col);
+    }
+}
+
+// ---------------------------------------------------------------- host side
+hipError_t wave_gi_round(const Scene &sc, const WaveBufs &w, int pass, int round, const GiArgs &A, hipStream_t s) {
+    const dim3 grid(w.seg_count), blk(WB);
+    switch (pass) {
+    case 0:  // init: rounds 0, 1, 2
+        if (round == 0) hipLaunchKernelGGL(wgi_start, grid, blk, 0, s, sc, w, A);
+        else if (round == 1) hipLaunchKernelGGL(wgi_step<1>, grid, blk, 0, s, sc, w, A);
+        else hipLaunchKernelGGL(wgi_step<2>, grid, blk, 0, s, sc, w, A);
+        break;
+    case 1: hipLaunchKernelGGL(wgi_temporal, grid, blk, 0, s, sc, w, A); break;
+    case 2:  // spatial: rounds 0, 1
+        if (round == 0) hipLaunchKernelGGL(wgis_start, grid, blk, 0, s, sc, w, A);
+        else hipLaunchKernelGGL(wgis_combine, grid, blk, 0, s, sc, w, A);
+        break;
+    default: hipLaunchKernelGGL(wgi_final, grid, blk, 0, s, sc, w, A); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace ptx

@@ -87,4 +87,20 @@ struct ReuseArgs {
 hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,
                             hipStream_t s);
 
+// ReSTIR GI (ptx_gi.hip; pipeline PTX_PIPELINE_RESTIR_GI): pass 0 init (logic rounds 0..2,
+// traces between), 1 temporal (one launch), 2 spatial (start, trace, combine), 3 final.
+constexpr int kWaveRoundsGiInit = 2, kWaveRoundsGiSpatial = 1;
+constexpr uint32_t kGiResU4 = 4u;  // 64-byte GI reservoir (oracle/pt_oracle_gi.c)
+struct GiArgs {
+    const uint4 *gbuf;  // G-buffer of the band's first row; halo rows at negative / >= npix indices
+    uint4 *cur;         // GI reservoirs (init output, temporal output in place), same addressing
+    uint4 *hist;        // spatial output = final input = next frame's history (band only)
+    float4 *direct;     // per-pixel direct light (band)
+    float4 *accum;      // accumulated radiance (band)
+    uint32_t *jray;     // spatial: per job its occlusion ray's index, or 0xffffffff (no path)
+    uint32_t jpp;       // spatial jobs per pixel (2 * neighbors)
+    uint32_t radius, neighbors, cap, hist_valid;
+};
+hipError_t wave_gi_round(const Scene &sc, const WaveBufs &w, int pass, int round, const GiArgs &A, hipStream_t s);
+
 }  // namespace ptx

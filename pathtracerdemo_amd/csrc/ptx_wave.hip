@@ -53,7 +53,8 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     for (uint32_t i = threadIdx.x; i < n; i += WB) {
         const float4 a = rays[2u * i], b = rays[2u * i + 1u];
         Ray r{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)};
-        const bool vis = asu(b.w) == Q_VIS;
+        const uint32_t kind = asu(b.w);
+        const bool vis = kind != Q_CLOSEST;
         // Visibility (SH/PT_1_InitPass.wgsl:774-802) walks through transmissive hits:
         // one trace site, looped, so the traversal code is emitted once
         float T = 1.0f, remain = a.w;
@@ -69,7 +70,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
             float out = -1.0f;
             if (!h.valid || h.t > remain) out = T;
             else {
-                const float tr = get_transmission(sc, h.s.inst, h.s.mat);
+                const float tr = kind == Q_OCC ? 0.0f : get_transmission(sc, h.s.inst, h.s.mat);
                 if (tr == 0.0f) out = 0.0f;
                 else {
                     T *= tr;
@@ -113,7 +114,8 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
     uint32_t next = threadIdx.x, cur = 0u;
     bool have = false;
     Ray r{};                       // world ray of the current trace
-    bool vis = false;              // Visibility query (else closest hit)
+    bool vis = false;              // Visibility / occlusion query (else closest hit)
+    bool occ = false;              // occlusion query: every hit inside `remain` blocks
     float T = 1.0f, remain = 0.0f; // Visibility product / remaining distance
     uint32_t vit = 0u;             // Visibility segment (0..4)
     uint32_t ii = 0u, s = 0u, nsub = 0u, grp = 0u, sub_base = 0u, tri_base = 0u;
@@ -131,7 +133,8 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
             next += WB;
             const float4 a = rays[2u * cur], b = rays[2u * cur + 1u];
             r = pub ? Ray{mk(a.x, a.y, a.z), mk(a.w, b.x, b.y)} : Ray{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)};
-            vis = !pub && asu(b.w) == Q_VIS;
+            vis = !pub && asu(b.w) != Q_CLOSEST;
+            occ = !pub && asu(b.w) == Q_OCC;
             T = 1.0f;
             remain = a.w;
             vit = 0u;
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
                     float out = -1.0f;
                     if (!h.valid || h.t > remain) out = T;
                     else {
-                        const float tr = get_transmission(sc, h.s.inst, h.s.mat);
+                        const float tr = occ ? 0.0f : get_transmission(sc, h.s.inst, h.s.mat);
                         if (tr == 0.0f) out = 0.0f;
                         else {
                             T *= tr;

@@ -10,7 +10,9 @@ constexpr uint32_t WB = kBlock;
 #ifndef LOGIC_WAVES
 #define LOGIC_WAVES 4  // start/step kernels: <=128 VGPRs, 4 waves/SIMD, no spill (5 spills)
 #endif
-enum : uint32_t { Q_CLOSEST = 0u, Q_VIS = 1u };
+// query kinds of the ray queues: closest hit; Visibility (through transmissive hits, result
+// in res.x, payload kept); occlusion (any hit inside `remain` occludes: binary, payload kept)
+enum : uint32_t { Q_CLOSEST = 0u, Q_VIS = 1u, Q_OCC = 2u };
 
 // ---------------------------------------------------------------- wave helpers
 // Exclusive prefix sum of `v` over the wave and the wave total.

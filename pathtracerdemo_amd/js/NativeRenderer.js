@@ -20,7 +20,7 @@ const { mat4 } = require('./wgpu_math');
 
 const addon = require(path.join(__dirname, '..', 'ptx_node.node'));
 
-const PIPELINE = { restir: 0, mcpt: 1, reuse: 2 };
+const PIPELINE = { restir: 0, mcpt: 1, reuse: 2, gi: 3 };
 const PASS = { GBUFFER: 0, INIT: 1, FINAL: 2, MCPT: 3, TRACE: 4, WAVE_TRACE: 5, WAVE_LOGIC: 6, FRAME: 7,
   TEMPORAL: 8, SPATIAL: 9, PASS_GROUP: 10 };
 const BUF = { GBUFFER: 0, RESERVOIR: 1, ACCUM: 2, COUNTERS: 3, RESERVOIR_HIST: 4 };
@@ -53,7 +53,7 @@ class NativeRenderer {
   /**
    * @param {number} width  image width (Canvas.width in the reference)
    * @param {number} height image height
-   * @param {object} [options] {pipeline: 'restir'|'mcpt'|'reuse', device, rowBegin, rowEnd, flags,
+   * @param {object} [options] {pipeline: 'restir'|'mcpt'|'reuse'|'gi', device, rowBegin, rowEnd, flags,
    *   reuseRadius, reuseNeighbors, temporalCap}
    */
   constructor(width, height, options = {}) {

@@ -5,7 +5,8 @@ Renderer_TEST.ts (constructor :83-126, GetCamera :129-132, ResetFrameCount :134-
 Initialize :141-163, Update :165-206, Render :208-261), with the WebGPU device replaced
 by libptx.so on one MI355X.  ``pipeline="mcpt"`` mirrors the legacy Renderer.ts
 (TEST_MCPT.wgsl brute force, GC/Renderer.ts:536-647); ``pipeline="reuse"`` adds the
-build-defined temporal + spatial reuse passes between PT_1 and PT_4.
+build-defined temporal + spatial reuse passes between PT_1 and PT_4 (DESIGN.md §Reuse);
+``pipeline="gi"`` is BASELINE configs[4], ReSTIR GI.
 """
 from __future__ import annotations
 
@@ -100,9 +101,18 @@ class Renderer:
     def halo_unpack(self, dev_top: int | None, dev_bottom: int | None) -> None:
         self._call("ptx_halo_unpack", self._h, dev_top, dev_bottom)
 
+    @property
+    def reservoir_words(self) -> int:
+        """32 (the reference's 128-byte Reservoir) or 16 (the GI reservoir)."""
+        return 16 if self.pipeline == "gi" else 32
+
     def read_history(self) -> np.ndarray:
-        """The reuse pipeline's spatial output (PT_4's input, next frame's history)."""
-        return self._read(N.PTX_BUF_RESERVOIR_HIST, np.uint32, 32)
+        """The reuse / GI pipeline's spatial output (final pass input, next frame's history)."""
+        return self._read(N.PTX_BUF_RESERVOIR_HIST, np.uint32, self.reservoir_words)
+
+    def read_direct(self) -> np.ndarray:
+        """The GI init pass's direct light (band_h, W, 4) f32."""
+        return self._read(N.PTX_BUF_DIRECT, np.float32, 4)
 
     def synchronize(self) -> None:
         self._call("ptx_synchronize", self._h)
@@ -126,7 +136,7 @@ class Renderer:
         return self._read(N.PTX_BUF_GBUFFER, np.uint32, 4)
 
     def read_reservoir(self) -> np.ndarray:
-        return self._read(N.PTX_BUF_RESERVOIR, np.uint32, 32)
+        return self._read(N.PTX_BUF_RESERVOIR, np.uint32, self.reservoir_words)
 
     def write_buffer(self, which: int, arr: np.ndarray) -> None:
         arr = np.ascontiguousarray(arr)

@@ -47,7 +47,7 @@ def test_addon_exports_the_abi():
     assert out.returncode == 0, out.stderr
     keys, abi = json.loads(out.stdout)
     assert sorted(keys) == sorted(EXPORTS)
-    assert abi == 2
+    assert abi == 3
 
 
 def test_js_uniform_matches_python_host(scene1, scene_dir):
