@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--workload", choices=["reuse", "restir", "mcpt", "gi"], default="reuse")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--frame", default=None,
+                    help="strong scaling: one fixed WxH frame split into row bands over the ranks "
+                         "(configs[3]: --workload reuse --frame 3840x2160); default: weak scaling, "
+                         "every rank renders --width x --height rows of a taller frame")
     ap.add_argument("--scene", default=None, help="default: c3_interior_32 (reuse), dummy_scene_1 (others)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -94,10 +98,16 @@ def main():
     from pathtracerdemo_amd.scene.world import compile_scene
     from pathtracerdemo_amd.scene.camera import Camera
 
-    W, Hb = args.width, args.height
-    H = Hb * world
     cs = compile_scene(args.scene)
-    row_begin, row_end = rank * Hb, (rank + 1) * Hb
+    if args.frame:  # strong scaling (configs[3]): the ranks share one frame
+        from pathtracerdemo_amd.bands import band
+        W, H = (int(v) for v in args.frame.lower().split("x"))
+        row_begin, row_end = band(H, world, rank)
+        Hb = row_end - row_begin
+    else:  # weak scaling: rank r renders rows [r*Hb, (r+1)*Hb) of a W x (Hb*N) frame
+        W, Hb = args.width, args.height
+        H = Hb * world
+        row_begin, row_end = rank * Hb, (rank + 1) * Hb
     pipeline = args.workload
     r = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
                  variant=args.variant)
@@ -242,8 +252,9 @@ def main():
         "metric": "Msamples/sec at 1920x1080, 1 spp ReSTIR DI; per-pixel L2 vs WebGPU ref",
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"{args.scene} {pipeline} {W}x{Hb} per GPU, 1 spp/frame",
+        "scaling": "strong" if args.frame else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": (f"{args.scene} {pipeline} {W}x{H} split over {world} GPU(s), 1 spp/frame"
+                                if args.frame else f"{args.scene} {pipeline} {W}x{Hb} per GPU, 1 spp/frame"),
                    "pipeline": {"restir": "PT_01 gbuffer -> PT_1 init -> PT_4 final",
                                 "reuse": "PT_01 gbuffer -> PT_1 init -> temporal -> spatial (3 neighbours, "
                                          "radius 30, pairwise MIS) -> PT_4 final",

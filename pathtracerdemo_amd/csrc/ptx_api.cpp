@@ -421,7 +421,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         for (int r = 0; e == hipSuccess && r <= rounds; ++r) {
             if (r > 0) {
                 TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
-                e = wave_trace(sc, w, r - 1, 1, h->stack_depth, st);
+                e = wave_trace(sc, w, r - 1, 1, h->stack_depth, st, gp == 2);  // spatial: occlusion only
                 event_end(t, st);
                 if (e != hipSuccess) break;
             }

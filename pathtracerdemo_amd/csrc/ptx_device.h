@@ -246,7 +246,10 @@ __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, Pa
 // ROOTQ: sub-mesh roots of an instance go through one per-lane root queue (incoherent
 // secondary rays); otherwise one root at a time for the whole wave (coherent primary rays,
 // whose lanes mostly enter the same roots).  Same per-lane order and results either way.
-template <bool COUNT, bool PROF = false, bool ROOTQ = true>
+// ANY (occlusion queries): stop at the first accepted hit, position not reconstructed.
+// Until that hit the visit order -- and the bound t_max -- are the closest-hit walk's, so
+// "some hit with t <= t_max" comes out exactly when the closest hit has t <= t_max.
+template <bool COUNT, bool PROF = false, bool ROOTQ = true, bool ANY = false>
 __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *subs, const Inst *insts, Ray ray,
                                               PassEps eps, uint32_t *stack, uint32_t stride, float t_max = 1e10f) {
     Prof pf{};
@@ -258,7 +261,8 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     const float vx = 1e-4f;
     float vy = t_max;  // 1e10 in the reference; a smaller bound only prunes hits beyond it
     uint32_t n_aabb = 0, n_tri = 0;
-    for (uint32_t ii = 0; ii < sc.n_inst; ++ii) {
+    bool stop = false;
+    for (uint32_t ii = 0; ii < sc.n_inst && !stop; ++ii) {
         const Inst &I = insts[ii];
         if (PROF) pf.hit(PROF_INST);
         // TransformRayWithMat4x4(InRay, M^-1, false), SH/PT_1_InitPass.wgsl:486-496
@@ -270,14 +274,14 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
         const SubRoot *roots = subs + I.sub_base;
         const float4 *tris = sc.tris + 3u * I.tri_base;
         n_aabb += nsub;  // the reference tests every sub-mesh root once
-        for (uint32_t s0 = 0; s0 < nsub; s0 += 32u) {
+        for (uint32_t s0 = 0; s0 < nsub && !stop; s0 += 32u) {
             const uint32_t nc = nsub - s0 < 32u ? nsub - s0 : 32u;
             // Coherent pre-filter: every root against the best t at this point.  The
             // reference tests root s against the best t after roots < s (never larger), so
             // this keeps every root it enters; the exact test is repeated when the root is
             // taken below, with the then-current best -- the reference's own test.
 #pragma unroll 1
-            for (uint32_t kk = 0; kk < (ROOTQ ? 1u : nc); ++kk) {
+            for (uint32_t kk = 0; kk < (ROOTQ ? 1u : nc) && !stop; ++kk) {
             uint32_t mask = 0u;
             if (ROOTQ) {
 #pragma unroll 1
@@ -356,6 +360,11 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                     best.s.inst = ii;
                     best.s.mat = grp;
                     best.s.prim = first + k;
+                    if (ANY) break;
+                }
+                if (ANY && best.valid) {  // occluded: drop the rest of the walk
+                    stop = true;
+                    break;
                 }
             }
             }  // roots (ROOTQ: one queue per chunk of 32; else one root at a time)
@@ -376,7 +385,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     }
     if (best.valid) {
         best.t = vy;
-        complete_hit(sc, ray, eps, best);
+        if (!ANY) complete_hit(sc, ray, eps, best);
     }
     return best;
 }

@@ -62,8 +62,9 @@ struct WaveBufs {
     uint32_t act_stride; // list entries per segment (seg_px; seg_px * jobs per pixel for reuse)
     uint32_t *cnt;       // 2 * kWaveMaxRounds * nseg counts
 };
+// occ_only: every query of the round is Q_OCC (any-hit kernel instance)
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t stack_depth,
-                      hipStream_t s);
+                      hipStream_t s, bool occ_only = false);
 hipError_t wave_init_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, uint4 *reservoir,
                            hipStream_t s);
 hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, const uint4 *reservoir,

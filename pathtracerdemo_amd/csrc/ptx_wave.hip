@@ -36,7 +36,9 @@ namespace ptx {
 // hit range capped at the remaining distance to the light: Visibility only looks at the
 // closest hit when its t <= remain, and the cap leaves the visit order -- hence which of
 // several equal-t triangles wins -- unchanged for every hit inside the cap.
-template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true>
+// OCC: every query of the launch is Q_OCC (the GI shift's binary visibility): an any-hit
+// walk (trace_core_tab ANY), exact for "is there a hit with t <= remain".
+template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true, bool OCC = false>
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     extern __shared__ uint32_t wstack[];
@@ -59,8 +61,8 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         // one trace site, looped, so the traversal code is emitted once
         float T = 1.0f, remain = a.w;
         for (uint32_t it = 0u;; ++it) {
-            const Hit h = trace_core_tab<COUNT, PROF>(sc, subs, insts, r, eps, stack, WB,
-                                                      vis ? fminf(remain, 1e10f) : 1e10f);
+            const Hit h = trace_core_tab<COUNT, PROF, true, OCC>(sc, subs, insts, r, eps, stack, WB,
+                                                                 vis ? fminf(remain, 1e10f) : 1e10f);
             if (!vis) {
                 const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
                 res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
@@ -873,9 +875,19 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
 }
 
 // =========================================================================== host side
-hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t depth, hipStream_t s) {
+hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t depth, hipStream_t s,
+                      bool occ_only) {
     const PassEps eps = eps_mode == 0 ? PassEps{1e-8f, 1e-6f} : PassEps{1e-4f, 1e-8f};
     const size_t lds = stack_lds_bytes(depth);
+    if (occ_only && sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts) {  // occlusion rounds (GI spatial)
+        if (sc.counters)
+            hipLaunchKernelGGL((trace_queue<true, 6, false, true, true>), dim3(w.seg_count), dim3(WB), lds, s, sc, w,
+                               (uint32_t)round, eps);
+        else
+            hipLaunchKernelGGL((trace_queue<false, 5, false, true, true>), dim3(w.seg_count), dim3(WB), lds, s, sc, w,
+                               (uint32_t)round, eps);
+        return hipGetLastError();
+    }
     static const bool refill = getenv("PTX_TRACE_REFILL") != nullptr;  // A/B switch for profiling
     if (refill) {
         const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.nseg + w.seg_base;
