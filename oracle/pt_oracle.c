@@ -1008,11 +1008,15 @@ void pto_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *re
  *    domain, identity shift), history confidence capped at `cap`.
  *  - spatial: M neighbours in a (2R+1)^2 square, pairwise MIS with confidences.
  *  - every reservoir written by a reuse pass stores p_hat (word 24) and q (word 25) of its
- *    sample in its own domain; RNG streams are salted per pass. */
+ *    sample in its own domain; RNG streams are salted per pass.
+ *  - ... and the sample's PathContribution f there (words 26, 27, 30 = f.xyz, word 31 = 1),
+ *    when known: eval_sample's f IS PT_4's PathContribution of that reservoir at that pixel
+ *    (same replay, same products), so PT_4 of a reused reservoir equals f * UCW; the GPU
+ *    final pass uses that instead of replaying (PT_4 below still replays: the check). */
 #define SALT_TEMPORAL 0x54454D50u
 #define SALT_SPATIAL 0x53504154u
 
-typedef struct eval_out { int valid; float phat, q; } eval_out;
+typedef struct eval_out { int valid; float phat, q; v3 f; } eval_out;
 
 static inline uint32_t reuse_seed(const ctx *c, uint32_t x, uint32_t y, uint32_t salt) {
     return pto_pcg(init_seed(c, x, y) ^ salt);
@@ -1037,7 +1041,7 @@ static void rr_step(const surface *X, v3 V, v3 L, float pdf, v3 *f, float *p, fl
 /* The reservoir sample `res` replayed in the domain of pixel (x, y) with G-buffer hit x1:
  * RegeneratePath + PathContribution of PT_4:1306-1384 plus the shift's pdf product. */
 static eval_out eval_sample(const ctx *c, uint32_t x, uint32_t y, compact x1, const uint32_t *res) {
-    eval_out o = {0, 0.0f, 0.0f};
+    eval_out o = {0, 0.0f, 0.0f, {0.0f, 0.0f, 0.0f}};
     const uint32_t length = res[23];
     if (!x1.valid || res[29] == 0u || length < 2u) return o;
     light_sample XL;
@@ -1089,10 +1093,20 @@ static eval_out eval_sample(const ctx *c, uint32_t x, uint32_t y, compact x1, co
     o.valid = rr_ok && q > 0.0f && q <= 3.402823466e38f;
     o.phat = o.valid ? luminance(f) : 0.0f;
     o.q = o.valid ? q : 0.0f;
+    if (o.valid) o.f = f;
     return o;
 }
 
-static void write_reused(uint32_t *out, const uint32_t *src, float p_sel, float q_sel, float w_sum, uint32_t C) {
+/* the contribution stored with a reused sample: f (known = its eval was valid) */
+typedef struct sel_f { int known; v3 f; } sel_f;
+static sel_f stored_f(const uint32_t *r) { /* words 26, 27, 30, 31 of a reused reservoir */
+    sel_f o = {r[31] == 1u, V3(f32_of(r[26]), f32_of(r[27]), f32_of(r[30]))};
+    return o;
+}
+static sel_f eval_f(eval_out e) { sel_f o = {e.valid, e.f}; return o; }
+
+static void write_reused(uint32_t *out, const uint32_t *src, float p_sel, float q_sel, sel_f f_sel, float w_sum,
+                         uint32_t C) {
     uint32_t tmp[24];
     memcpy(tmp, src, sizeof tmp); /* src may alias out (temporal works in place) */
     memset(out, 0, 4u * PTO_RESERVOIR_WORDS);
@@ -1101,6 +1115,12 @@ static void write_reused(uint32_t *out, const uint32_t *src, float p_sel, float 
     out[25] = u32_of(q_sel);
     out[28] = u32_of(p_sel > 0.0f ? w_sum / p_sel : 0.0f);
     out[29] = C;
+    if (f_sel.known) {
+        out[26] = u32_of(f_sel.f.x);
+        out[27] = u32_of(f_sel.f.y);
+        out[30] = u32_of(f_sel.f.z);
+        out[31] = 1u;
+    }
 }
 
 /* Temporal reuse (ReSTIR_Pipeline.md:259-340) of pixel (x, y): canonical = this frame's
@@ -1124,9 +1144,10 @@ static void temporal_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t *cur,
     float w_sum = 0.0f;
     const uint32_t *src = cur;
     float p_sel = ec.phat, q_sel = ec.q;
-    if (wrs_update(&w_sum, wc, &seed)) { src = cur; p_sel = ec.phat; q_sel = ec.q; }
-    if (wrs_update(&w_sum, wp, &seed)) { src = hist; p_sel = pp; q_sel = qp; }
-    write_reused(cur, src, p_sel, q_sel, w_sum, 1u + Cp);
+    sel_f f_sel = eval_f(ec);
+    if (wrs_update(&w_sum, wc, &seed)) { src = cur; p_sel = ec.phat; q_sel = ec.q; f_sel = eval_f(ec); }
+    if (wrs_update(&w_sum, wp, &seed)) { src = hist; p_sel = pp; q_sel = qp; f_sel = stored_f(hist); }
+    write_reused(cur, src, p_sel, q_sel, f_sel, w_sum, 1u + Cp);
 }
 
 /* Spatial neighbour k of (x, y): two draws, offsets in [-R, R]^2. Returns 1 if inside the
@@ -1169,9 +1190,11 @@ static void spatial_pixel(const ctx *c, const uint32_t *gbuffer, const uint32_t 
     const float pc = f32_of(rc[24]), qc = f32_of(rc[25]), Wc = f32_of(rc[28]);
     const int canon_ok = rc[29] != 0u && rc[23] >= 2u && pc > 0.0f;
     float wn[16], pf[16], qf[16], sumQ = 0.0f;
+    sel_f ff[16];
     uint32_t Csum = rc[29];
     for (uint32_t k = 0; k < M; ++k) {
         wn[k] = 0.0f; pf[k] = 0.0f; qf[k] = 0.0f;
+        ff[k].known = 0; ff[k].f = V3(0.0f, 0.0f, 0.0f);
         float Q = 1.0f;
         if (present[k]) {
             const uint32_t *rn = cur + PTO_RESERVOIR_WORDS * nb[k];
@@ -1188,6 +1211,7 @@ static void spatial_pixel(const ctx *c, const uint32_t *gbuffer, const uint32_t 
                     wn[k] = m * F.phat * Wn * J;
                     pf[k] = F.phat;
                     qf[k] = F.q;
+                    ff[k] = eval_f(F);
                 }
             }
             if (canon_ok) { /* backward: this pixel's sample in the neighbour's domain */
@@ -1204,14 +1228,16 @@ static void spatial_pixel(const ctx *c, const uint32_t *gbuffer, const uint32_t 
     const float wc = canon_ok ? (sumQ / Mf) * pc * Wc : 0.0f;
     float w_sum = 0.0f, p_sel = pc, q_sel = qc;
     const uint32_t *src = rc;
-    if (wrs_update(&w_sum, wc, &seed)) { src = rc; p_sel = pc; q_sel = qc; }
+    sel_f f_sel = stored_f(rc);
+    if (wrs_update(&w_sum, wc, &seed)) { src = rc; p_sel = pc; q_sel = qc; f_sel = stored_f(rc); }
     for (uint32_t k = 0; k < M; ++k)
         if (wrs_update(&w_sum, wn[k], &seed)) {
             src = cur + PTO_RESERVOIR_WORDS * nb[k];
             p_sel = pf[k];
             q_sel = qf[k];
+            f_sel = ff[k];
         }
-    write_reused(o, src, p_sel, q_sel, w_sum, Csum);
+    write_reused(o, src, p_sel, q_sel, f_sel, w_sum, Csum);
 }
 
 /* Test helper: eval_sample of reservoir `res` in the domain of pixel (x, y). out = {valid, p_hat, q}. */

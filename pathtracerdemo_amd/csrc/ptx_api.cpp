@@ -372,7 +372,7 @@ static int reuse_buffers(ptx_handle *h) {
     const size_t njobs = (size_t)h->band_h * h->cfg.width * 2u * h->reuse_neighbors;
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) return alloc_buf(h, h->d_jres, njobs * 4u);  // ray index per job
     if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
-    return alloc_buf(h, h->d_jres, njobs * 8u);
+    return alloc_buf(h, h->d_jres, njobs * 16u);
 }
 static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     ReuseArgs A{};
@@ -380,7 +380,7 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.cur = res_band(h);
     A.hist = (uint4 *)h->d_hist.p;
     A.jstate = (float4 *)h->d_jstate.p;
-    A.jres = (float2 *)h->d_jres.p;
+    A.jres = (float4 *)h->d_jres.p;
     A.jpp = pass == PTX_PASS_TEMPORAL ? 1u : 2u * h->reuse_neighbors;
     A.njobs = h->band_h * h->cfg.width * A.jpp;
     A.radius = h->reuse_radius;

@@ -81,7 +81,7 @@ struct ReuseArgs {
     uint4 *cur;         // PT_1 reservoirs (temporal output in place), same addressing
     uint4 *hist;        // spatial output = PT_4 input = next frame's history (band only)
     float4 *jstate;     // shift-job state, 6 float4 slots x njobs (SoA)
-    float2 *jres;       // per job: {p_hat, q} (q = 0: invalid)
+    float4 *jres;       // per job: {f (PathContribution, rgb), q} (q = 0: invalid); p_hat = Luminance(f)
     uint32_t njobs, jpp;  // jobs of the pass (npix * jpp), jobs per pixel
     uint32_t radius, neighbors, cap, hist_valid;
 };

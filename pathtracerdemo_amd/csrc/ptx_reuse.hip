@@ -138,7 +138,7 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
             vis = true;
         }
         if (ok) ray = true;
-        else A.jres[jid] = make_float2(0.0f, 0.0f);  // PT_1 would have ended such a path
+        else A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // PT_1 would have ended such a path
     }
     const uint32_t idx = g.rbase + wave_alloc(g.l_ray, ray ? 1u : 0u);
     if (ray) {
@@ -165,7 +165,7 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
             if (s.phase == 0u) {  // regenerated vertex i+1 arrived (PT_4:1378-1380)
                 const Hit h = get_hit(g.res_in, s.idx);
                 if (!h.valid) {
-                    A.jres[jid] = make_float2(0.0f, 0.0f);  // the replayed path escapes here
+                    A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the replayed path escapes here
                 } else {
                     const Surface next = surface_at(sc, h.s, h.pos);
                     const f3 V = normalize(s.prev - s.cur.pos);
@@ -182,7 +182,8 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
                 s.f = s.f * (mk(a.y, a.z, a.w) * a.x);
                 const float qv = s.prod;
                 const bool valid = qv > 0.0f && qv <= 3.402823466e38f;
-                A.jres[jid] = valid ? make_float2(luminance(s.f), qv) : make_float2(0.0f, 0.0f);
+                // the job's PathContribution f (PT_4's, of this sample at this pixel) and q
+                A.jres[jid] = valid ? make_float4(s.f.x, s.f.y, s.f.z, qv) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
         }
         const bool live = job_emit(sc, g, A, emit, s, jid);
@@ -199,13 +200,21 @@ __device__ __forceinline__ bool wrs_update(float &w_sum, float wt, uint32_t &see
     w_sum += wt;
     return rnd(seed) < wt / w_sum;
 }
-__device__ __forceinline__ void write_reused(uint4 *out, const uint4 *src, float p_sel, float q_sel, float w_sum,
-                                             uint32_t C) {
+// The selected sample's PathContribution at this pixel, when known (oracle sel_f): a job's
+// valid result, or what an earlier reuse pass stored (words 26, 27, 30 + flag word 31).
+struct SelF { bool known; f3 f; };
+__device__ __forceinline__ SelF job_f(float4 r) { return SelF{r.w > 0.0f, mk(r.x, r.y, r.z)}; }
+__device__ __forceinline__ SelF stored_f(const uint4 *r) {
+    const uint4 r6 = r[6], r7 = r[7];
+    return SelF{r7.w == 1u, mk(asf(r6.z), asf(r6.w), asf(r7.z))};
+}
+__device__ __forceinline__ void write_reused(uint4 *out, const uint4 *src, float p_sel, float q_sel, SelF fs,
+                                             float w_sum, uint32_t C) {
     // all loads before the stores: src may be out itself (temporal)
     const uint4 a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], a4 = src[4], a5 = src[5];
     out[0] = a0; out[1] = a1; out[2] = a2; out[3] = a3; out[4] = a4; out[5] = a5;
-    out[6] = make_uint4(asu(p_sel), asu(q_sel), 0u, 0u);
-    out[7] = make_uint4(asu(p_sel > 0.0f ? w_sum / p_sel : 0.0f), C, 0u, 0u);
+    out[6] = make_uint4(asu(p_sel), asu(q_sel), fs.known ? asu(fs.f.x) : 0u, fs.known ? asu(fs.f.y) : 0u);
+    out[7] = make_uint4(asu(p_sel > 0.0f ? w_sum / p_sel : 0.0f), C, fs.known ? asu(fs.f.z) : 0u, fs.known ? 1u : 0u);
 }
 
 // ---------------------------------------------------------------- temporal
@@ -244,7 +253,8 @@ __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, Re
         const uint4 *hv = A.hist + 8u * (size_t)pix;
         uint32_t seed = reuse_seed(sc, x, y, SALT_TEMPORAL);
         const uint4 r5 = rv[5], r7 = rv[7];
-        const float2 ec = (r7.y != 0u && r5.w >= 2u) ? A.jres[pix] : make_float2(0.0f, 0.0f);
+        const float4 er = (r7.y != 0u && r5.w >= 2u) ? A.jres[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float2 ec = make_float2(er.w > 0.0f ? luminance(mk(er.x, er.y, er.z)) : 0.0f, er.w);
         const bool canon_ok = ec.y > 0.0f && ec.x > 0.0f;
         const uint4 h5 = hv[5], h6 = hv[6], h7 = hv[7];
         const uint32_t Cp = A.hist_valid ? min(h7.y, A.cap) : 0u;
@@ -257,7 +267,7 @@ __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, Re
         bool from_hist = false;
         if (wrs_update(w_sum, wc, seed)) { from_hist = false; p_sel = ec.x; q_sel = ec.y; }
         if (wrs_update(w_sum, wp, seed)) { from_hist = true; p_sel = pp; q_sel = qp; }
-        write_reused(rv, from_hist ? hv : rv, p_sel, q_sel, w_sum, 1u + Cp);
+        write_reused(rv, from_hist ? hv : rv, p_sel, q_sel, from_hist ? stored_f(hv) : job_f(er), w_sum, 1u + Cp);
     }
 }
 
@@ -319,7 +329,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                     want = rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
                     act = want && job_begin(sc, A, s, nx, ny, xn, (int32_t)pix);
                 }
-                if (want && !act) A.jres[jid] = make_float2(0.0f, 0.0f);
+                if (want && !act) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
         }
         const bool live = job_emit(sc, g, A, act, s, jid);
@@ -361,9 +371,9 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
                     const uint32_t Cn = res_at(A.cur, nidx)[7].y;
                     Csum += Cn;
                     if (canon_ok) {
-                        const float2 B = A.jres[pix * A.jpp + 2u * m + 1u];
-                        if (B.y > 0.0f) {
-                            const float pbc = B.x * qc / B.y;
+                        const float4 B = A.jres[pix * A.jpp + 2u * m + 1u];
+                        if (B.w > 0.0f) {
+                            const float pbc = luminance(mk(B.x, B.y, B.z)) * qc / B.w;
                             const float den = cc * pc + Mf * (float)Cn * pbc;
                             Q = den > 0.0f ? (cc * pc) / den : 1.0f;
                         }
@@ -377,18 +387,21 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
         float w_sum = 0.0f, p_sel = pc, q_sel = qc;
         int32_t src = (int32_t)pix;
         uint32_t nseed = seed0;
-        if (wrs_update(w_sum, wc, seed)) { src = (int32_t)pix; p_sel = pc; q_sel = qc; }
+        SelF f_sel = stored_f(rc);
+        if (wrs_update(w_sum, wc, seed)) { src = (int32_t)pix; p_sel = pc; q_sel = qc; f_sel = stored_f(rc); }
         for (uint32_t m = 0; m < M; ++m) {
             uint32_t nx = 0u, ny = 0u;
             float wn = 0.0f, pf = 0.0f, qf = 0.0f;
+            SelF fj{false, mk(0.0f, 0.0f, 0.0f)};
             int32_t nidx = 0;
             if (spatial_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
                 nidx = band_index(sc, nx, ny);
                 const uint4 *rn = res_at(A.cur, nidx);
                 const float pn = asf(rn[6].x);
                 if (gdecode(A.gbuf[nidx]).valid && rn[5].w >= 2u && pn > 0.0f) {
-                    const float2 F = A.jres[pix * A.jpp + 2u * m];
-                    if (F.y > 0.0f) {
+                    const float4 Fr = A.jres[pix * A.jpp + 2u * m];
+                    if (Fr.w > 0.0f) {
+                        const float2 F = make_float2(luminance(mk(Fr.x, Fr.y, Fr.z)), Fr.w);
                         const float cn = (float)rn[7].y, qn = asf(rn[6].y), Wn = asf(rn[7].x);
                         const float J = qn / F.y;
                         const float pb = pn / J;
@@ -397,12 +410,13 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
                         wn = mw * F.x * Wn * J;
                         pf = F.x;
                         qf = F.y;
+                        fj = job_f(Fr);
                     }
                 }
             }
-            if (wrs_update(w_sum, wn, seed)) { src = nidx; p_sel = pf; q_sel = qf; }
+            if (wrs_update(w_sum, wn, seed)) { src = nidx; p_sel = pf; q_sel = qf; f_sel = fj; }
         }
-        write_reused(out, res_at(A.cur, src), p_sel, q_sel, w_sum, Csum);
+        write_reused(out, res_at(A.cur, src), p_sel, q_sel, f_sel, w_sum, Csum);
     }
 }
 

@@ -638,6 +638,11 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                 s.length = r5.w;
                 if (r7.y == 0u || s.length < 2u) {
                     mix_color(sc, accum, pix, mk(0.0f, 0.0f, 0.0f));
+                } else if (r7.w == 1u) {
+                    // a reused reservoir carrying its sample's PathContribution at this pixel
+                    // (words 26, 27, 30; ptx_reuse.hip write_reused): PT_4's f without the replay
+                    const uint4 r6 = rv[6];
+                    mix_color(sc, accum, pix, mk(asf(r6.z), asf(r6.w), asf(r7.z)) * asf(r7.x));
                 } else {
                     active = true;
                     s.seed1 = r0.y;
