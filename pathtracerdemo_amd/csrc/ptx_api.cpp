@@ -68,6 +68,9 @@ struct ptx_handle {
     // and the GI pipeline's per-pixel direct light
     uint32_t res_u4 = 8;
     DevBuf d_direct;
+    // the wave state holds the PT_1 pass of the reservoirs in d_res (enqueued, nothing since
+    // rewrote them): the reuse temporal pass may read its path hits instead of re-tracing
+    bool init_state_valid = false;
     uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
     bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
     uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
@@ -387,6 +390,7 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.neighbors = h->reuse_neighbors;
     A.cap = h->temporal_cap;
     A.hist_valid = h->hist_valid ? 1u : 0u;
+    A.use_init = (pass == PTX_PASS_TEMPORAL && h->init_state_valid) ? 1u : 0u;
     return A;
 }
 
@@ -434,8 +438,9 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
     if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL) {
         const ReuseArgs A = reuse_args(h, pass);
         const WaveBufs &wj = w;
-        for (int r = 0; e == hipSuccess && r <= kWaveRoundsReuse + 1; ++r) {
-            if (r > 0 && r <= kWaveRoundsReuse) {
+        const int nr = reuse_rounds(pass == PTX_PASS_TEMPORAL, A);
+        for (int r = 0; e == hipSuccess && r <= nr + 1; ++r) {
+            if (r > 0 && r <= nr) {
                 TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
                 e = wave_trace(sc, wj, r - 1, 1, h->stack_depth, st);
                 event_end(t, st);
@@ -449,6 +454,8 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
     }
     // the reuse pipeline's PT_4 reads the spatial output
     const uint4 *fres = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? (const uint4 *)h->d_hist.p : res;
+    // PT_1 fills the wave state the temporal pass may read; PT_4 / MCPT reuse those slots
+    h->init_state_valid = pass == PTX_PASS_INIT && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
     const int rounds = pass == PTX_PASS_INIT ? kWaveRoundsInit : pass == PTX_PASS_FINAL ? kWaveRoundsFinal
                                                                                         : kWaveRoundsMcpt;
     for (int r = 0; e == hipSuccess && r <= rounds; ++r) {
@@ -513,6 +520,9 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
         if ((e = hipEventRecord(h->ev_join[q], h->sub[q])) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(h->stream, h->ev_join[q], 0)) != hipSuccess) return e;
     }
+    // the temporal pass rewrote the reservoirs PT_1's state describes
+    for (int i = 0; i < npasses; ++i)
+        if (passes[i] == PTX_PASS_TEMPORAL) h->init_state_valid = false;
     return hipSuccess;
 }
 static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass) {
@@ -735,6 +745,7 @@ int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const
     h->layout_valid = false;
     h->scene_loaded = true;
     h->hist_valid = false;
+    h->init_state_valid = false;
     if (h->frame_set) return build_layout(h);
     return PTX_OK;
 }
@@ -942,6 +953,7 @@ int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t byte
         return fail(h, PTX_E_INVALID, "write of %zu bytes to buffer %d", bytes, which);
     HIP_CHECK(h, hipStreamSynchronize(h->stream));
     HIP_CHECK(h, hipMemcpy(b.p, host_src, bytes, hipMemcpyHostToDevice));
+    h->init_state_valid = false;  // the wave state no longer matches the buffers
     return PTX_OK;
 }
 

@@ -43,7 +43,10 @@ hipError_t launch_mcpt_tiled(const Scene &sc, float4 *accum, uint32_t stack_dept
 // launch has one workgroup per segment; queue lengths live on the device
 // (cnt[(2r) * nseg + j] pixels of segment j active after logic round r, cnt[(2r+1) *
 // nseg + j] rays it emitted), so the host never synchronises inside a pass.
-constexpr uint32_t kWaveStateSlots = 9u;   // float4 per pixel (PT_1 needs the most)
+constexpr uint32_t kWaveStateSlots = 10u;  // float4 per pixel (PT_1 needs the most)
+// PT_1 state slots the reuse pipeline's temporal pass reads (vertex 2 / 3 hit compacts, the
+// selected NEE candidate's Visibility or -1 for an env candidate): ptx_wave.hip IS_*
+constexpr uint32_t kStateCs2 = 7u, kStateCs3 = 8u, kStateTsel = 9u;
 constexpr uint32_t kWaveSegPixels = 512u;  // padded pixels per segment (8 8x8 tiles); 512 > 1024 > 256
 constexpr int kWaveRoundsInit = 3, kWaveRoundsFinal = 3, kWaveRoundsMcpt = 4;
 constexpr int kWaveMaxRounds = 5;
@@ -84,7 +87,10 @@ struct ReuseArgs {
     float4 *jres;       // per job: {f (PathContribution, rgb), q} (q = 0: invalid); p_hat = Luminance(f)
     uint32_t njobs, jpp;  // jobs of the pass (npix * jpp), jobs per pixel
     uint32_t radius, neighbors, cap, hist_valid;
+    uint32_t use_init;  // temporal: this frame's PT_1 wave state (path hits, NEE Visibility) is in w.state
 };
+// rounds of {trace, step} between a reuse pass's start and combine launches
+int reuse_rounds(int pass_temporal, const ReuseArgs &A);
 hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,
                             hipStream_t s);
 

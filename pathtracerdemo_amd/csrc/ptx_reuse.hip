@@ -218,7 +218,57 @@ __device__ __forceinline__ void write_reused(uint4 *out, const uint4 *src, float
 }
 
 // ---------------------------------------------------------------- temporal
-__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+// The canonical sample is PT_1's own path: replaying its BSDF draws from its pixel's hit
+// gives back PT_1's vertices, whose hits PT_1 left in its wave state (vertex 2 / 3 compacts),
+// and its light segment's Visibility is the one PT_1 traced for the selected NEE candidate.
+// So the job runs without tracing -- the same operations as job_emit + wjob_step, with the
+// trace results read instead of recomputed (identical bits: same rays, deterministic
+// traversal).  Returns true when the job still needs its light ray (an env candidate).
+__device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBufs &w, const ReuseArgs &A, Job &s,
+                                                   uint32_t pix) {
+    const uint4 *rv = res_at(A.cur, s.ref);
+    while (s.i + 1u < s.length) {
+        f3 V = normalize(s.prev - s.cur.pos);
+        uint32_t seed = s.i == 1u ? rv[0].x : s.seed1, lobe;
+        const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
+        const float pdf = pdf_bsdf(s.cur, V, dir);
+        s.prod *= pdf;
+        if (!rr_step(s, s.cur, V, dir, pdf)) {
+            A.jres[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            return false;
+        }
+        const float4 c = w.state[(s.i == 1u ? kStateCs2 : kStateCs3) * w.npix + pix];
+        const Surface next = get_surface(sc, gdecode(make_uint4(asu(c.x), asu(c.y), asu(c.z), asu(c.w))));
+        V = normalize(s.prev - s.cur.pos);
+        const f3 L = normalize(next.pos - s.cur.pos);
+        s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+        s.prev = s.cur.pos;
+        s.cur = next;
+        s.i += 1u;
+    }
+    const float T = w.state[kStateTsel * w.npix + pix].x;
+    if (T < 0.0f) return true;  // env candidate: its Visibility was never traced
+    const LightSample XL = load_xl(rv);
+    const f3 V = normalize(s.prev - s.cur.pos);
+    const f3 L = direction_to_light(s.cur, XL);
+    s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+    float gl = 1.0f;
+    if (XL.type == LIGHT_RECT) {
+        const f3 r = XL.pos - s.cur.pos;
+        const f3 Ld = normalize(r);
+        gl = fabsf(dot(get_light(sc, (uint32_t)XL.id).dir, Ld)) / dot(r, r);
+    }
+    s.prod = s.prod / (gl * s.beta);
+    const f3 Le = l_emit<true>(XL, s.cur);
+    s.f = s.f * (Le * T);
+    const float qv = s.prod;
+    const bool valid = qv > 0.0f && qv <= 3.402823466e38f;
+    A.jres[pix] = valid ? make_float4(s.f.x, s.f.y, s.f.z, qv) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    return false;
+}
+
+// (the inlined replay needs more registers than the 4-wave budget: 160 B/lane spilled there)
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(2, 8)))
 void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, 0u, lds);
@@ -231,6 +281,7 @@ void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
         if (q < np && tile_xy(sc, q, x, y)) {
             pix = (y - sc.row_begin) * sc.width + x;
             active = job_begin(sc, A, s, x, y, gdecode(A.gbuf[pix]), (int32_t)pix);
+            if (active && A.use_init) active = temporal_from_init(sc, w, A, s, pix);
         }
         const bool live = job_emit(sc, g, A, active, s, pix);
         if (live) job_store(A, pix, s);
@@ -423,13 +474,16 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
 // ---------------------------------------------------------------- host side
 // Logic round 0 creates the jobs, rounds 1..kWaveRoundsReuse step them, the last round
 // combines (so round r > 0 consumes trace round r-1).
+// temporal from PT_1's state: only env candidates trace (one light ray each)
+int reuse_rounds(int pass_temporal, const ReuseArgs &A) { return pass_temporal && A.use_init ? 1 : kWaveRoundsReuse; }
+
 hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,
                             hipStream_t s) {
     const dim3 grid(w.seg_count), blk(WB);
     if (round == 0) {
         if (pass_temporal) hipLaunchKernelGGL(wtemporal_start, grid, blk, 0, s, sc, w, A);
         else hipLaunchKernelGGL(wspatial_start, grid, blk, 0, s, sc, w, A);
-    } else if (round <= kWaveRoundsReuse) {
+    } else if (round <= reuse_rounds(pass_temporal, A)) {
         hipLaunchKernelGGL(wjob_step, grid, blk, 0, s, sc, w, (uint32_t)round, A);
     } else {
         if (pass_temporal) hipLaunchKernelGGL(wtemporal_combine, grid, blk, 0, s, sc, w, A);

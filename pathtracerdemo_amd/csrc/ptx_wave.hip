@@ -300,7 +300,9 @@ __global__ __launch_bounds__(WB) void wgbuffer(Scene sc, WaveBufs w, uint4 *gbuf
 
 // =========================================================================== PT_1 (init)
 // Pixel state, SoA float4 slots (slot k of pixel p at state[k * npix + p]).
-enum : uint32_t { IS_HDR, IS_FP, IS_RES, IS_X, IS_XL, IS_L, IS_BSEED, IS_CS2, IS_CS3, IS_COUNT };
+enum : uint32_t { IS_HDR, IS_FP, IS_RES, IS_X, IS_XL, IS_L, IS_BSEED, IS_CS2, IS_CS3, IS_TSEL, IS_COUNT };
+static_assert(IS_CS2 == kStateCs2 && IS_CS3 == kStateCs3 && IS_TSEL == kStateTsel && IS_COUNT <= kWaveStateSlots,
+              "PT_1 state slots read by the temporal pass (ptx_reuse.hip)");
 // flags (IS_HDR.y >> 8): bit0 selected, bit1 has BSDF ray, bit2 far12, bit3 far23,
 // bit4 rough1 >= 0.5, bit5 rough2 >= 0.5, bits 8-9 Lobe[1], bits 10-11 Lobe[2]
 enum : uint32_t { F_SEL = 1u, F_BSDF = 2u, F_FAR12 = 4u, F_FAR23 = 8u, F_R1 = 16u, F_R2 = 32u };
@@ -508,6 +510,9 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
             if (b.y < ris / s.w_sum) {
                 s.flags |= F_SEL;
                 s.p_hat_sel = p_hat;
+                // the selected NEE candidate's Visibility (the temporal pass's canonical
+                // evaluation reuses it instead of re-tracing the light segment)
+                state[IS_TSEL * npix + pix] = make_float4(a.x, 0.0f, 0.0f, 0.0f);
                 LightSample XL;
                 const Light ls = get_light(sc, asu(b.w));
                 XL.id = (int32_t)asu(b.w);
@@ -534,6 +539,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                     if (u < ris_e / s.w_sum) {
                         s.flags |= F_SEL;
                         s.p_hat_sel = ph;
+                        state[IS_TSEL * npix + pix] = make_float4(-1.0f, 0.0f, 0.0f, 0.0f);  // env: traced later
                         LightSample env;
                         env.pos = s.xpos + s.L * INF_F;
                         env.type = LIGHT_ENV;
