@@ -1,0 +1,22 @@
+#!/usr/bin/env bash
+# Copy a round_evidence.sh run's rocprofv3 summaries from gpurun_out/ (scratch) into the
+# tracked profiles/<round>/<workload>/ and refresh profiles/hbm_traffic.json.
+# usage: ROUND=r1 WORKLOADS="reuse restir mcpt gi" bash tools/collect_profiles.sh
+set -eu
+R="$(cd "$(dirname "$0")/.." && pwd)"
+cd "$R"
+ROUND=${ROUND:-r1}
+declare -A SCENE=([reuse]=c3_interior_32 [gi]=c3_interior_32 [restir]=dummy_scene_1 [mcpt]=dummy_scene_1)
+for WL in ${WORKLOADS:-reuse restir mcpt gi}; do
+  src=gpurun_out/prof_${ROUND}_$WL
+  dst=profiles/$ROUND/$WL
+  mkdir -p "$dst/pmc_FETCH_SIZE" "$dst/pmc_WRITE_SIZE"
+  cp "$src/trace/run_kernel_stats.csv" "$dst/kernel_stats.csv"
+  cp "$src/trace/run_kernel_trace.csv" "$dst/kernel_trace.csv"
+  cp "$src/pmc_FETCH_SIZE/run_counter_collection.csv" "$dst/pmc_FETCH_SIZE/counter_collection.csv"
+  cp "$src/pmc_WRITE_SIZE/run_counter_collection.csv" "$dst/pmc_WRITE_SIZE/counter_collection.csv"
+  cp "$src/bench_trace.log" "$dst/bench_under_rocprof.log"
+  tail -n 1 "gpurun_out/bench_${ROUND}_$WL.log" > "$dst/bench_line.json"
+  python3 tools/hbm_traffic.py "$dst" "$WL:${SCENE[$WL]}:trace_queue:1920x1080" "trace_queue<false" > /dev/null
+  echo "$WL -> $dst"
+done
