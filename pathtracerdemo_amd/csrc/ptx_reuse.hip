@@ -341,29 +341,57 @@ __device__ __forceinline__ int32_t band_index(const Scene &sc, uint32_t x, uint3
     return ((int32_t)y - (int32_t)sc.row_begin) * (int32_t)sc.width + (int32_t)x;
 }
 
-// One thread per job: job slot 2m (+1) of a pixel = the forward (backward) shift with
-// neighbour m.  A workgroup walks its segment slot by slot, so a wave holds one 8x8 tile's
-// jobs of the same kind; the neighbour offsets are re-drawn per job (2 PCG draws each).
-__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+// job_begin with the domain's camera point and hit surface already at hand
+__device__ __forceinline__ bool job_begin_at(const ReuseArgs &A, Job &s, f3 x0, const Surface &X1, const Compact &x1,
+                                             int32_t ref) {
+    const uint4 *rv = res_at(A.cur, ref);
+    const uint32_t C = rv[7].y, length = rv[5].w;
+    if (!x1.valid || C == 0u || length < 2u) return false;
+    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = rv[0].y; s.idx = 0u; s.ref = ref;
+    s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
+    s.prev = x0;
+    s.cur = X1;
+    s.matref = (x1.inst << 16) | x1.mat;
+    s.beta = 1.0f; s.rr_p = 1.0f; s.rr_f = mk(1.0f, 1.0f, 1.0f);
+    return true;
+}
+
+// One thread per (pixel, kind): the forward shifts (slots 2m: neighbour m's sample in this
+// pixel's domain) share the pixel's camera point and hit surface, the backward ones (2m+1:
+// this pixel's sample in neighbour m's domain) its reservoir; the neighbour offsets come
+// from one pass over the pixel's salted stream.  A workgroup walks its segment kind by kind
+// and neighbour by neighbour, so a wave emits one 8x8 tile's jobs of one slot at a time.
+#ifndef SPATIAL_START_WAVES
+#define SPATIAL_START_WAVES 3  // the shared surface + one job: 128 VGPRs spill 108 B/lane
+#endif
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(SPATIAL_START_WAVES, 8)))
 void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, 0u, lds);
     const uint32_t np = padded_pixels(sc), jpp = A.jpp;
-    for (uint32_t base = 0; base < w.seg_px * jpp; base += WB) {  // workgroup-uniform
-        const uint32_t slot = base / w.seg_px, m = slot >> 1;
-        const bool backward = (slot & 1u) != 0u;
+    for (uint32_t base = 0; base < w.seg_px * 2u; base += WB) {  // workgroup-uniform
+        const bool backward = base >= w.seg_px;
         const uint32_t q = seg_pixel(w, g.j, base % w.seg_px);
-        uint32_t x, y, jid = 0u;
-        bool act = false;
-        Job s;
+        uint32_t x = 0u, y = 0u, pix = 0u, seed = 0u;
+        Compact x1{};
+        Surface X1{};
+        f3 x0{};
         if (q < np && tile_xy(sc, q, x, y)) {
-            const uint32_t pix = (y - sc.row_begin) * sc.width + x;
-            jid = pix * jpp + slot;
-            const Compact x1 = gdecode(A.gbuf[pix]);
+            pix = (y - sc.row_begin) * sc.width + x;
+            x1 = gdecode(A.gbuf[pix]);
+            seed = reuse_seed(sc, x, y, SALT_SPATIAL);
+            if (x1.valid && !backward) {
+                X1 = get_surface(sc, x1);
+                x0 = x0_of(sc, x, y);
+            }
+        }
+        for (uint32_t m = 0; m < A.neighbors; ++m) {  // uniform
+            const uint32_t jid = pix * jpp + 2u * m + (backward ? 1u : 0u);
+            bool act = false;
+            Job s;
             if (x1.valid) {
-                uint32_t seed = reuse_seed(sc, x, y, SALT_SPATIAL), nx = 0u, ny = 0u;
-                bool present = false;
-                for (uint32_t k = 0; k <= m; ++k) present = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+                uint32_t nx = 0u, ny = 0u;
+                bool present = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
                 const int32_t nidx = present ? band_index(sc, nx, ny) : 0;
                 Compact xn{};
                 if (present) {
@@ -374,7 +402,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 if (present && !backward) {  // the neighbour's sample in this pixel's domain
                     const uint4 *rn = res_at(A.cur, nidx);
                     want = rn[5].w >= 2u && asf(rn[6].x) > 0.0f;
-                    act = want && job_begin(sc, A, s, x, y, x1, nidx);
+                    act = want && job_begin_at(A, s, x0, X1, x1, nidx);
                 } else if (present) {  // this pixel's sample in the neighbour's domain
                     const uint4 *rc = A.cur + 8u * (size_t)pix;
                     want = rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
@@ -382,10 +410,10 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 }
                 if (want && !act) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
+            const bool live = job_emit(sc, g, A, act, s, jid);
+            if (live) job_store(A, jid, s);
+            seg_keep(g, live, jid);
         }
-        const bool live = job_emit(sc, g, A, act, s, jid);
-        if (live) job_store(A, jid, s);
-        seg_keep(g, live, jid);
     }
     seg_end(w, g);
 }
