@@ -302,6 +302,9 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
             // (SH/PT_1_InitPass.wgsl:605-715), so hits, ties and work counts are unchanged.
             int sp = -1;
             uint32_t grp = 0u, leaf = 0u;
+            // the pre-filter's bound: while no hit has shrunk vy since, its result for a root
+            // IS the reference's test of that root (same function, same arguments)
+            const float vy_pf = vy;
             for (;;) {
                 while (leaf == 0u && (sp >= 0 || mask != 0u)) {
                     if (PROF) pf.hit(PROF_NODE);
@@ -310,7 +313,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                         mask &= mask - 1u;
                         const SubRoot &R = roots[s0 + k];
                         float tn;
-                        if (box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) {
+                        if ((ROOTQ && vy == vy_pf) || box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) {
                             stack[0] = R.ref;
                             sp = 0;
                             grp = s0 + k;
