@@ -213,7 +213,8 @@ static int build_layout(ptx_handle *h) {
                 return PTX_OK;
             };
             SubRoot r{};
-            for (int k = 0; k < 3; ++k) { r.bmin[k] = as_f32(A[base + k]); r.bmax[k] = as_f32(A[base + 3 + k]); }
+            float *axis[3] = {r.x, r.y, r.z};
+            for (int k = 0; k < 3; ++k) { axis[k][0] = as_f32(A[base + k]); axis[k][1] = as_f32(A[base + 3 + k]); }
             if (int rc = ref_of(0u, r.ref)) return rc;
             subs.push_back(r);
             for (uint32_t n : interior) {
@@ -221,9 +222,10 @@ static int build_layout(ptx_handle *h) {
                 uint32_t L = n + 1u, R = A[w + 6] / 8u;
                 size_t wl = (size_t)base + 8u * L, wr = (size_t)base + 8u * R;
                 NodePair np{};
+                float *naxis[3] = {np.x, np.y, np.z};
                 for (int k = 0; k < 3; ++k) {
-                    np.lmin[k] = as_f32(A[wl + k]); np.lmax[k] = as_f32(A[wl + 3 + k]);
-                    np.rmin[k] = as_f32(A[wr + k]); np.rmax[k] = as_f32(A[wr + 3 + k]);
+                    naxis[k][0] = as_f32(A[wl + k]); naxis[k][1] = as_f32(A[wr + k]);
+                    naxis[k][2] = as_f32(A[wl + 3 + k]); naxis[k][3] = as_f32(A[wr + 3 + k]);
                 }
                 if (int rc = ref_of(L, np.lref)) return rc;
                 if (int rc = ref_of(R, np.rref)) return rc;

@@ -48,12 +48,14 @@ enum : uint32_t {
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 constexpr uint32_t LEAF_FIRST_MASK = 0x00FFFFFFu;
 
+// Both children's boxes by axis: {lmin.a, rmin.a, lmax.a, rmax.a} for a = x, y, z, then the
+// refs -- each axis's slab terms of the two children are one packed-FP32 pair (box_pair).
 struct alignas(16) NodePair {   // 64 B
-    float lmin[3], lmax[3], rmin[3], rmax[3];
+    float x[4], y[4], z[4];
     uint32_t lref, rref, pad0, pad1;
 };
-struct alignas(16) SubRoot {    // 32 B
-    float bmin[3], bmax[3];
+struct alignas(16) SubRoot {    // 32 B: the root box by axis, {min, max} pairs (box_root)
+    float x[2], y[2], z[2];
     uint32_t ref, pad;
 };
 struct alignas(16) Inst {       // 144 B
@@ -159,15 +161,41 @@ struct Hit { bool valid; float t; Compact s; f3 pos; };
 struct PassEps { float det_eps, bary_eps; };
 
 // GetRayAABBIntersectionRange + DoRangesOverlap(RayValidRange, .) (SH/PT_1_InitPass.wgsl:475-514)
-// with InvDirection hoisted (it is the same 1/dir for every test of the ray).
-__device__ __forceinline__ bool box_overlap(f3 o, f3 inv, const float *bmin, const float *bmax, float vx,
-                                            float vy, float &tnear) {
-    float t1x = (bmin[0] - o.x) * inv.x, t1y = (bmin[1] - o.y) * inv.y, t1z = (bmin[2] - o.z) * inv.z;
-    float t2x = (bmax[0] - o.x) * inv.x, t2y = (bmax[1] - o.y) * inv.y, t2z = (bmax[2] - o.z) * inv.z;
-    float tmin = fmaxf(fminf(t1x, t2x), fmaxf(fminf(t1y, t2y), fminf(t1z, t2z)));
-    float tmax = fminf(fmaxf(t1x, t2x), fminf(fmaxf(t1y, t2y), fmaxf(t1z, t2z)));
+// with InvDirection hoisted (it is the same 1/dir for every test of the ray): per axis
+// t1 = (min - o) * inv, t2 = (max - o) * inv; tmin = max of the per-axis mins, tmax = min of
+// the maxes; an empty range becomes (1, 0); overlap with the closed [vx, vy].
+// The slab test for a node's two children at once.  The slab terms (b - o) * inv of both
+// children go through packed FP32 (v_pk_add_f32 / v_pk_mul_f32: two IEEE f32 operations per
+// lane, rounded exactly as the scalar ones -- no contraction under -ffp-contract=off), the
+// min/max reduction per child stays scalar.  Same results as two scalar slab tests.
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void box_pair(f3 o, f3 inv, float4 qx, float4 qy, float4 qz, float vx, float vy, bool &hl,
+                                         bool &hr, float &tl, float &tr) {
+    const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const v2f ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    const v2f t1x = (v2f{qx.x, qx.y} - ox) * ix, t2x = (v2f{qx.z, qx.w} - ox) * ix;
+    const v2f t1y = (v2f{qy.x, qy.y} - oy) * iy, t2y = (v2f{qy.z, qy.w} - oy) * iy;
+    const v2f t1z = (v2f{qz.x, qz.y} - oz) * iz, t2z = (v2f{qz.z, qz.w} - oz) * iz;
+    float lmin = fmaxf(fminf(t1x.x, t2x.x), fmaxf(fminf(t1y.x, t2y.x), fminf(t1z.x, t2z.x)));
+    float lmax = fminf(fmaxf(t1x.x, t2x.x), fminf(fmaxf(t1y.x, t2y.x), fmaxf(t1z.x, t2z.x)));
+    float rmin = fmaxf(fminf(t1x.y, t2x.y), fmaxf(fminf(t1y.y, t2y.y), fminf(t1z.y, t2z.y)));
+    float rmax = fminf(fmaxf(t1x.y, t2x.y), fminf(fmaxf(t1y.y, t2y.y), fmaxf(t1z.y, t2z.y)));
+    if (lmin > lmax) { lmin = 1.0f; lmax = 0.0f; }
+    if (rmin > rmax) { rmin = 1.0f; rmax = 0.0f; }
+    tl = lmin;
+    tr = rmin;
+    hl = (vx <= lmax) && (lmin <= vy);
+    hr = (vx <= rmax) && (rmin <= vy);
+}
+
+// The slab test of a sub-mesh root, each axis's {min, max} slab terms as one packed pair
+__device__ __forceinline__ bool box_root(f3 o, f3 inv, const SubRoot &R, float vx, float vy) {
+    const v2f t_x = (v2f{R.x[0], R.x[1]} - v2f{o.x, o.x}) * v2f{inv.x, inv.x};
+    const v2f t_y = (v2f{R.y[0], R.y[1]} - v2f{o.y, o.y}) * v2f{inv.y, inv.y};
+    const v2f t_z = (v2f{R.z[0], R.z[1]} - v2f{o.z, o.z}) * v2f{inv.z, inv.z};
+    float tmin = fmaxf(fminf(t_x.x, t_x.y), fmaxf(fminf(t_y.x, t_y.y), fminf(t_z.x, t_z.y)));
+    float tmax = fminf(fmaxf(t_x.x, t_x.y), fminf(fmaxf(t_y.x, t_y.y), fmaxf(t_z.x, t_z.y)));
     if (tmin > tmax) { tmin = 1.0f; tmax = 0.0f; }
-    tnear = tmin;
     return (vx <= tmax) && (tmin <= vy);
 }
 
@@ -286,14 +314,12 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
             if (ROOTQ) {
 #pragma unroll 1
                 for (uint32_t k = 0; k < nc; ++k) {
-                    float tn;
                     if (PROF) pf.hit(PROF_ROOT);
-                    if (box_overlap(lo, inv, roots[s0 + k].bmin, roots[s0 + k].bmax, vx, vy, tn)) mask |= 1u << k;
+                    if (box_root(lo, inv, roots[s0 + k], vx, vy)) mask |= 1u << k;
                 }
             } else {
-                float tn;
                 if (PROF) pf.hit(PROF_ROOT);
-                if (box_overlap(lo, inv, roots[s0 + kk].bmin, roots[s0 + kk].bmax, vx, vy, tn)) mask = 1u << kk;
+                if (box_root(lo, inv, roots[s0 + kk], vx, vy)) mask = 1u << kk;
             }
             // while-while traversal over all of this lane's roots: lanes descend interior
             // nodes (taking their next root, in index order, when the stack runs dry) until
@@ -312,8 +338,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                         const uint32_t k = (uint32_t)__builtin_ctz(mask);
                         mask &= mask - 1u;
                         const SubRoot &R = roots[s0 + k];
-                        float tn;
-                        if ((ROOTQ && vy == vy_pf) || box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) {
+                        if ((ROOTQ && vy == vy_pf) || box_root(lo, inv, R, vx, vy)) {
                             stack[0] = R.ref;
                             sp = 0;
                             grp = s0 + k;
@@ -328,12 +353,10 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                     }
                     const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + ref);
                     float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
-                    float lmin[3] = {q0.x, q0.y, q0.z}, lmax[3] = {q0.w, q1.x, q1.y};
-                    float rmin[3] = {q1.z, q1.w, q2.x}, rmax[3] = {q2.y, q2.z, q2.w};
                     uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
                     float tl, tr;
-                    bool hl = box_overlap(lo, inv, lmin, lmax, vx, vy, tl);
-                    bool hr = box_overlap(lo, inv, rmin, rmax, vx, vy, tr);
+                    bool hl, hr;
+                    box_pair(lo, inv, q0, q1, q2, vx, vy, hl, hr, tl, tr);
                     n_aabb += 2;
                     if (hl && hr) {
                         uint32_t first = tl < tr ? rref : lref;

@@ -167,8 +167,7 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
                 grp = s;
                 ++s;
                 ++n_aabb;
-                float tn;
-                if (box_overlap(lo, inv, R.bmin, R.bmax, vx, vy, tn)) {
+                if (box_root(lo, inv, R, vx, vy)) {
                     sp = 0;
                     stack[0] = R.ref;
                 }
@@ -247,12 +246,10 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
         } else if (do_node) {  // one interior node: both children, nearer on top
             const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + node);
             const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
-            const float lmin[3] = {q0.x, q0.y, q0.z}, lmax[3] = {q0.w, q1.x, q1.y};
-            const float rmin[3] = {q1.z, q1.w, q2.x}, rmax[3] = {q2.y, q2.z, q2.w};
             const uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
             float tl, tr;
-            const bool hl = box_overlap(lo, inv, lmin, lmax, vx, vy, tl);
-            const bool hr = box_overlap(lo, inv, rmin, rmax, vx, vy, tr);
+            bool hl, hr;
+            box_pair(lo, inv, q0, q1, q2, vx, vy, hl, hr, tl, tr);
             n_aabb += 2u;
             if (hl && hr) {
                 stack[(uint32_t)(sp + 1) * WB] = tl < tr ? rref : lref;
