@@ -142,3 +142,43 @@ def test_reuse_bands_with_halo_exchange_gloo(tmp_path, world, scene1, oracle_mod
     got = np.concatenate([np.load(out % r) for r in range(world)], axis=0)
     assert (got[..., 4 + 29] > 1).any()  # the history took part
     np.testing.assert_array_equal(got, full)
+
+
+def _gi_rank_main(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from oracle_band import OracleBand
+    from pathtracerdemo_amd.bands import ReuseBand, band
+    from pathtracerdemo_amd.scene.world import compile_scene
+    cs = compile_scene("c3_interior_32")
+    W, H = REUSE_W, REUSE_H
+    b, e = band(H, world, rank)
+    fr = O.Frame(uniform_for(cs, W, H), cs.scene, cs.geometry, cs.accel)
+    fr.reuse = REUSE_PRM
+    rb = ReuseBand(OracleBand(O, fr, b, e, gi=True), rank, world)
+    for f in (1, 2, 3):
+        fr.set_frame_index(f)
+        rb.render_frame()
+    np.save(out % rank, np.concatenate([fr.accum[b:e].view(np.uint32), fr.gi_hist[b:e]], axis=-1))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gi_bands_with_halo_exchange_gloo(tmp_path, world, scene3, oracle_mod):
+    """ReSTIR GI over N ranks (gloo): the same two-pass-group band driver with 80-byte halo
+    rows (G-buffer + GI reservoir) reproduces the full-frame GI render bit for bit."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "gi%d.npy")
+    mp.spawn(_gi_rank_main, args=(world, _free_port(), out), nprocs=world, join=True)
+    fr = oracle_mod.Frame(uniform_for(scene3, REUSE_W, REUSE_H), scene3.scene, scene3.geometry, scene3.accel)
+    fr.reuse = REUSE_PRM
+    for f in (1, 2, 3):
+        fr.set_frame_index(f)
+        fr.run_gi_frame(threads=2)
+    full = np.concatenate([fr.accum.view(np.uint32), fr.gi_hist], axis=-1)
+    got = np.concatenate([np.load(out % r) for r in range(world)], axis=0)
+    assert (got[..., 4 + 11] > 1).any()  # the history took part
+    np.testing.assert_array_equal(got, full)

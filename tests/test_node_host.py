@@ -68,7 +68,7 @@ def test_js_uniform_matches_python_host(scene1, scene_dir):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pipeline,frames", [("restir", 3), ("mcpt", 1)])
+@pytest.mark.parametrize("pipeline,frames", [("restir", 3), ("mcpt", 1), ("reuse", 3), ("gi", 3)])
 def test_native_renderer_frames_bit_exact(scene1, scene_dir, oracle_mod, tmp_path, pipeline, frames):
     W, H = 96, 64
     out = str(tmp_path / "img.f32")
@@ -79,6 +79,11 @@ def test_native_renderer_frames_bit_exact(scene1, scene_dir, oracle_mod, tmp_pat
     fr = oracle_mod.Frame(uniform_for(scene1, W, H, 1), scene1.scene, scene1.geometry, scene1.accel)
     for f in range(1, frames + 1):
         fr.set_frame_index(f)
-        fr.run(oracle_mod.PASS_RESTIR if pipeline == "restir" else oracle_mod.PASS_MCPT)
+        if pipeline == "reuse":
+            fr.run_reuse_frame()
+        elif pipeline == "gi":
+            fr.run_gi_frame()
+        else:
+            fr.run(oracle_mod.PASS_RESTIR if pipeline == "restir" else oracle_mod.PASS_MCPT)
     np.testing.assert_array_equal(np.array(info["uniform"], dtype=np.uint64).astype(np.uint32), fr.uniform)
     np.testing.assert_array_equal(img.view(np.uint32), fr.accum.view(np.uint32))
