@@ -242,70 +242,82 @@ __device__ __forceinline__ int32_t gi_band_index(const Scene &sc, uint32_t x, ui
 }
 
 // The shift of GI reservoir s into domain (x, y) with hit y1, up to its occlusion query
-// (oracle gi_shift): false when no such path exists (q invalid).
-__device__ __forceinline__ bool gi_shift_begin(const Scene &sc, uint32_t x, uint32_t y, const Compact &y1,
-                                               const uint4 *s, f3 &f, float &q, f3 &o, f3 &dir, float &remain) {
-    const uint4 s0 = s[0], s1 = s[1], s2 = s[2];
-    if (!y1.valid || s2.w == 0u) return false;
-    const Surface Y = get_surface(sc, y1);
-    const f3 Vy = normalize(x0_of(sc, x, y) - Y.pos);
-    if (!(s0.x & 0x80000000u)) {
-        dir = ld3(s1);
-        f = (bsdf(Y, Vy, dir) * fabsf(dot(Y.nrm, dir))) * ENV_C;
+// (oracle gi_shift): false when no such path exists (q invalid).  Split in the two halves
+// a pixel's jobs share: the domain (camera point + hit surface: every forward job of a
+// pixel) and the sample (x2 surface: every backward job of a pixel).
+struct GiDomain { Surface Y; f3 Vy; };
+struct GiSample { bool env; f3 dir, lt; Surface X2; };
+__device__ __forceinline__ GiDomain gi_domain(const Scene &sc, uint32_t x, uint32_t y, const Compact &y1) {
+    GiDomain d;
+    d.Y = get_surface(sc, y1);
+    d.Vy = normalize(x0_of(sc, x, y) - d.Y.pos);
+    return d;
+}
+__device__ __forceinline__ GiSample gi_sample(const Scene &sc, const uint4 *s) {
+    const uint4 s0 = s[0];
+    GiSample m;
+    m.env = !(s0.x & 0x80000000u);
+    m.dir = ld3(s[1]);
+    m.lt = ld3(s[2]);
+    if (!m.env) m.X2 = get_surface(sc, gdecode(s0));
+    return m;
+}
+__device__ __forceinline__ bool gi_shift_begin(const GiDomain &d, const GiSample &m, f3 &f, float &q, f3 &o,
+                                               f3 &dir, float &remain) {
+    if (m.env) {
+        dir = m.dir;
+        f = (bsdf(d.Y, d.Vy, dir) * fabsf(dot(d.Y.nrm, dir))) * ENV_C;
         q = 1.0f;
         remain = FLT_MAX_F;
     } else {
-        const Surface X2 = get_surface(sc, gdecode(s0));
-        const f3 r = X2.pos - Y.pos;
+        const f3 r = m.X2.pos - d.Y.pos;
         const float dist = length(r);
         dir = r / dist;
-        const f3 V2 = normalize(Y.pos - X2.pos);
-        f = (bsdf(Y, Vy, dir) * fabsf(dot(Y.nrm, dir))) * gi_lo(X2, V2, ld3(s1), ld3(s2));
-        q = gi_q(Y.pos, X2);
+        const f3 V2 = normalize(d.Y.pos - m.X2.pos);
+        f = (bsdf(d.Y, d.Vy, dir) * fabsf(dot(d.Y.nrm, dir))) * gi_lo(m.X2, V2, m.dir, m.lt);
+        q = gi_q(d.Y.pos, m.X2);
         remain = dist * GI_VIS_SHORTEN;
     }
-    o = Y.pos;
+    o = d.Y.pos;
     return gi_q_ok(q);
 }
 
-// One thread per job (slot 2m: neighbour m's sample -> this pixel, 2m+1: this pixel's
-// sample -> neighbour m); the job's contribution and q ride in its ray's result slot.
-__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
-void wgis_start(Scene sc, WaveBufs w, GiArgs A) {
-    __shared__ uint32_t lds[2];
-    const Seg g = seg_begin(w, 0u, lds);
-    const uint32_t np = padded_pixels(sc), jpp = A.jpp;
-    for (uint32_t base = 0; base < w.seg_px * jpp; base += WB) {  // workgroup-uniform
-        const uint32_t slot = base / w.seg_px, m = slot >> 1;
-        const bool backward = (slot & 1u) != 0u;
-        const uint32_t q = seg_pixel(w, g.j, base % w.seg_px);
-        uint32_t x, y, jid = 0u;
-        bool ray = false, job = false;
+// The jobs of one pixel of one kind (workgroup-uniform): forward jobs (slot 2m: neighbour
+// m's sample -> this pixel) share this pixel's domain, backward jobs (2m+1: this pixel's
+// sample -> neighbour m) its sample; each job's contribution and q ride in its ray's
+// result slot.  Called by every lane of the wave (wave_alloc).
+template <bool BACKWARD>
+__device__ __forceinline__ void gis_pixel_jobs(const Scene &sc, const Seg &g, const GiArgs &A, bool valid, uint32_t x,
+                                               uint32_t y, uint32_t pix, const Compact &x1) {
+    uint32_t seed = valid ? gi_seed(sc, x, y, SALT_GI_SPATIAL) : 0u;
+    bool own_ok = false;
+    GiDomain D{};
+    GiSample S{};
+    if (valid && !BACKWARD) D = gi_domain(sc, x, y, x1);
+    if (valid && BACKWARD) {
+        const uint4 *rc = A.cur + 4u * (size_t)pix;
+        own_ok = rc[2].w != 0u && luminance(ld3(rc[3])) > 0.0f;
+        if (own_ok) S = gi_sample(sc, rc);
+    }
+    for (uint32_t m = 0; m < A.neighbors; ++m) {  // uniform
+        const uint32_t jid = pix * A.jpp + 2u * m + (BACKWARD ? 1u : 0u);
+        bool ray = false;
         f3 f{}, o{}, dir{};
         float qv = 0.0f, remain = 0.0f;
-        if (q < np && tile_xy(sc, q, x, y)) {
-            const uint32_t pix = (y - sc.row_begin) * sc.width + x;
-            jid = pix * jpp + slot;
-            const Compact x1 = gdecode(A.gbuf[pix]);
-            if (x1.valid) {
-                job = true;
-                uint32_t seed = gi_seed(sc, x, y, SALT_GI_SPATIAL), nx = 0u, ny = 0u;
-                bool present = false;
-                for (uint32_t kk = 0; kk <= m; ++kk) present = gi_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
-                const int32_t nidx = present ? gi_band_index(sc, nx, ny) : 0;
-                Compact xn{};
-                if (present) {
-                    xn = gdecode(A.gbuf[nidx]);
-                    present = xn.valid != 0u;
-                }
-                if (present && !backward) {
-                    const uint4 *rn = A.cur + 4 * (ptrdiff_t)nidx;
-                    if (luminance(ld3(rn[3])) > 0.0f) ray = gi_shift_begin(sc, x, y, x1, rn, f, qv, o, dir, remain);
-                } else if (present) {
-                    const uint4 *rc = A.cur + 4u * (size_t)pix;
-                    if (rc[2].w != 0u && luminance(ld3(rc[3])) > 0.0f)
-                        ray = gi_shift_begin(sc, nx, ny, xn, rc, f, qv, o, dir, remain);
-                }
+        if (valid) {
+            uint32_t nx = 0u, ny = 0u;
+            bool present = gi_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+            const int32_t nidx = present ? gi_band_index(sc, nx, ny) : 0;
+            Compact xn{};
+            if (present) {
+                xn = gdecode(A.gbuf[nidx]);
+                present = xn.valid != 0u;
+            }
+            if (BACKWARD) {
+                if (present && own_ok) ray = gi_shift_begin(gi_domain(sc, nx, ny, xn), S, f, qv, o, dir, remain);
+            } else if (present) {  // (the neighbour's confidence is >= 1: it has a G-buffer hit)
+                const uint4 *rn = A.cur + 4 * (ptrdiff_t)nidx;
+                if (luminance(ld3(rn[3])) > 0.0f) ray = gi_shift_begin(D, gi_sample(sc, rn), f, qv, o, dir, remain);
             }
         }
         const uint32_t idx = g.rbase + wave_alloc(g.l_ray, ray ? 1u : 0u);
@@ -314,7 +326,28 @@ void wgis_start(Scene sc, WaveBufs w, GiArgs A) {
             g.res_out[2u * idx] = make_float4(0.0f, f.x, f.y, f.z);
             g.res_out[2u * idx + 1u] = make_float4(qv, 0.0f, 0.0f, 0.0f);
         }
-        if (job) A.jray[jid] = ray ? idx : GI_NO_RAY;
+        if (valid) A.jray[jid] = ray ? idx : GI_NO_RAY;
+    }
+}
+
+#ifndef GIS_START_WAVES
+#define GIS_START_WAVES 3  // 3: 168 VGPRs, 12 B/lane spilled; 4: 128 VGPRs, 148 B spilled
+#endif
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(GIS_START_WAVES, 8)))
+void wgis_start(Scene sc, WaveBufs w, GiArgs A) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    const uint32_t np = padded_pixels(sc);
+    for (uint32_t base = 0; base < w.seg_px * 2u; base += WB) {  // workgroup-uniform: kind, then pixels
+        const uint32_t q = seg_pixel(w, g.j, base % w.seg_px);
+        uint32_t x = 0u, y = 0u, pix = 0u;
+        Compact x1{};
+        if (q < np && tile_xy(sc, q, x, y)) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            x1 = gdecode(A.gbuf[pix]);
+        }
+        if (base >= w.seg_px) gis_pixel_jobs<true>(sc, g, A, x1.valid != 0u, x, y, pix, x1);
+        else gis_pixel_jobs<false>(sc, g, A, x1.valid != 0u, x, y, pix, x1);
     }
     seg_end(w, g);
 }
