@@ -277,9 +277,32 @@ __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, Pa
 // ANY (occlusion queries): stop at the first accepted hit, position not reconstructed.
 // Until that hit the visit order -- and the bound t_max -- are the closest-hit walk's, so
 // "some hit with t <= t_max" comes out exactly when the closest hit has t <= t_max.
-template <bool COUNT, bool PROF = false, bool ROOTQ = true, bool ANY = false>
+// COOP (`coop` = this wave's LDS scratch, used when the whole wave entered): the leaves the
+// lanes hold after a node phase are tested by the whole wave -- their triangles are dealt
+// out 64 at a time, each lane testing one (lane, triangle) pair with the owning lane's ray
+// and bound.  A leaf's sequential loop (`if (best < t) continue`: ties replace) ends with the
+// minimum accepted t and the LAST triangle reaching it, which is exactly a min over the key
+// (t bits, ~k) -- t > 0, so its bits order like the floats -- taken with an LDS atomic per
+// owner.  Every lane's own walk (pops, pushes, bound, counts) is unchanged; a NaN t (which
+// the sequential loop accepts and then poisons the bound with) sends the phase through the
+// sequential loop instead.  Cross-lane data moves only through shuffles and LDS atomics
+// (atomic loads / stores for the keys: plain accesses would let the compiler assume no
+// other lane writes them).
+struct CoopLds { unsigned long long *key; };  // 64 entries per wave
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t &total) {
+    const uint32_t lane = __lane_id();
+    uint32_t incl = v;
+    for (uint32_t o = 1u; o < 64u; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    total = __shfl(incl, 63);
+    return incl - v;
+}
+template <bool COUNT, bool PROF = false, bool ROOTQ = true, bool ANY = false, bool COOP = false>
 __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *subs, const Inst *insts, Ray ray,
-                                              PassEps eps, uint32_t *stack, uint32_t stride, float t_max = 1e10f) {
+                                              PassEps eps, uint32_t *stack, uint32_t stride, float t_max = 1e10f,
+                                              CoopLds coop = CoopLds{nullptr}) {
     Prof pf{};
     Hit best;
     best.valid = false;
@@ -290,6 +313,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     float vy = t_max;  // 1e10 in the reference; a smaller bound only prunes hits beyond it
     uint32_t n_aabb = 0, n_tri = 0;
     bool stop = false;
+    const bool wave_coop = COOP && !ANY && __ballot(1) == ~0ull;  // wave-uniform
     for (uint32_t ii = 0; ii < sc.n_inst && !stop; ++ii) {
         const Inst &I = insts[ii];
         if (PROF) pf.hit(PROF_INST);
@@ -369,8 +393,61 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                         sp += 1;
                     }
                 }
+                // (the whole wave must be here: after a NaN fallback lanes leave one by one)
+                if (wave_coop && __ballot(1) == ~0ull) {  // a wave-uniform leaf phase
+                    if (__ballot(leaf != 0u) == 0ull) break;
+                    if (PROF) pf.hit(PROF_LEAF);
+                    const uint32_t lane = __lane_id();
+                    const uint32_t cnt = leaf ? (leaf >> 24) & 0x7Fu : 0u, lfirst = leaf & LEAF_FIRST_MASK;
+                    uint32_t total;
+                    const uint32_t excl = wave_excl_sum(cnt, total);
+                    __hip_atomic_store(&coop.key[lane], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (compiler order; one wave's LDS ops run in order)
+                    bool nan_seen = false;
+                    for (uint32_t c0 = 0; c0 < total; c0 += 64u) {
+                        const uint32_t u = c0 + lane;
+                        // owner of triangle u = the last lane whose exclusive count is <= u
+                        // (it holds a nonempty leaf: the next lane's count start is > u)
+                        int owner = 0;
+                        for (int step = 32; step >= 1; step >>= 1) {
+                            const uint32_t e = __shfl(excl, owner + step);
+                            if (e <= u) owner += step;
+                        }
+                        const uint32_t o_excl = __shfl(excl, owner), o_first = __shfl(lfirst, owner);
+                        const f3 olo = mk(__shfl(lo.x, owner), __shfl(lo.y, owner), __shfl(lo.z, owner));
+                        const f3 old = mk(__shfl(ld.x, owner), __shfl(ld.y, owner), __shfl(ld.z, owner));
+                        const float ovy = __shfl(vy, owner);
+                        if (u < total) {
+                            if (PROF) pf.hit(PROF_TRI);
+                            const uint32_t k = u - o_excl;
+                            const float4 *tp = tris + 3u * (o_first + k);
+                            const float t = ray_tri(olo, old, tp[0], tp[1], tp[2], eps.det_eps);
+                            if (t != t) nan_seen = true;
+                            else if (!(ovy < t))
+                                atomicMin(&coop.key[owner], ((unsigned long long)__float_as_uint(t) << 32) |
+                                                                (unsigned long long)(0xffffffffu - k));
+                        }
+                    }
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    if (__ballot(nan_seen) == 0ull) {
+                        if (leaf) {
+                            const unsigned long long key =
+                                __hip_atomic_load(&coop.key[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                            n_tri += cnt;
+                            if (key != ~0ull) {
+                                vy = __uint_as_float((uint32_t)(key >> 32));
+                                best.valid = true;
+                                best.s.inst = ii;
+                                best.s.mat = grp;
+                                best.s.prim = lfirst + (0xffffffffu - (uint32_t)key);
+                            }
+                            leaf = 0u;
+                        }
+                        continue;
+                    }
+                }
                 if (leaf == 0u) break;  // roots and stack exhausted
-                if (PROF) pf.hit(PROF_LEAF);
+                if (PROF && !wave_coop) pf.hit(PROF_LEAF);
                 const uint32_t first = leaf & LEAF_FIRST_MASK;
                 const uint32_t count = (leaf >> 24) & 0x7Fu;
                 leaf = 0u;

@@ -38,6 +38,9 @@ namespace ptx {
 // several equal-t triangles wins -- unchanged for every hit inside the cap.
 // OCC: every query of the launch is Q_OCC (the GI shift's binary visibility): an any-hit
 // walk (trace_core_tab ANY), exact for "is there a hit with t <= remain".
+#ifndef TRACE_COOP
+#define TRACE_COOP true
+#endif
 template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true, bool OCC = false>
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
@@ -45,6 +48,8 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     uint32_t *stack = wstack + threadIdx.x;
     __shared__ SubRoot l_subs[LDS_TABLES ? kLdsSubs : 1];
     __shared__ Inst l_insts[LDS_TABLES ? kLdsInsts : 1];
+    __shared__ unsigned long long c_key[WB];
+    const CoopLds coop{c_key + (threadIdx.x & ~63u)};
     if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
     const SubRoot *subs = LDS_TABLES ? l_subs : sc.subs;
     const Inst *insts = LDS_TABLES ? l_insts : sc.insts;
@@ -61,8 +66,8 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         // one trace site, looped, so the traversal code is emitted once
         float T = 1.0f, remain = a.w;
         for (uint32_t it = 0u;; ++it) {
-            const Hit h = trace_core_tab<COUNT, PROF, true, OCC>(sc, subs, insts, r, eps, stack, WB,
-                                                                 vis ? fminf(remain, 1e10f) : 1e10f);
+            const Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP>(sc, subs, insts, r, eps, stack, WB,
+                                                                             vis ? fminf(remain, 1e10f) : 1e10f, coop);
             if (!vis) {
                 const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
                 res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);

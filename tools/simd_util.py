@@ -24,16 +24,18 @@ REGIONS = ["inst", "root", "node", "leaf", "tri"]
 ORDER = {"root": 0, "node": 1, "leaf": 2, "tri": 3, "inst": 4}
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--workload", default="restir", choices=["restir", "mcpt"])
+ap.add_argument("--workload", default="restir", choices=["restir", "mcpt", "reuse"])
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 args = ap.parse_args()
-cs = compile_scene("dummy_scene_1")
+cs = compile_scene("c3_interior_32" if args.workload == "reuse" else "dummy_scene_1")
 r = Renderer(args.width, args.height, device=0, pipeline=args.workload, count_work=True)
 r.Initialize(cs)
 r.Update()
-passes = [("gbuffer", N.PTX_PASS_GBUFFER), ("init", N.PTX_PASS_INIT), ("final", N.PTX_PASS_FINAL)] \
-    if args.workload == "restir" else [("mcpt", N.PTX_PASS_MCPT)]
+passes = {"restir": [("gbuffer", N.PTX_PASS_GBUFFER), ("init", N.PTX_PASS_INIT), ("final", N.PTX_PASS_FINAL)],
+          "reuse": [("gbuffer", N.PTX_PASS_GBUFFER), ("init", N.PTX_PASS_INIT), ("temporal", N.PTX_PASS_TEMPORAL),
+                    ("spatial", N.PTX_PASS_SPATIAL), ("final", N.PTX_PASS_FINAL)],
+          "mcpt": [("mcpt", N.PTX_PASS_MCPT)]}[args.workload]
 for name, pid in passes:
     r.reset_stats()
     r.run_pass(pid)
