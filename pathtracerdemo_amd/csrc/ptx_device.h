@@ -313,8 +313,9 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     float vy = t_max;  // 1e10 in the reference; a smaller bound only prunes hits beyond it
     uint32_t n_aabb = 0, n_tri = 0;
     bool stop = false;
-    const bool wave_coop = COOP && !ANY && __ballot(1) == ~0ull;  // wave-uniform
-    for (uint32_t ii = 0; ii < sc.n_inst && !stop; ++ii) {
+    const bool wave_coop = COOP && __ballot(1) == ~0ull;  // wave-uniform
+    // (with COOP an occluded lane keeps iterating, without work, so the wave stays whole)
+    for (uint32_t ii = 0; ii < sc.n_inst && (COOP || !stop); ++ii) {
         const Inst &I = insts[ii];
         if (PROF) pf.hit(PROF_INST);
         // TransformRayWithMat4x4(InRay, M^-1, false), SH/PT_1_InitPass.wgsl:486-496
@@ -326,16 +327,18 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
         const SubRoot *roots = subs + I.sub_base;
         const float4 *tris = sc.tris + 3u * I.tri_base;
         n_aabb += nsub;  // the reference tests every sub-mesh root once
-        for (uint32_t s0 = 0; s0 < nsub && !stop; s0 += 32u) {
+        for (uint32_t s0 = 0; s0 < nsub && (COOP || !stop); s0 += 32u) {
             const uint32_t nc = nsub - s0 < 32u ? nsub - s0 : 32u;
             // Coherent pre-filter: every root against the best t at this point.  The
             // reference tests root s against the best t after roots < s (never larger), so
             // this keeps every root it enters; the exact test is repeated when the root is
             // taken below, with the then-current best -- the reference's own test.
 #pragma unroll 1
-            for (uint32_t kk = 0; kk < (ROOTQ ? 1u : nc) && !stop; ++kk) {
+            for (uint32_t kk = 0; kk < (ROOTQ ? 1u : nc) && (COOP || !stop); ++kk) {
             uint32_t mask = 0u;
-            if (ROOTQ) {
+            if (stop) {
+                // occluded (ANY): nothing more to test
+            } else if (ROOTQ) {
 #pragma unroll 1
                 for (uint32_t k = 0; k < nc; ++k) {
                     if (PROF) pf.hit(PROF_ROOT);
@@ -440,6 +443,11 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                                 best.s.inst = ii;
                                 best.s.mat = grp;
                                 best.s.prim = lfirst + (0xffffffffu - (uint32_t)key);
+                                if (ANY) {  // occluded: no more work for this lane
+                                    stop = true;
+                                    sp = -1;
+                                    mask = 0u;
+                                }
                             }
                             leaf = 0u;
                         }
