@@ -366,9 +366,13 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                         mask &= mask - 1u;
                         const SubRoot &R = roots[s0 + k];
                         if ((ROOTQ && vy == vy_pf) || box_root(lo, inv, R, vx, vy)) {
+                            grp = s0 + k;
+                            if (R.ref & LEAF_BIT) {  // a one-leaf root: its push + pop, folded
+                                leaf = R.ref;
+                                break;
+                            }
                             stack[0] = R.ref;
                             sp = 0;
-                            grp = s0 + k;
                         }
                         continue;
                     }
