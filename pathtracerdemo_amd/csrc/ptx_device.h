@@ -485,13 +485,14 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
             }  // roots (ROOTQ: one queue per chunk of 32; else one root at a time)
         }
     }
-    if (PROF) {
+    const bool counted = t_max == t_max;  // a NaN bound: an idle lane keeping its wave whole
+    if (PROF && counted) {
         for (int r = 0; r < PROF_REGIONS; ++r) {
             if (pf.wave[r]) atomicAdd(&sc.counters[8 + 2 * r], (unsigned long long)pf.wave[r]);
             if (pf.lane[r]) atomicAdd(&sc.counters[9 + 2 * r], (unsigned long long)pf.lane[r]);
         }
     }
-    if (COUNT) {
+    if (COUNT && counted) {
         atomicAdd(&sc.counters[CNT_RAYS], 1ull);
         atomicAdd(&sc.counters[CNT_INST], (unsigned long long)sc.n_inst);
         atomicAdd(&sc.counters[CNT_AABB], (unsigned long long)n_aabb);

@@ -57,8 +57,17 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     const uint32_t n = w.cnt[(2u * round + 1u) * w.nseg + j];
     const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
     float4 *res = w.res[round & 1u] + 2u * (size_t)j * w.ray_stride;
-    for (uint32_t i = threadIdx.x; i < n; i += WB) {
-        const float4 a = rays[2u * i], b = rays[2u * i + 1u];
+    // Every lane of the wave calls the traversal every time -- lanes without a query (past
+    // the segment's end, or whose Visibility walk is over) with a NaN bound, which no box
+    // overlaps -- so the whole wave takes part in the cooperative leaf phases.
+    for (uint32_t i0 = 0; i0 < n; i0 += WB) {  // workgroup-uniform
+        const uint32_t i = i0 + threadIdx.x;
+        bool active = i < n;
+        float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+        if (active) {
+            a = rays[2u * i];
+            b = rays[2u * i + 1u];
+        }
         Ray r{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)};
         const uint32_t kind = asu(b.w);
         const bool vis = kind != Q_CLOSEST;
@@ -66,30 +75,33 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         // one trace site, looped, so the traversal code is emitted once
         float T = 1.0f, remain = a.w;
         for (uint32_t it = 0u;; ++it) {
-            const Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP>(sc, subs, insts, r, eps, stack, WB,
-                                                                             vis ? fminf(remain, 1e10f) : 1e10f, coop);
-            if (!vis) {
+            const float t_max = !active ? __builtin_nanf("") : vis ? fminf(remain, 1e10f) : 1e10f;
+            const Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP>(sc, subs, insts, r, eps, stack, WB, t_max,
+                                                                             coop);
+            if (active && !vis) {
                 const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
                 res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
                 res[2u * i + 1u] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
-                break;
-            }
-            float out = -1.0f;
-            if (!h.valid || h.t > remain) out = T;
-            else {
-                const float tr = kind == Q_OCC ? 0.0f : get_transmission(sc, h.s.inst, h.s.mat);
-                if (tr == 0.0f) out = 0.0f;
+                active = false;
+            } else if (active) {
+                float out = -1.0f;
+                if (!h.valid || h.t > remain) out = T;
                 else {
-                    T *= tr;
-                    remain -= h.t;
-                    r.o = h.pos;
-                    if (it == 4u) out = 0.0f;  // Visibility gives up after 5 segments
+                    const float tr = kind == Q_OCC ? 0.0f : get_transmission(sc, h.s.inst, h.s.mat);
+                    if (tr == 0.0f) out = 0.0f;
+                    else {
+                        T *= tr;
+                        remain -= h.t;
+                        r.o = h.pos;
+                        if (it == 4u) out = 0.0f;  // Visibility gives up after 5 segments
+                    }
+                }
+                if (out >= 0.0f) {  // only res.x is written: .yzw and res[2i+1] carry the payload
+                    res[2u * i].x = out;
+                    active = false;
                 }
             }
-            if (out >= 0.0f) {  // only res.x is written: .yzw and res[2i+1] carry the payload
-                res[2u * i].x = out;
-                break;
-            }
+            if (__ballot(active) == 0ull) break;
         }
     }
 }
