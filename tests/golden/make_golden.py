@@ -50,10 +50,16 @@ def frame_fixture(cs, frames):
     for f in range(1, REUSE_FRAMES + 1):
         ru.set_frame_index(f)
         ru.run_reuse_frame(threads=1)
+    # the build-defined ReSTIR GI pipeline, default parameters, 3 frames
+    gi = O.Frame(uniform_for(cs, W, H, 1), cs.scene, cs.geometry, cs.accel)
+    for f in range(1, REUSE_FRAMES + 1):
+        gi.set_frame_index(f)
+        gi.run_gi_frame(threads=1)
     return dict(uniform=fr.uniform, gbuffer=fr.gbuffer, reservoir=fr.reservoir, accum_restir=fr.accum,
                 accum_mcpt=mc.accum, frames=np.int32(frames), scene_sha256=scene_digest(cs),
                 accum_reuse=ru.accum, hist_reuse=ru.res_hist, reuse_frames=np.int32(REUSE_FRAMES),
-                reuse_params=np.array(ru.reuse, dtype=np.int32))
+                reuse_params=np.array(ru.reuse, dtype=np.int32),
+                accum_gi=gi.accum, hist_gi=gi.gi_hist, direct_gi=gi.direct)
 
 
 def kat_table():
