@@ -389,16 +389,14 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                     bool hl, hr;
                     box_pair(lo, inv, q0, q1, q2, vx, vy, hl, hr, tl, tr);
                     n_aabb += 2;
-                    if (hl && hr) {
-                        uint32_t first = tl < tr ? rref : lref;
-                        uint32_t second = tl < tr ? lref : rref;
-                        stack[(uint32_t)(sp + 1) * stride] = first;
-                        stack[(uint32_t)(sp + 2) * stride] = second;
-                        sp += 2;
-                    } else if (hl || hr) {
-                        stack[(uint32_t)(sp + 1) * stride] = hl ? lref : rref;
-                        sp += 1;
-                    }
+                    // branch-free pushes: both entries are written, the stack pointer moves by
+                    // the number of hits (entries above the top are never read; the slots are
+                    // the two-hit case's, within the max_depth + 2 entries per lane)
+                    const bool both = hl && hr;
+                    const uint32_t near = tl < tr ? lref : rref, far = tl < tr ? rref : lref;
+                    stack[(uint32_t)(sp + 1) * stride] = both ? far : (hl ? lref : rref);
+                    stack[(uint32_t)(sp + 2) * stride] = near;
+                    sp += both ? 2 : ((hl || hr) ? 1 : 0);
                 }
                 // (the whole wave must be here: after a NaN fallback lanes leave one by one)
                 if (wave_coop && __ballot(1) == ~0ull) {  // a wave-uniform leaf phase
