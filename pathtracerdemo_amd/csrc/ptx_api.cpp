@@ -511,6 +511,7 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
             if (passes[i] == PTX_PASS_GBUFFER) {
                 TimedLaunch *t = event_begin(h, PTX_PASS_GBUFFER, st);
                 e = wave_gbuffer(sc, part, gbuf_band(h), h->stack_depth, st);
+                h->init_state_valid = false;  // PT_1's state described the previous G-buffer
                 event_end(t, st);
             } else {
                 e = launch_wave_seq(h, sc, part, passes[i], st);
@@ -623,7 +624,10 @@ static int timed_launch(ptx_handle *h, int pass) {
         return PTX_OK;
     }
     switch (pass) {
-    case PTX_PASS_GBUFFER: e = launch_gbuffer(sc, gbuf_band(h), d, h->stream); break;
+    case PTX_PASS_GBUFFER:
+        e = launch_gbuffer(sc, gbuf_band(h), d, h->stream);
+        h->init_state_valid = false;
+        break;
     case PTX_PASS_INIT:
         e = variant == 0   ? launch_init_tiled(sc, gb, res, d, h->stream)
             : variant == 1 ? launch_init_persistent(sc, gb, res, ctr, d, h->stream)
