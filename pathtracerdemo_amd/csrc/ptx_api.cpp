@@ -480,11 +480,12 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
 // (fork/join through events on the handle's stream), so one part's latency-bound traces
 // overlap another's ALU-bound shading and trace tails.  Each part runs `passes` in order
 // over its own segments (a frame: G-buffer -> init -> final per part, nothing shared).
-// PTX_WAVE_STREAMS=1..4 overrides K (A/B; 2 measured best, 4 oversubscribes the queues).
+// PTX_WAVE_STREAMS=1..4 overrides K (A/B: 3 measured best since the cooperative traversal,
+// +2.5 % over 2 on reuse / ReSTIR; 4 oversubscribes the 4 hardware queues).
 static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes,
                                    int npasses) {
     static const int env_k = getenv("PTX_WAVE_STREAMS") ? atoi(getenv("PTX_WAVE_STREAMS")) : 0;
-    int k = env_k > 0 ? env_k : 2;
+    int k = env_k > 0 ? env_k : 3;
     if (h->cfg.flags & PTX_FLAG_SINGLE_STREAM) k = 1;
     k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
     if ((uint32_t)k > w.nseg) k = (int)w.nseg;
