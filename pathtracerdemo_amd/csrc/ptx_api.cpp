@@ -50,7 +50,7 @@ struct ptx_handle {
     std::vector<uint32_t> scene, geometry, accel;
     DevBuf d_scene, d_geometry;
     // derived MI355X layout
-    DevBuf d_tris, d_nodes, d_subs, d_insts;
+    DevBuf d_tris, d_nodes, d_subs, d_insts, d_mats;
     uint32_t n_tris = 0, n_nodes = 0, n_inst = 0, n_subs = 0, max_depth = 0, stack_depth = 0;
     uint32_t layout_key[8] = {0};
     bool layout_valid = false;
@@ -163,6 +163,7 @@ static int build_layout(ptx_handle *h) {
     std::vector<SubRoot> subs;
     std::vector<NodePair> nodes;
     std::vector<float> tris;  // 12 floats per triangle
+    std::vector<float> mats;  // 8 floats per sub-mesh, in SubRoot order (Scene::mats)
     std::vector<uint32_t> mesh_sub_base(n_mesh), mesh_nsub(n_mesh), mesh_tri_base(n_mesh);
     uint32_t max_depth = 0;
 
@@ -172,6 +173,17 @@ static int build_layout(ptx_handle *h) {
         mesh_sub_base[m] = (uint32_t)subs.size();
         mesh_nsub[m] = nsub;
         mesh_tri_base[m] = (uint32_t)(tris.size() / 12);
+        // GetMaterial (SH/PT_1_InitPass.wgsl:285-314) per sub-mesh: material d[2] + 15*sub.  A record
+        // past the scene buffer reads as zeros (WebGPU's robust buffer access would clamp or zero).
+        for (uint32_t s = 0; s < nsub; ++s) {
+            const size_t mi = (size_t)off_mat + d[2] + (size_t)STRIDE_MATERIAL * s;
+            auto word = [&](uint32_t k) { return mi + k < S.size() ? as_f32(S[mi + k]) : 0.0f; };
+            const float trans = word(10);
+            const bool yellow = trans > 0.0f;
+            const float rec[8] = {yellow ? 1.0f : word(0), yellow ? 1.0f : word(1), yellow ? 0.0f : word(2), word(8),
+                                  std::fmax(word(9), 0.01f), trans, word(11), 0.0f};
+            mats.insert(mats.end(), rec, rec + 8);
+        }
         uint32_t mesh_tris = 0;
         struct Pending { uint32_t base; std::vector<uint32_t> order; };
         std::vector<Pending> per_sub;
@@ -263,12 +275,13 @@ static int build_layout(ptx_handle *h) {
     if (tris.empty()) tris.resize(12, 0.0f);
     if (nodes.empty()) nodes.resize(1);
     if (subs.empty()) subs.resize(1);
+    if (mats.empty()) mats.resize(8, 0.0f);
     if (int rc = upload(h, h->d_tris, tris.data(), tris.size() * sizeof(float))) return rc;
     if (int rc = upload(h, h->d_nodes, nodes.data(), nodes.size() * sizeof(NodePair))) return rc;
     if (int rc = upload(h, h->d_subs, subs.data(), subs.size() * sizeof(SubRoot))) return rc;
     h->n_subs = (uint32_t)subs.size();
     if (int rc = upload(h, h->d_insts, insts.data(), std::max<size_t>(1, insts.size()) * sizeof(Inst))) return rc;
-    (void)off_mat;
+    if (int rc = upload(h, h->d_mats, mats.data(), mats.size() * sizeof(float))) return rc;
     h->n_tris = (uint32_t)(tris.size() / 12);
     h->n_nodes = (uint32_t)nodes.size();
     h->n_inst = n_inst;
@@ -289,6 +302,7 @@ static Scene make_scene(ptx_handle *h) {
     sc.nodes = (const NodePair *)h->d_nodes.p;
     sc.subs = (const SubRoot *)h->d_subs.p;
     sc.insts = (const Inst *)h->d_insts.p;
+    sc.mats = (const float4 *)h->d_mats.p;
     sc.n_inst = h->n_inst;
     sc.n_subs = h->n_subs;
     sc.width = h->cfg.width;
@@ -928,7 +942,7 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
     out->instances = h->n_inst;
     out->max_bvh_depth = h->max_depth;
     out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
-                        h->d_subs.bytes + h->d_insts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
+                        h->d_subs.bytes + h->d_insts.bytes + h->d_mats.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
                         h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_direct.bytes;
     return PTX_OK;
 }
@@ -1025,7 +1039,7 @@ int ptx_destroy(ptx_handle *h) {
         if (t.start) (void)hipEventDestroy(t.start);
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
-    for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_gbuf,
+    for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
                       &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_direct})

@@ -73,6 +73,7 @@ struct Scene {
     const NodePair *nodes;
     const SubRoot *subs;
     const Inst *insts;
+    const float4 *mats;   // 2 float4 per sub-mesh (SubRoot numbering): GetMaterial, pre-applied
     uint32_t n_inst, n_subs;
     uint32_t width, height, row_begin, row_end;
     unsigned long long *counters;  // nullptr unless PTX_FLAG_COUNT_WORK

@@ -66,7 +66,7 @@ __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, ui
     s.matref = asu(cu.w);
     s.cur.pos = mk(cu.x, cu.y, cu.z);
     s.cur.nrm = mk(nr.x, nr.y, nr.z);
-    s.cur.mat = get_material(sc, desc_ptr(sc, sc.insts[s.matref >> 16].mesh), s.matref & 0xffffu);
+    s.cur.mat = material_at(sc, s.matref);
     s.beta = nr.w;
     s.prev = mk(pv.x, pv.y, pv.z); s.rr_p = pv.w;
     s.rr_f = mk(rf.x, rf.y, rf.z);
@@ -94,7 +94,7 @@ __device__ __forceinline__ bool job_begin(const Scene &sc, const ReuseArgs &A, J
     s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
     s.prev = x0_of(sc, x, y);
     s.cur = get_surface(sc, x1);
-    s.matref = (x1.inst << 16) | x1.mat;
+    s.matref = mat_index(sc, x1.inst, x1.mat);
     s.beta = 1.0f; s.rr_p = 1.0f; s.rr_f = mk(1.0f, 1.0f, 1.0f);
     return true;
 }
@@ -173,7 +173,7 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
                     s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
                     s.prev = s.cur.pos;
                     s.cur = next;
-                    s.matref = (h.s.inst << 16) | h.s.mat;
+                    s.matref = mat_index(sc, h.s.inst, h.s.mat);
                     s.i += 1u;
                     emit = true;
                 }
@@ -342,8 +342,8 @@ __device__ __forceinline__ int32_t band_index(const Scene &sc, uint32_t x, uint3
 }
 
 // job_begin with the domain's camera point and hit surface already at hand
-__device__ __forceinline__ bool job_begin_at(const ReuseArgs &A, Job &s, f3 x0, const Surface &X1, const Compact &x1,
-                                             int32_t ref) {
+__device__ __forceinline__ bool job_begin_at(const Scene &sc, const ReuseArgs &A, Job &s, f3 x0, const Surface &X1,
+                                             const Compact &x1, int32_t ref) {
     const uint4 *rv = res_at(A.cur, ref);
     const uint32_t C = rv[7].y, length = rv[5].w;
     if (!x1.valid || C == 0u || length < 2u) return false;
@@ -351,7 +351,7 @@ __device__ __forceinline__ bool job_begin_at(const ReuseArgs &A, Job &s, f3 x0, 
     s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
     s.prev = x0;
     s.cur = X1;
-    s.matref = (x1.inst << 16) | x1.mat;
+    s.matref = mat_index(sc, x1.inst, x1.mat);
     s.beta = 1.0f; s.rr_p = 1.0f; s.rr_f = mk(1.0f, 1.0f, 1.0f);
     return true;
 }
@@ -402,7 +402,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 if (present && !backward) {  // the neighbour's sample in this pixel's domain
                     const uint4 *rn = res_at(A.cur, nidx);
                     want = rn[5].w >= 2u && asf(rn[6].x) > 0.0f;
-                    act = want && job_begin_at(A, s, x0, X1, x1, nidx);
+                    act = want && job_begin_at(sc, A, s, x0, X1, x1, nidx);
                 } else if (present) {  // this pixel's sample in the neighbour's domain
                     const uint4 *rc = A.cur + 8u * (size_t)pix;
                     want = rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;

@@ -9,21 +9,24 @@ namespace ptx {
 struct Material { f3 albedo; float metal, rough, trans, ior; };
 struct Surface { f3 pos, nrm; Material mat; };
 
-// GetMaterial (SH/PT_1_InitPass.wgsl:285-314): transmissive -> yellow albedo, roughness >= 0.01
-__device__ __forceinline__ Material get_material(const Scene &sc, const uint32_t *desc, uint32_t mid) {
-    const uint32_t *p = sc.S + sc.U[U_OFF_MAT] + desc[2] + STRIDE_MATERIAL * mid;
+// GetMaterial (SH/PT_1_InitPass.wgsl:285-314): transmissive -> yellow albedo, roughness >= 0.01.
+// Applied once per sub-mesh on the host (ptx_api.cpp build_layout) into Scene::mats, indexed
+// by the flat sub-mesh number Inst::sub_base + sub: one load instead of inst -> desc -> material.
+__device__ __forceinline__ uint32_t mat_index(const Scene &sc, uint32_t inst, uint32_t sub) {
+    return sc.insts[inst].sub_base + sub;
+}
+__device__ __forceinline__ Material material_at(const Scene &sc, uint32_t flat) {
+    const float4 a = sc.mats[2u * flat], b = sc.mats[2u * flat + 1u];
     Material m;
-    m.albedo = mk(asf(p[0]), asf(p[1]), asf(p[2]));
-    m.metal = asf(p[8]);
-    m.rough = fmaxf(asf(p[9]), 0.01f);
-    m.trans = asf(p[10]);
-    m.ior = asf(p[11]);
-    if (m.trans > 0.0f) m.albedo = mk(1.0f, 1.0f, 0.0f);
+    m.albedo = mk(a.x, a.y, a.z);
+    m.metal = a.w;
+    m.rough = b.x;
+    m.trans = b.y;
+    m.ior = b.z;
     return m;
 }
 __device__ __forceinline__ float get_transmission(const Scene &sc, uint32_t inst, uint32_t mid) {
-    const uint32_t *desc = desc_ptr(sc, sc.insts[inst].mesh);
-    return asf(sc.S[sc.U[U_OFF_MAT] + desc[2] + STRIDE_MATERIAL * mid + 10u]);
+    return sc.mats[2u * mat_index(sc, inst, mid) + 1u].y;
 }
 
 // GetSurface (SH/PT_1_InitPass.wgsl:438-467) with GetTriangleWorldSpace (:390-407)
@@ -31,7 +34,7 @@ __device__ __forceinline__ Surface get_surface(const Scene &sc, Compact x) {
     const Inst &I = sc.insts[x.inst];
     const uint32_t *desc = desc_ptr(sc, I.mesh);
     Surface s;
-    s.mat = get_material(sc, desc, x.mat);
+    s.mat = material_at(sc, I.sub_base + x.mat);
     uint32_t id[3];
     tri_vertex_ids(sc, desc, x.prim, id);
     f3 p0 = xform_point(I.m, vtx_pos(sc, desc, id[0]));
@@ -51,7 +54,7 @@ __device__ __forceinline__ Surface surface_at(const Scene &sc, const Compact &x,
     const Inst &I = sc.insts[x.inst];
     const uint32_t *desc = desc_ptr(sc, I.mesh);
     Surface s;
-    s.mat = get_material(sc, desc, x.mat);
+    s.mat = material_at(sc, I.sub_base + x.mat);
     uint32_t id[3];
     tri_vertex_ids(sc, desc, x.prim, id);
     f3 n0 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[0]));

@@ -669,7 +669,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                     s.ucw = asf(r7.x);
                     s.prev = x0_of(sc, x, y);
                     s.cur = get_surface(sc, x1);
-                    matref = (x1.inst << 16) | x1.mat;
+                    matref = mat_index(sc, x1.inst, x1.mat);
                     s.f = mk(1.0f, 1.0f, 1.0f);
                     s.i = 1u;
                 }
@@ -706,10 +706,9 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                 const float4 pv = state[FS_PREV * npix + pix];
                 s.prev = mk(pv.x, pv.y, pv.z);
                 matref = asu(cu.w);
-                const Inst &I = sc.insts[matref >> 16];
                 s.cur.pos = mk(cu.x, cu.y, cu.z);
                 s.cur.nrm = mk(nr.x, nr.y, nr.z);
-                s.cur.mat = get_material(sc, desc_ptr(sc, I.mesh), matref & 0xffffu);
+                s.cur.mat = material_at(sc, matref);
             }
             if (s.phase == 0u) {  // regenerated vertex i+1 (PT_4:1378-1380) and f over vertex i
                 const Hit h = get_hit(res_in, s.idx);
@@ -719,7 +718,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                 s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
                 s.prev = s.cur.pos;
                 s.cur = next;
-                matref = (h.s.inst << 16) | h.s.mat;
+                matref = mat_index(sc, h.s.inst, h.s.mat);
                 s.i += 1u;
                 emit = true;
             } else {  // light segment's Visibility arrived (PT_4:1332)
