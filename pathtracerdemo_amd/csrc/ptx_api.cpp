@@ -63,7 +63,7 @@ struct ptx_handle {
     uint32_t band_h = 0, halo_top = 0, halo_bot = 0;
     DevBuf d_gbuf, d_res, d_accum, d_counters, d_queue;
     // reuse pipeline: spatial output / history, shift-job state and results
-    DevBuf d_hist, d_jstate, d_jres;
+    DevBuf d_hist, d_jstate, d_jres, d_nbr;
     // reservoir size in uint4 (8: the reference's 128-byte Reservoir; 4: the GI reservoir)
     // and the GI pipeline's per-pixel direct light
     uint32_t res_u4 = 8;
@@ -387,10 +387,14 @@ static void event_end(TimedLaunch *t, hipStream_t st) {
     if (t && hipEventRecord(t->stop, st) == hipSuccess) t->pending = true;
 }
 
+static size_t px_with_halo(const ptx_handle *h) {
+    return (size_t)(h->halo_top + h->band_h + h->halo_bot) * h->cfg.width;
+}
 static int reuse_buffers(ptx_handle *h) {
     const size_t njobs = (size_t)h->band_h * h->cfg.width * 2u * h->reuse_neighbors;
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) return alloc_buf(h, h->d_jres, njobs * 4u);  // ray index per job
     if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
+    if (int rc = alloc_buf(h, h->d_nbr, px_with_halo(h) * 16u)) return rc;
     return alloc_buf(h, h->d_jres, njobs * 16u);
 }
 static ReuseArgs reuse_args(ptx_handle *h, int pass) {
@@ -407,6 +411,7 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.cap = h->temporal_cap;
     A.hist_valid = h->hist_valid ? 1u : 0u;
     A.use_init = (pass == PTX_PASS_TEMPORAL && h->init_state_valid) ? 1u : 0u;
+    A.nbr = (const uint4 *)h->d_nbr.p + (size_t)h->halo_top * h->cfg.width;
     return A;
 }
 
@@ -504,6 +509,15 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
     k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
     if ((uint32_t)k > w.nseg) k = (int)w.nseg;
     hipError_t e = hipSuccess;
+    // the spatial pass gathers neighbours (halo rows included) through their summaries
+    for (int i = 0; i < npasses; ++i)
+        if (passes[i] == PTX_PASS_SPATIAL && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, h->stream);
+            e = wave_reuse_summary((const uint4 *)h->d_gbuf.p, (const uint4 *)h->d_res.p, (uint4 *)h->d_nbr.p,
+                                   px_with_halo(h), h->stream);
+            event_end(t, h->stream);
+            if (e != hipSuccess) return e;
+        }
     if (k > 1) {
         if (!h->ev_fork && (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return e;
         for (int q = 1; q < k; ++q) {
@@ -943,7 +957,7 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
     out->max_bvh_depth = h->max_depth;
     out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
                         h->d_subs.bytes + h->d_insts.bytes + h->d_mats.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
-                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_direct.bytes;
+                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_nbr.bytes + h->d_direct.bytes;
     return PTX_OK;
 }
 
@@ -1042,7 +1056,7 @@ int ptx_destroy(ptx_handle *h) {
     for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
-                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_direct})
+                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_direct})
         free_buf(*b);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

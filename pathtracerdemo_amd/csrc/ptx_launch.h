@@ -88,11 +88,16 @@ struct ReuseArgs {
     uint32_t njobs, jpp;  // jobs of the pass (npix * jpp), jobs per pixel
     uint32_t radius, neighbors, cap, hist_valid;
     uint32_t use_init;  // temporal: this frame's PT_1 wave state (path hits, NEE Visibility) is in w.state
+    const uint4 *nbr;   // spatial: per-pixel neighbour summary (wave_reuse_summary), cur's addressing
 };
 // rounds of {trace, step} between a reuse pass's start and combine launches
 int reuse_rounds(int pass_temporal, const ReuseArgs &A);
 hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,
                             hipStream_t s);
+// Spatial pass prologue over every band + halo pixel (npx of them, from the first halo row):
+// the 16-byte neighbour summary {p_hat, q, W, valid | length | C} the spatial kernels gather
+// instead of a G-buffer line and a reservoir line per neighbour.
+hipError_t wave_reuse_summary(const uint4 *gbuf, const uint4 *res, uint4 *nbr, size_t npx, hipStream_t s);
 
 // ReSTIR GI (ptx_gi.hip; pipeline PTX_PIPELINE_RESTIR_GI): pass 0 init (logic rounds 0..2,
 // traces between), 1 temporal (one launch), 2 spatial (start, trace, combine), 3 final.

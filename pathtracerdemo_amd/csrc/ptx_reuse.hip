@@ -341,13 +341,42 @@ __device__ __forceinline__ int32_t band_index(const Scene &sc, uint32_t x, uint3
     return ((int32_t)y - (int32_t)sc.row_begin) * (int32_t)sc.width + (int32_t)x;
 }
 
-// job_begin with the domain's camera point and hit surface already at hand
+// Neighbour summary (one uint4 per band + halo pixel, written by wnbr_summary before the
+// spatial jobs start): {p_hat (word 24), q (25), W (28), G-buffer valid << 31 | length << 24 |
+// C}, or w = kNbrEscape when length or C does not fit (then read the reservoir itself).  A
+// neighbour costs one 16-byte gather instead of a G-buffer line and a reservoir line.
+constexpr uint32_t kNbrEscape = 0xFFFFFFFFu;
+struct Nbr { bool valid; uint32_t length, C; float p, q, W; };
+__device__ __forceinline__ Nbr nbr_at(const ReuseArgs &A, int32_t idx) {
+    const uint4 v = A.nbr[idx];
+    if (v.w != kNbrEscape)
+        return Nbr{(v.w >> 31) != 0u, (v.w >> 24) & 0x7fu, v.w & 0xffffffu, asf(v.x), asf(v.y), asf(v.z)};
+    const uint4 *rv = res_at(A.cur, idx);
+    const uint4 r5 = rv[5], r6 = rv[6], r7 = rv[7];
+    return Nbr{gdecode(A.gbuf[idx]).valid != 0u, r5.w, r7.y, asf(r6.x), asf(r6.y), asf(r7.x)};
+}
+__global__ __launch_bounds__(WB) void wnbr_summary(const uint4 *gbuf, const uint4 *res, uint4 *nbr, size_t npx) {
+    const size_t i = (size_t)blockIdx.x * WB + threadIdx.x;
+    if (i >= npx) return;
+    const uint4 *rv = res + 8u * i;
+    const uint32_t valid = gbuf[i].x >> 31;
+    const uint4 r5 = rv[5], r6 = rv[6], r7 = rv[7];
+    uint32_t w = 0u;
+    if (valid) w = (r5.w > 0x7fu || r7.y > 0xfffffeu) ? kNbrEscape : (1u << 31) | (r5.w << 24) | r7.y;
+    nbr[i] = make_uint4(r6.x, r6.y, r7.x, w);
+}
+hipError_t wave_reuse_summary(const uint4 *gbuf, const uint4 *res, uint4 *nbr, size_t npx, hipStream_t s) {
+    if (npx == 0) return hipSuccess;
+    hipLaunchKernelGGL(wnbr_summary, dim3((unsigned)((npx + WB - 1) / WB)), dim3(WB), 0, s, gbuf, res, nbr, npx);
+    return hipGetLastError();
+}
+
+// job_begin with the domain's camera point and hit surface and the sample's summary at hand
 __device__ __forceinline__ bool job_begin_at(const Scene &sc, const ReuseArgs &A, Job &s, f3 x0, const Surface &X1,
-                                             const Compact &x1, int32_t ref) {
-    const uint4 *rv = res_at(A.cur, ref);
-    const uint32_t C = rv[7].y, length = rv[5].w;
+                                             const Compact &x1, int32_t ref, const Nbr &nb) {
+    const uint32_t C = nb.C, length = nb.length;
     if (!x1.valid || C == 0u || length < 2u) return false;
-    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = rv[0].y; s.idx = 0u; s.ref = ref;
+    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = res_at(A.cur, ref)[0].y; s.idx = 0u; s.ref = ref;
     s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
     s.prev = x0;
     s.cur = X1;
@@ -393,19 +422,15 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 uint32_t nx = 0u, ny = 0u;
                 bool present = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
                 const int32_t nidx = present ? band_index(sc, nx, ny) : 0;
-                Compact xn{};
-                if (present) {
-                    xn = gdecode(A.gbuf[nidx]);
-                    present = xn.valid != 0u;
-                }
                 bool want = false;
                 if (present && !backward) {  // the neighbour's sample in this pixel's domain
-                    const uint4 *rn = res_at(A.cur, nidx);
-                    want = rn[5].w >= 2u && asf(rn[6].x) > 0.0f;
-                    act = want && job_begin_at(sc, A, s, x0, X1, x1, nidx);
+                    const Nbr nb = nbr_at(A, nidx);
+                    want = nb.valid && nb.length >= 2u && nb.p > 0.0f;
+                    act = want && job_begin_at(sc, A, s, x0, X1, x1, nidx, nb);
                 } else if (present) {  // this pixel's sample in the neighbour's domain
+                    const Compact xn = gdecode(A.gbuf[nidx]);
                     const uint4 *rc = A.cur + 8u * (size_t)pix;
-                    want = rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
+                    want = xn.valid && rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
                     act = want && job_begin(sc, A, s, nx, ny, xn, (int32_t)pix);
                 }
                 if (want && !act) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -445,9 +470,9 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
             uint32_t nx = 0u, ny = 0u;
             float Q = 1.0f;
             if (spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
-                const int32_t nidx = band_index(sc, nx, ny);
-                if (gdecode(A.gbuf[nidx]).valid) {
-                    const uint32_t Cn = res_at(A.cur, nidx)[7].y;
+                const Nbr nb = nbr_at(A, band_index(sc, nx, ny));
+                if (nb.valid) {
+                    const uint32_t Cn = nb.C;
                     Csum += Cn;
                     if (canon_ok) {
                         const float4 B = A.jres[pix * A.jpp + 2u * m + 1u];
@@ -475,13 +500,13 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
             int32_t nidx = 0;
             if (spatial_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
                 nidx = band_index(sc, nx, ny);
-                const uint4 *rn = res_at(A.cur, nidx);
-                const float pn = asf(rn[6].x);
-                if (gdecode(A.gbuf[nidx]).valid && rn[5].w >= 2u && pn > 0.0f) {
+                const Nbr nb = nbr_at(A, nidx);
+                const float pn = nb.p;
+                if (nb.valid && nb.length >= 2u && pn > 0.0f) {
                     const float4 Fr = A.jres[pix * A.jpp + 2u * m];
                     if (Fr.w > 0.0f) {
                         const float2 F = make_float2(luminance(mk(Fr.x, Fr.y, Fr.z)), Fr.w);
-                        const float cn = (float)rn[7].y, qn = asf(rn[6].y), Wn = asf(rn[7].x);
+                        const float cn = (float)nb.C, qn = nb.q, Wn = nb.W;
                         const float J = qn / F.y;
                         const float pb = pn / J;
                         const float den = cc * F.x + Mf * cn * pb;
