@@ -444,55 +444,117 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
 }
 
 // Pairwise-MIS resampling of the pixel's temporal reservoir and its neighbours' shifted
-// samples (oracle spatial_pixel); writes the reservoir PT_4 reads.
-__global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, ReuseArgs A) {
-    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc), M = A.neighbors;
-    for (uint32_t k = 0; k < w.seg_px; k += WB) {
-        const uint32_t q = seg_pixel(w, j, k);
-        uint32_t x, y;
-        if (q >= np || !tile_xy(sc, q, x, y)) continue;
-        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
-        uint4 *out = A.hist + 8u * (size_t)pix;
-        if (!gdecode(A.gbuf[pix]).valid) {
-            for (int t = 0; t < 8; ++t) out[t] = make_uint4(0u, 0u, 0u, 0u);
-            continue;
+// samples (oracle spatial_pixel); writes the reservoir PT_4 reads.  Pass 1 sums the
+// neighbours' confidences and the canonical sample's MIS weight, pass 2 resamples (canonical
+// first; the selection draws follow the offset draws).
+struct CombineCanon { float cc, pc, qc, Wc; bool ok; };
+__device__ __forceinline__ float canon_q(const CombineCanon &c, float Mf, uint32_t Cn, float4 B) {
+    float Q = 1.0f;
+    if (c.ok && B.w > 0.0f) {
+        const float pbc = luminance(mk(B.x, B.y, B.z)) * c.qc / B.w;
+        const float den = c.cc * c.pc + Mf * (float)Cn * pbc;
+        Q = den > 0.0f ? (c.cc * c.pc) / den : 1.0f;
+    }
+    return Q;
+}
+// the neighbour's sample shifted here: resampling weight, p_hat, q, f (zeros if unusable)
+__device__ __forceinline__ float neighbour_weight(const CombineCanon &c, float Mf, const Nbr &nb, float4 Fr, float &pf,
+                                                  float &qf, SelF &fj) {
+    float wn = 0.0f;
+    pf = 0.0f; qf = 0.0f; fj = SelF{false, mk(0.0f, 0.0f, 0.0f)};
+    const float pn = nb.p;
+    if (nb.valid && nb.length >= 2u && pn > 0.0f && Fr.w > 0.0f) {
+        const float2 F = make_float2(luminance(mk(Fr.x, Fr.y, Fr.z)), Fr.w);
+        const float cn = (float)nb.C, qn = nb.q, Wn = nb.W;
+        const float J = qn / F.y;
+        const float pb = pn / J;
+        const float den = c.cc * F.x + Mf * cn * pb;
+        const float mw = den > 0.0f ? (cn * pb) / den : 0.0f;
+        wn = mw * F.x * Wn * J;
+        pf = F.x;
+        qf = F.y;
+        fj = job_f(Fr);
+    }
+    return wn;
+}
+
+// MT = the launch's neighbour count when it is a compile-time constant: every neighbour's
+// summary and job results are gathered up front (one memory round trip instead of 2 MT
+// dependent ones); MT = 0: any count, gathered per neighbour.
+template <uint32_t MT>
+__device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &A, uint32_t x, uint32_t y,
+                                              uint32_t pix) {
+    uint4 *out = A.hist + 8u * (size_t)pix;
+    const uint4 *rc = A.cur + 8u * (size_t)pix;
+    const uint32_t M = MT ? MT : A.neighbors;
+    const uint4 c5 = rc[5], c6 = rc[6], c7 = rc[7];
+    const float Mf = (float)M;
+    const CombineCanon c{(float)c7.y, asf(c6.x), asf(c6.y), asf(c7.x), c7.y != 0u && c5.w >= 2u && asf(c6.x) > 0.0f};
+    const uint32_t seed0 = reuse_seed(sc, x, y, SALT_SPATIAL);
+    const float4 *jr = A.jres + (size_t)pix * A.jpp;
+    uint32_t seed = seed0, Csum = c7.y;
+    float sumQ = 0.0f, w_sum = 0.0f, p_sel = c.pc, q_sel = c.qc;
+    int32_t src = (int32_t)pix;
+    SelF f_sel = stored_f(rc);
+    if constexpr (MT > 0) {
+        int32_t nid[MT];
+        bool pres[MT];
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {
+            uint32_t nx = 0u, ny = 0u;
+            pres[m] = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+            nid[m] = pres[m] ? band_index(sc, nx, ny) : (int32_t)pix;
         }
-        const uint4 *rc = A.cur + 8u * (size_t)pix;
-        const uint4 c5 = rc[5], c6 = rc[6], c7 = rc[7];
-        const float Mf = (float)M, cc = (float)c7.y;
-        const float pc = asf(c6.x), qc = asf(c6.y), Wc = asf(c7.x);
-        const bool canon_ok = c7.y != 0u && c5.w >= 2u && pc > 0.0f;
-        const uint32_t seed0 = reuse_seed(sc, x, y, SALT_SPATIAL);
-        // pass 1: neighbours' confidences and the canonical sample's MIS weight
-        uint32_t seed = seed0, Csum = c7.y;
-        float sumQ = 0.0f;
+        uint4 nv[MT];
+        float4 Fr[MT], B[MT];
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {  // (job results of absent neighbours are never used)
+            nv[m] = A.nbr[nid[m]];
+            Fr[m] = jr[2u * m];
+            B[m] = jr[2u * m + 1u];
+        }
+        Nbr nb[MT];
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {
+            nb[m] = nv[m].w != kNbrEscape ? Nbr{(nv[m].w >> 31) != 0u, (nv[m].w >> 24) & 0x7fu, nv[m].w & 0xffffffu,
+                                                asf(nv[m].x), asf(nv[m].y), asf(nv[m].z)}
+                                          : nbr_at(A, nid[m]);
+            if (!pres[m]) nb[m].valid = false;
+        }
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {
+            float Q = 1.0f;
+            if (nb[m].valid) {
+                Csum += nb[m].C;
+                Q = canon_q(c, Mf, nb[m].C, B[m]);
+            }
+            sumQ += Q;
+        }
+        const float wc = c.ok ? (sumQ / Mf) * c.pc * c.Wc : 0.0f;
+        if (wrs_update(w_sum, wc, seed)) { src = (int32_t)pix; p_sel = c.pc; q_sel = c.qc; f_sel = stored_f(rc); }
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {
+            float pf, qf;
+            SelF fj;
+            const float wn = neighbour_weight(c, Mf, nb[m], Fr[m], pf, qf, fj);
+            if (wrs_update(w_sum, wn, seed)) { src = pres[m] ? nid[m] : 0; p_sel = pf; q_sel = qf; f_sel = fj; }
+        }
+    } else {
         for (uint32_t m = 0; m < M; ++m) {
             uint32_t nx = 0u, ny = 0u;
             float Q = 1.0f;
             if (spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
                 const Nbr nb = nbr_at(A, band_index(sc, nx, ny));
                 if (nb.valid) {
-                    const uint32_t Cn = nb.C;
-                    Csum += Cn;
-                    if (canon_ok) {
-                        const float4 B = A.jres[pix * A.jpp + 2u * m + 1u];
-                        if (B.w > 0.0f) {
-                            const float pbc = luminance(mk(B.x, B.y, B.z)) * qc / B.w;
-                            const float den = cc * pc + Mf * (float)Cn * pbc;
-                            Q = den > 0.0f ? (cc * pc) / den : 1.0f;
-                        }
-                    }
+                    Csum += nb.C;
+                    Q = canon_q(c, Mf, nb.C, jr[2u * m + 1u]);
                 }
             }
             sumQ += Q;
         }
-        // pass 2: resampling, canonical first (the selection draws follow the offsets)
-        const float wc = canon_ok ? (sumQ / Mf) * pc * Wc : 0.0f;
-        float w_sum = 0.0f, p_sel = pc, q_sel = qc;
-        int32_t src = (int32_t)pix;
+        const float wc = c.ok ? (sumQ / Mf) * c.pc * c.Wc : 0.0f;
         uint32_t nseed = seed0;
-        SelF f_sel = stored_f(rc);
-        if (wrs_update(w_sum, wc, seed)) { src = (int32_t)pix; p_sel = pc; q_sel = qc; f_sel = stored_f(rc); }
+        if (wrs_update(w_sum, wc, seed)) { src = (int32_t)pix; p_sel = c.pc; q_sel = c.qc; f_sel = stored_f(rc); }
         for (uint32_t m = 0; m < M; ++m) {
             uint32_t nx = 0u, ny = 0u;
             float wn = 0.0f, pf = 0.0f, qf = 0.0f;
@@ -500,27 +562,28 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
             int32_t nidx = 0;
             if (spatial_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
                 nidx = band_index(sc, nx, ny);
-                const Nbr nb = nbr_at(A, nidx);
-                const float pn = nb.p;
-                if (nb.valid && nb.length >= 2u && pn > 0.0f) {
-                    const float4 Fr = A.jres[pix * A.jpp + 2u * m];
-                    if (Fr.w > 0.0f) {
-                        const float2 F = make_float2(luminance(mk(Fr.x, Fr.y, Fr.z)), Fr.w);
-                        const float cn = (float)nb.C, qn = nb.q, Wn = nb.W;
-                        const float J = qn / F.y;
-                        const float pb = pn / J;
-                        const float den = cc * F.x + Mf * cn * pb;
-                        const float mw = den > 0.0f ? (cn * pb) / den : 0.0f;
-                        wn = mw * F.x * Wn * J;
-                        pf = F.x;
-                        qf = F.y;
-                        fj = job_f(Fr);
-                    }
-                }
+                wn = neighbour_weight(c, Mf, nbr_at(A, nidx), jr[2u * m], pf, qf, fj);
             }
             if (wrs_update(w_sum, wn, seed)) { src = nidx; p_sel = pf; q_sel = qf; f_sel = fj; }
         }
-        write_reused(out, res_at(A.cur, src), p_sel, q_sel, f_sel, w_sum, Csum);
+    }
+    write_reused(out, res_at(A.cur, src), p_sel, q_sel, f_sel, w_sum, Csum);
+}
+
+__global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, ReuseArgs A) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        if (!gdecode(A.gbuf[pix]).valid) {
+            uint4 *out = A.hist + 8u * (size_t)pix;
+            for (int t = 0; t < 8; ++t) out[t] = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
+        if (A.neighbors == 3u) combine_pixel<3>(sc, A, x, y, pix);
+        else combine_pixel<0>(sc, A, x, y, pix);
     }
 }
 
