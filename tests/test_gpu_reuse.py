@@ -77,6 +77,31 @@ def test_temporal_and_spatial_passes_bit_exact(scene1, oracle_mod, native, prm):
     r.close()
 
 
+def test_spatial_confidence_past_the_summary_field(scene1, oracle_mod, native):
+    """Confidences C >= 2^24 do not fit the spatial pass's 16-byte neighbour summary
+    (ptx_reuse.hip wnbr_summary): those neighbours take the escape path (the reservoir itself
+    is read) and the pass stays bit-exact.  Spatial pass alone, on the oracle's PT_1 output
+    with every third reservoir's C raised past the field."""
+    O, W, H = oracle_mod, 64, 48
+    fr = oracle_frame(O, scene1, W, H)
+    fr.set_frame_index(2)
+    for p in (O.PASS_GBUFFER, O.PASS_INIT):
+        fr.run(p)
+    C = fr.reservoir[..., 29]
+    big = (C > 0) & (np.arange(W * H).reshape(H, W) % 3 == 0)
+    assert big.sum() > 100
+    C[big] += np.uint32(0x00FFFFFF)
+    r = reuse_renderer(scene1, W, H)
+    r.set_uniform(fr.uniform)
+    r.write_buffer(native.PTX_BUF_GBUFFER, fr.gbuffer)
+    r.write_buffer(native.PTX_BUF_RESERVOIR, fr.reservoir)
+    r.run_pass(native.PTX_PASS_SPATIAL)
+    fr.run(O.PASS_SPATIAL)
+    assert (fr.res_hist[..., 29] > 0x00FFFFFF).any()
+    assert_same(r.read_history(), fr.res_hist, "spatial output with wide confidences")
+    r.close()
+
+
 @pytest.mark.parametrize("W,H,frames", [(48, 40, 4), (37, 23, 3), (1, 1, 2), (8, 1, 2), (130, 70, 2)])
 def test_reuse_frames_bit_exact(scene1, oracle_mod, W, H, frames):
     O = oracle_mod
