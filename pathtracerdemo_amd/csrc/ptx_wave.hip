@@ -931,7 +931,8 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
         hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     else {
         // A/B switches (profiling only): occupancy target, LDS-staged tables.  Measured at
-        // 1080p C1: 5 waves/SIMD (94 VGPRs, no spill) with LDS tables is fastest; capping
+        // 1080p C1: 5 waves/SIMD (96 VGPRs; since the cooperative leaf phase 48 B/lane spill,
+        // which 4 waves would avoid: +0.5 %, noise) with LDS tables is fastest; capping
         // registers lower spills in the traversal loop.
         static const int occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 5;
         const bool tables_fit = sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts && !getenv("PTX_TRACE_NOLDS");
