@@ -39,29 +39,6 @@ struct Job {
 
 __device__ __forceinline__ const uint4 *res_at(const uint4 *base, int32_t idx) { return base + 8 * (ptrdiff_t)idx; }
 
-// Job lists sorted by what the next step does with the job: jobs whose ray was a regenerated
-// BSDF direction (next step: surface, BSDF, next ray -- "heavy") from the front of the
-// segment's list, jobs waiting for a Visibility (next step: one product) from the back, so
-// the next step's waves run one kind, not both.  The count word is heavy | light << 16
-// (a segment holds at most seg_px * 32 jobs).  Job results do not depend on list order.
-struct JobLists { uint32_t *l_light; uint32_t stride; };
-__device__ __forceinline__ JobLists job_lists(const WaveBufs &w, uint32_t *lds) {
-    if (threadIdx.x == 0) lds[2] = 0u;  // (seg_begin's barrier publishes it)
-    return JobLists{lds + 2, w.act_stride};
-}
-__device__ __forceinline__ void job_keep(const Seg &g, const JobLists &L, bool keep, bool light, uint32_t jid) {
-    const uint32_t sh = wave_alloc(g.l_act, keep && !light ? 1u : 0u);
-    const uint32_t sl = wave_alloc(L.l_light, keep && light ? 1u : 0u);
-    if (keep) g.act_out[light ? L.stride - 1u - sl : sh] = jid;
-}
-__device__ __forceinline__ void job_seg_end(const WaveBufs &w, const Seg &g, const JobLists &L) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        w.cnt[(2u * g.round) * w.nseg + g.j] = *g.l_act | (*L.l_light << 16);
-        w.cnt[(2u * g.round + 1u) * w.nseg + g.j] = *g.l_ray;
-    }
-}
-
 // A job waiting for its light segment's Visibility (phase 1) only needs HDR and F.
 __device__ __forceinline__ void job_store(const ReuseArgs &A, uint32_t jid, const Job &s) {
     const size_t n = A.njobs;
@@ -177,14 +154,15 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
-    const uint32_t nh = g.n_in & 0xffffu, n = nh + (g.n_in >> 16);
+    uint32_t nh;
+    const uint32_t n = split_count(g, nh);
     for (uint32_t base = 0; base < n; base += WB) {
         const uint32_t q = base + threadIdx.x;
         bool emit = false;
         uint32_t jid = 0u;
         Job s;
         if (q < n) {
-            jid = g.act_in[q < nh ? q : JL.stride - 1u - (q - nh)];
+            jid = split_at(g, JL, q, nh);
             job_load(sc, A, jid, s);
             if (s.phase == 0u) {  // regenerated vertex i+1 arrived (PT_4:1378-1380)
                 const Hit h = get_hit(g.res_in, s.idx);

@@ -461,7 +461,8 @@ __device__ __forceinline__ void winit_finish(const WInit &s, uint4 *reservoir, u
 }
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void winit_start(Scene sc, WaveBufs w, const uint4 *gbuf, uint4 *reservoir) {
-    __shared__ uint32_t lds[2];
+    __shared__ uint32_t lds[3];
+    const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
     float4 *state = w.state;
     const uint32_t npix = w.npix, np = padded_pixels(sc);
@@ -493,17 +494,21 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         // ray emission is executed by the whole wave (wave_alloc), active or not
         winit_vertex(sc, g, active, s, X, prev);
         if (active) winit_store(state, npix, pix, s);
-        seg_keep(g, active, pix);
+        // light next round: no BSDF ray out, only the NEE candidate to book and the path to end
+        job_keep(g, JL, active, active && !(s.flags & F_BSDF), pix);
     }
-    seg_end(w, g);
+    job_seg_end(w, g, JL);
 }
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void winit_step(Scene sc, WaveBufs w, uint32_t round, uint4 *reservoir) {
-    __shared__ uint32_t lds[2];
+    __shared__ uint32_t lds[3];
+    const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
     float4 *state = w.state;
     const float4 *res_in = g.res_in;
-    const uint32_t npix = w.npix, n = g.n_in;
+    const uint32_t npix = w.npix;
+    uint32_t nh;
+    const uint32_t n = split_count(g, nh);
     for (uint32_t base = 0; base < n; base += WB) {
         const uint32_t q = base + threadIdx.x;
         bool emit = false;
@@ -512,7 +517,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         Surface X;
         f3 prev;
         if (q < n) {
-            pix = g.act_in[q];
+            pix = split_at(g, JL, q, nh);
             winit_load(state, npix, pix, s);
             // 1. resolve the NEE candidate of vertex i with its Visibility (PT_1:1413-1421)
             const float4 a = res_in[2u * s.vis_idx], b = res_in[2u * s.vis_idx + 1u];
@@ -584,9 +589,9 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         }
         winit_vertex(sc, g, emit, s, X, prev);
         if (emit) winit_store(state, npix, pix, s);
-        seg_keep(g, emit, pix);
+        job_keep(g, JL, emit, emit && !(s.flags & F_BSDF), pix);
     }
-    seg_end(w, g);
+    job_seg_end(w, g, JL);
 }
 
 // =========================================================================== PT_4 (final)

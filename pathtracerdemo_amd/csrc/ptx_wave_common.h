@@ -90,6 +90,38 @@ __device__ __forceinline__ void seg_keep(const Seg &g, bool keep, uint32_t pix) 
     if (keep) g.act_out[slot] = pix;
 }
 
+// Active lists split by what the next logic round does with the entry: "heavy" entries (a
+// new path vertex: surface, BSDF, next rays) from the front of the segment's list, "light"
+// ones (only a Visibility result or a path's end to book) from the back, so the next
+// round's waves run one kind, not both.  The count word is heavy | light << 16 (a segment
+// holds at most seg_px * 32 entries).  Results never depend on list order.  Readers:
+// split_count, split_at.
+struct JobLists { uint32_t *l_light; uint32_t stride; };
+__device__ __forceinline__ JobLists job_lists(const WaveBufs &w, uint32_t *lds) {
+    if (threadIdx.x == 0) lds[2] = 0u;  // (seg_begin's barrier publishes it)
+    return JobLists{lds + 2, w.act_stride};
+}
+__device__ __forceinline__ void job_keep(const Seg &g, const JobLists &L, bool keep, bool light, uint32_t jid) {
+    const uint32_t sh = wave_alloc(g.l_act, keep && !light ? 1u : 0u);
+    const uint32_t sl = wave_alloc(L.l_light, keep && light ? 1u : 0u);
+    if (keep) g.act_out[light ? L.stride - 1u - sl : sh] = jid;
+}
+__device__ __forceinline__ void job_seg_end(const WaveBufs &w, const Seg &g, const JobLists &L) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        w.cnt[(2u * g.round) * w.nseg + g.j] = *g.l_act | (*L.l_light << 16);
+        w.cnt[(2u * g.round + 1u) * w.nseg + g.j] = *g.l_ray;
+    }
+}
+
+__device__ __forceinline__ uint32_t split_count(const Seg &g, uint32_t &nh) {
+    nh = g.n_in & 0xffffu;
+    return nh + (g.n_in >> 16);
+}
+__device__ __forceinline__ uint32_t split_at(const Seg &g, const JobLists &L, uint32_t q, uint32_t nh) {
+    return g.act_in[q < nh ? q : L.stride - 1u - (q - nh)];
+}
+
 __device__ __forceinline__ void put_ray(float4 *rays, uint32_t idx, f3 o, f3 d, float remain, uint32_t kind) {
     rays[2u * idx] = make_float4(o.x, o.y, o.z, remain);
     rays[2u * idx + 1u] = make_float4(d.x, d.y, d.z, asf(kind));
