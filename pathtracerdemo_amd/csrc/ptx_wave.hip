@@ -855,11 +855,14 @@ __global__ __launch_bounds__(WB) void wmcpt_start(Scene sc, WaveBufs w) {
 
 template <int FIRST>
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wmcpt_step(Scene sc, WaveBufs w, uint32_t round, float4 *accum) {
-    __shared__ uint32_t lds[2];
+    __shared__ uint32_t lds[3];
+    const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
     float4 *state = w.state;
     const float4 *res_in = g.res_in;
-    const uint32_t npix = w.npix, n = g.n_in;
+    const uint32_t npix = w.npix;
+    uint32_t nh;  // (wmcpt_start's plain count reads as all-heavy)
+    const uint32_t n = split_count(g, nh);
     const uint32_t nl = sc.U[U_LIGHT_COUNT];
     for (uint32_t base = 0; base < n; base += WB) {
         const uint32_t q = base + threadIdx.x;
@@ -868,7 +871,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         WMcpt s;
         Surface X;
         if (q < n) {
-            pix = g.act_in[q];
+            pix = split_at(g, JL, q, nh);
             const float4 hd = state[MS_HDR * npix + pix], co = state[MS_COL * npix + pix];
             const float4 fp = state[MS_FP * npix + pix], og = state[MS_ORG * npix + pix];
             s.seed = asu(hd.x); s.bounce = asu(hd.y) & 0xffu; s.flags = asu(hd.y) >> 8;
@@ -898,9 +901,10 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         }
         wmcpt_vertex(sc, g, emit, s, X);
         if (emit) wmcpt_store(state, npix, pix, s);
-        seg_keep(g, emit, pix);
+        // light next round: the shadow rays' terms to add and the path to end (no BSDF ray)
+        job_keep(g, JL, emit, emit && !(s.flags & 1u), pix);
     }
-    seg_end(w, g);
+    job_seg_end(w, g, JL);
 }
 
 // =========================================================================== host side
