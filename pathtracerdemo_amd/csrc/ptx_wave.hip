@@ -643,7 +643,8 @@ __device__ __forceinline__ void wfinal_store(float4 *state, uint32_t npix, uint3
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wfinal_start(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir,
                                                    float4 *accum) {
-    __shared__ uint32_t lds[2];
+    __shared__ uint32_t lds[3];
+    const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
     float4 *state = w.state;
     const uint32_t npix = w.npix, np = padded_pixels(sc);
@@ -682,25 +683,28 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         }
         wfinal_emit(sc, g, active, s, reservoir + 8u * (size_t)pix);
         if (active) wfinal_store(state, npix, pix, s, matref);
-        seg_keep(g, active, pix);
+        job_keep(g, JL, active, active && s.phase != 0u, pix);  // light: a Visibility result
     }
-    seg_end(w, g);
+    job_seg_end(w, g, JL);
 }
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wfinal_step(Scene sc, WaveBufs w, uint32_t round, const uint4 *reservoir,
                                                   float4 *accum) {
-    __shared__ uint32_t lds[2];
+    __shared__ uint32_t lds[3];
+    const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
     float4 *state = w.state;
     const float4 *res_in = g.res_in;
-    const uint32_t npix = w.npix, n = g.n_in;
+    const uint32_t npix = w.npix;
+    uint32_t nh;
+    const uint32_t n = split_count(g, nh);
     for (uint32_t base = 0; base < n; base += WB) {
         const uint32_t q = base + threadIdx.x;
         bool emit = false;
         uint32_t pix = 0u, matref = 0u;
         WFinal s;
         if (q < n) {
-            pix = g.act_in[q];
+            pix = split_at(g, JL, q, nh);
             const float4 hd = state[FS_HDR * npix + pix], fv = state[FS_F * npix + pix];
             const uint32_t hw = asu(hd.x);
             s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = hw >> 16;
@@ -734,9 +738,9 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         }
         wfinal_emit(sc, g, emit, s, reservoir + 8u * (size_t)pix);
         if (emit) wfinal_store(state, npix, pix, s, matref);
-        seg_keep(g, emit, pix);
+        job_keep(g, JL, emit, emit && s.phase != 0u, pix);
     }
-    seg_end(w, g);
+    job_seg_end(w, g, JL);
 }
 
 // =========================================================================== TEST_MCPT
