@@ -363,19 +363,16 @@ __device__ __forceinline__ bool gi_job(const GiArgs &A, const float4 *res, uint3
 }
 
 // Pairwise-MIS resampling (oracle gi_spatial_pixel); res = trace round 0's results.
-__global__ __launch_bounds__(WB) void wgis_combine(Scene sc, WaveBufs w, GiArgs A) {
-    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc), M = A.neighbors;
-    const float4 *res = w.res[0];
-    for (uint32_t k = 0; k < w.seg_px; k += WB) {
-        const uint32_t q = seg_pixel(w, j, k);
-        uint32_t x, y;
-        if (q >= np || !tile_xy(sc, q, x, y)) continue;
-        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
-        uint4 *out = A.hist + 4u * (size_t)pix;
-        if (!gdecode(A.gbuf[pix]).valid) {
-            for (int t = 0; t < 4; ++t) out[t] = make_uint4(0u, 0u, 0u, 0u);
-            continue;
-        }
+// MT = the neighbour count when it is a compile-time constant (the default 3): every
+// neighbour's G-buffer word, reservoir and job ray index are loaded in one round trip and
+// the job results in a second, instead of ~3 dependent loads per neighbour and pass;
+// MT = 0: any count, per neighbour (the same arithmetic in the same order either way).
+template <uint32_t MT>
+__device__ __forceinline__ void gis_combine_pixel(const Scene &sc, const GiArgs &A, const float4 *res, uint32_t x,
+                                                  uint32_t y, uint32_t pix) {
+    uint4 *out = A.hist + 4u * (size_t)pix;
+    const uint32_t M = MT ? MT : A.neighbors;
+    if constexpr (MT > 0) {
         const uint4 *rc = A.cur + 4u * (size_t)pix;
         const uint4 c1 = rc[1], c2 = rc[2], c3 = rc[3];
         const float Mf = (float)M, cc = (float)c2.w;
@@ -384,22 +381,50 @@ __global__ __launch_bounds__(WB) void wgis_combine(Scene sc, WaveBufs w, GiArgs 
         const bool canon_ok = c2.w != 0u && pc > 0.0f;
         const uint32_t seed0 = gi_seed(sc, x, y, SALT_GI_SPATIAL);
         uint32_t seed = seed0, Csum = c2.w;
-        float sumQ = 0.0f;
-        for (uint32_t m = 0; m < M; ++m) {  // confidences + the canonical MIS weight
+        int32_t nid[MT];
+        bool pres[MT];
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {
             uint32_t nx = 0u, ny = 0u;
+            pres[m] = gi_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+            nid[m] = pres[m] ? gi_band_index(sc, nx, ny) : (int32_t)pix;
+        }
+        uint32_t gv[MT], jf[MT], jb[MT];
+        uint4 n1[MT], n2[MT], n3[MT];
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {
+            const uint4 *rn = A.cur + 4 * (ptrdiff_t)nid[m];
+            gv[m] = A.gbuf[nid[m]].x;
+            n1[m] = rn[1]; n2[m] = rn[2]; n3[m] = rn[3];
+            jf[m] = A.jray[pix * A.jpp + 2u * m];
+            jb[m] = A.jray[pix * A.jpp + 2u * m + 1u];
+        }
+        bool valid[MT], hf[MT], hb[MT];
+        float pn[MT];
+        float4 fa[MT], fb[MT], ba[MT], bb[MT];
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {  // (a job index is read only where gi_job would read it)
+            valid[m] = pres[m] && (gv[m] >> 31) != 0u;
+            pn[m] = luminance(ld3(n3[m]));
+            hb[m] = valid[m] && canon_ok && jb[m] != GI_NO_RAY;
+            hf[m] = valid[m] && pn[m] > 0.0f && jf[m] != GI_NO_RAY;
+            ba[m] = bb[m] = fa[m] = fb[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (hb[m]) { ba[m] = res[2u * jb[m]]; bb[m] = res[2u * jb[m] + 1u]; }
+            if (hf[m]) { fa[m] = res[2u * jf[m]]; fb[m] = res[2u * jf[m] + 1u]; }
+        }
+        float sumQ = 0.0f;
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {  // confidences + the canonical MIS weight
             float Q = 1.0f;
-            if (gi_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
-                const int32_t nidx = gi_band_index(sc, nx, ny);
-                if (gdecode(A.gbuf[nidx]).valid) {
-                    const uint32_t Cn = A.cur[4 * (ptrdiff_t)nidx + 2].w;
-                    Csum += Cn;
-                    f3 B;
-                    float qB;
-                    if (canon_ok && gi_job(A, res, pix * A.jpp + 2u * m + 1u, B, qB)) {
-                        const float pbc = luminance(B) * qc / qB;
-                        const float den = cc * pc + Mf * (float)Cn * pbc;
-                        Q = den > 0.0f ? (cc * pc) / den : 1.0f;
-                    }
+            if (valid[m]) {
+                const uint32_t Cn = n2[m].w;
+                Csum += Cn;
+                if (hb[m]) {
+                    const f3 B = mk(ba[m].y, ba[m].z, ba[m].w) * ba[m].x;
+                    const float qB = bb[m].x;
+                    const float pbc = luminance(B) * qc / qB;
+                    const float den = cc * pc + Mf * (float)Cn * pbc;
+                    Q = den > 0.0f ? (cc * pc) / den : 1.0f;
                 }
             }
             sumQ += Q;
@@ -411,34 +436,106 @@ __global__ __launch_bounds__(WB) void wgis_combine(Scene sc, WaveBufs w, GiArgs 
         float qsel = qc;
         w_sum += wc;
         if (rnd(seed) < wc / w_sum) { src = rc; fsel = fcv; qsel = qc; }
-        uint32_t nseed = seed0;
-        for (uint32_t m = 0; m < M; ++m) {
-            uint32_t nx = 0u, ny = 0u;
+#pragma unroll
+        for (uint32_t m = 0; m < MT; ++m) {
             float wn = 0.0f;
             f3 F = mk(0.0f, 0.0f, 0.0f);
             float qF = 0.0f;
-            int32_t nidx = 0;
-            if (gi_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
-                nidx = gi_band_index(sc, nx, ny);
-                const uint4 *rn = A.cur + 4 * (ptrdiff_t)nidx;
-                const uint4 n1 = rn[1], n2 = rn[2], n3 = rn[3];
-                const float pn = luminance(ld3(n3));
-                if (gdecode(A.gbuf[nidx]).valid && pn > 0.0f && gi_job(A, res, pix * A.jpp + 2u * m, F, qF)) {
-                    const float pF = luminance(F);
-                    const float J = asf(n3.w) / qF;
-                    const float pb = pn / J;
-                    const float den = cc * pF + Mf * (float)n2.w * pb;
-                    const float mw = den > 0.0f ? ((float)n2.w * pb) / den : 0.0f;
-                    wn = mw * pF * asf(n1.w) * J;
-                } else {
-                    F = mk(0.0f, 0.0f, 0.0f);
-                    qF = 0.0f;
-                }
+            if (pres[m] && hf[m]) {
+                F = mk(fa[m].y, fa[m].z, fa[m].w) * fa[m].x;
+                qF = fb[m].x;
+                const float pF = luminance(F);
+                const float J = asf(n3[m].w) / qF;
+                const float pb = pn[m] / J;
+                const float den = cc * pF + Mf * (float)n2[m].w * pb;
+                const float mw = den > 0.0f ? ((float)n2[m].w * pb) / den : 0.0f;
+                wn = mw * pF * asf(n1[m].w) * J;
             }
             w_sum += wn;
-            if (rnd(seed) < wn / w_sum) { src = A.cur + 4 * (ptrdiff_t)nidx; fsel = F; qsel = qF; }
+            if (rnd(seed) < wn / w_sum) { src = A.cur + 4 * (ptrdiff_t)(pres[m] ? nid[m] : 0); fsel = F; qsel = qF; }
         }
         gi_write(out, src, fsel, qsel, w_sum, Csum);
+    } else {
+    const uint4 *rc = A.cur + 4u * (size_t)pix;
+    const uint4 c1 = rc[1], c2 = rc[2], c3 = rc[3];
+    const float Mf = (float)M, cc = (float)c2.w;
+    const f3 fcv = ld3(c3);
+    const float pc = luminance(fcv), qc = asf(c3.w), Wc = asf(c1.w);
+    const bool canon_ok = c2.w != 0u && pc > 0.0f;
+    const uint32_t seed0 = gi_seed(sc, x, y, SALT_GI_SPATIAL);
+    uint32_t seed = seed0, Csum = c2.w;
+    float sumQ = 0.0f;
+    for (uint32_t m = 0; m < M; ++m) {  // confidences + the canonical MIS weight
+        uint32_t nx = 0u, ny = 0u;
+        float Q = 1.0f;
+        if (gi_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
+            const int32_t nidx = gi_band_index(sc, nx, ny);
+            if (gdecode(A.gbuf[nidx]).valid) {
+                const uint32_t Cn = A.cur[4 * (ptrdiff_t)nidx + 2].w;
+                Csum += Cn;
+                f3 B;
+                float qB;
+                if (canon_ok && gi_job(A, res, pix * A.jpp + 2u * m + 1u, B, qB)) {
+                    const float pbc = luminance(B) * qc / qB;
+                    const float den = cc * pc + Mf * (float)Cn * pbc;
+                    Q = den > 0.0f ? (cc * pc) / den : 1.0f;
+                }
+            }
+        }
+        sumQ += Q;
+    }
+    const float wc = canon_ok ? (sumQ / Mf) * pc * Wc : 0.0f;
+    float w_sum = 0.0f;
+    const uint4 *src = rc;
+    f3 fsel = fcv;
+    float qsel = qc;
+    w_sum += wc;
+    if (rnd(seed) < wc / w_sum) { src = rc; fsel = fcv; qsel = qc; }
+    uint32_t nseed = seed0;
+    for (uint32_t m = 0; m < M; ++m) {
+        uint32_t nx = 0u, ny = 0u;
+        float wn = 0.0f;
+        f3 F = mk(0.0f, 0.0f, 0.0f);
+        float qF = 0.0f;
+        int32_t nidx = 0;
+        if (gi_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
+            nidx = gi_band_index(sc, nx, ny);
+            const uint4 *rn = A.cur + 4 * (ptrdiff_t)nidx;
+            const uint4 n1 = rn[1], n2 = rn[2], n3 = rn[3];
+            const float pn = luminance(ld3(n3));
+            if (gdecode(A.gbuf[nidx]).valid && pn > 0.0f && gi_job(A, res, pix * A.jpp + 2u * m, F, qF)) {
+                const float pF = luminance(F);
+                const float J = asf(n3.w) / qF;
+                const float pb = pn / J;
+                const float den = cc * pF + Mf * (float)n2.w * pb;
+                const float mw = den > 0.0f ? ((float)n2.w * pb) / den : 0.0f;
+                wn = mw * pF * asf(n1.w) * J;
+            } else {
+                F = mk(0.0f, 0.0f, 0.0f);
+                qF = 0.0f;
+            }
+        }
+        w_sum += wn;
+        if (rnd(seed) < wn / w_sum) { src = A.cur + 4 * (ptrdiff_t)nidx; fsel = F; qsel = qF; }
+    }
+        gi_write(out, src, fsel, qsel, w_sum, Csum);
+    }
+}
+__global__ __launch_bounds__(WB) void wgis_combine(Scene sc, WaveBufs w, GiArgs A) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    const float4 *res = w.res[0];
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        if (!gdecode(A.gbuf[pix]).valid) {
+            uint4 *out = A.hist + 4u * (size_t)pix;
+            for (int t = 0; t < 4; ++t) out[t] = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
+        if (A.neighbors == 3u) gis_combine_pixel<3>(sc, A, res, x, y, pix);
+        else gis_combine_pixel<0>(sc, A, res, x, y, pix);
     }
 }
 
