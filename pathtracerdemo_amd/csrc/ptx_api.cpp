@@ -71,6 +71,9 @@ struct ptx_handle {
     // the wave state holds the PT_1 pass of the reservoirs in d_res (enqueued, nothing since
     // rewrote them): the reuse temporal pass may read its path hits instead of re-tracing
     bool init_state_valid = false;
+    // d_nbr holds the summaries of the band's reservoirs as the temporal pass left them
+    // (set by that pass, dropped by anything else that rewrites G-buffer or reservoirs)
+    bool nbr_valid = false;
     uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
     bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
     uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
@@ -411,7 +414,8 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.cap = h->temporal_cap;
     A.hist_valid = h->hist_valid ? 1u : 0u;
     A.use_init = (pass == PTX_PASS_TEMPORAL && h->init_state_valid) ? 1u : 0u;
-    A.nbr = (const uint4 *)h->d_nbr.p + (size_t)h->halo_top * h->cfg.width;
+    A.nbr_out = (uint4 *)h->d_nbr.p + (size_t)h->halo_top * h->cfg.width;
+    A.nbr = A.nbr_out;
     return A;
 }
 
@@ -509,15 +513,29 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
     k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
     if ((uint32_t)k > w.nseg) k = (int)w.nseg;
     hipError_t e = hipSuccess;
-    // the spatial pass gathers neighbours (halo rows included) through their summaries
-    for (int i = 0; i < npasses; ++i)
+    // the spatial pass gathers neighbours (halo rows included) through their summaries: the
+    // temporal pass wrote the band's; halo rows (just unpacked) or a band whose buffers were
+    // written since get them here
+    for (int i = 0; i < npasses; ++i) {
         if (passes[i] == PTX_PASS_SPATIAL && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+            const size_t W = h->cfg.width, top = h->halo_top * W, band = (size_t)h->band_h * W;
+            const uint4 *gb = (const uint4 *)h->d_gbuf.p, *rs = (const uint4 *)h->d_res.p;
+            uint4 *nb = (uint4 *)h->d_nbr.p;
             TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, h->stream);
-            e = wave_reuse_summary((const uint4 *)h->d_gbuf.p, (const uint4 *)h->d_res.p, (uint4 *)h->d_nbr.p,
-                                   px_with_halo(h), h->stream);
+            if (!h->nbr_valid) {
+                e = wave_reuse_summary(gb, rs, nb, px_with_halo(h), h->stream);
+            } else {
+                e = wave_reuse_summary(gb, rs, nb, top, h->stream);
+                const size_t b0 = top + band;
+                if (e == hipSuccess)
+                    e = wave_reuse_summary(gb + b0, rs + 8u * b0, nb + b0, px_with_halo(h) - b0, h->stream);
+            }
             event_end(t, h->stream);
             if (e != hipSuccess) return e;
+        } else if (passes[i] != PTX_PASS_FINAL && passes[i] != PTX_PASS_TEMPORAL) {
+            h->nbr_valid = false;  // G-buffer / PT_1 / MCPT rewrite what the summaries describe
         }
+    }
     if (k > 1) {
         if (!h->ev_fork && (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return e;
         for (int q = 1; q < k; ++q) {
@@ -552,9 +570,12 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
         if ((e = hipEventRecord(h->ev_join[q], h->sub[q])) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(h->stream, h->ev_join[q], 0)) != hipSuccess) return e;
     }
-    // the temporal pass rewrote the reservoirs PT_1's state describes
+    // the temporal pass rewrote the reservoirs PT_1's state describes, and summarised them
     for (int i = 0; i < npasses; ++i)
-        if (passes[i] == PTX_PASS_TEMPORAL) h->init_state_valid = false;
+        if (passes[i] == PTX_PASS_TEMPORAL) {
+            h->init_state_valid = false;
+            h->nbr_valid = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
+        }
     return hipSuccess;
 }
 static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBufs &w, int pass) {
@@ -609,6 +630,7 @@ static int timed_wave_frame(ptx_handle *h) {
 
 static int timed_launch(ptx_handle *h, int pass) {
     if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before rendering");
+    if (pass != PTX_PASS_TEMPORAL && pass != PTX_PASS_SPATIAL && pass != PTX_PASS_FINAL) h->nbr_valid = false;
     if (!h->layout_valid) {
         if (int rc = build_layout(h)) return rc;
     }
@@ -656,6 +678,7 @@ static int timed_launch(ptx_handle *h, int pass) {
     case PTX_PASS_GBUFFER:
         e = launch_gbuffer(sc, gbuf_band(h), d, h->stream);
         h->init_state_valid = false;
+        h->nbr_valid = false;
         break;
     case PTX_PASS_INIT:
         e = variant == 0   ? launch_init_tiled(sc, gb, res, d, h->stream)
@@ -781,6 +804,7 @@ int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const
     h->scene_loaded = true;
     h->hist_valid = false;
     h->init_state_valid = false;
+    h->nbr_valid = false;
     if (h->frame_set) return build_layout(h);
     return PTX_OK;
 }
@@ -989,6 +1013,7 @@ int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t byte
     HIP_CHECK(h, hipStreamSynchronize(h->stream));
     HIP_CHECK(h, hipMemcpy(b.p, host_src, bytes, hipMemcpyHostToDevice));
     h->init_state_valid = false;  // the wave state no longer matches the buffers
+    h->nbr_valid = false;
     return PTX_OK;
 }
 

@@ -89,6 +89,7 @@ struct ReuseArgs {
     uint32_t radius, neighbors, cap, hist_valid;
     uint32_t use_init;  // temporal: this frame's PT_1 wave state (path hits, NEE Visibility) is in w.state
     const uint4 *nbr;   // spatial: per-pixel neighbour summary (wave_reuse_summary), cur's addressing
+    uint4 *nbr_out;     // the same buffer: the temporal pass writes its output's summaries
 };
 // rounds of {trace, step} between a reuse pass's start and combine launches
 int reuse_rounds(int pass_temporal, const ReuseArgs &A);

@@ -219,6 +219,14 @@ __device__ __forceinline__ void write_reused(uint4 *out, const uint4 *src, float
     out[7] = make_uint4(asu(p_sel > 0.0f ? w_sum / p_sel : 0.0f), C, fs.known ? asu(fs.f.z) : 0u, fs.known ? 1u : 0u);
 }
 
+// The spatial pass's 16-byte neighbour summary of a reservoir (see wnbr_summary below).
+constexpr uint32_t kNbrEscape = 0xFFFFFFFFu;
+__device__ __forceinline__ uint4 nbr_pack(bool valid, uint4 r5, uint4 r6, uint4 r7) {
+    uint32_t w = 0u;
+    if (valid) w = (r5.w > 0x7fu || r7.y > 0xfffffeu) ? kNbrEscape : (1u << 31) | (r5.w << 24) | r7.y;
+    return make_uint4(r6.x, r6.y, r7.x, w);
+}
+
 // ---------------------------------------------------------------- temporal
 // The canonical sample is PT_1's own path: replaying its BSDF draws from its pixel's hit
 // gives back PT_1's vertices, whose hits PT_1 left in its wave state (vertex 2 / 3 compacts),
@@ -302,7 +310,10 @@ __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, Re
         uint32_t x, y;
         if (q >= np || !tile_xy(sc, q, x, y)) continue;
         const uint32_t pix = (y - sc.row_begin) * sc.width + x;
-        if (!gdecode(A.gbuf[pix]).valid) continue;  // PT_1 wrote the zero reservoir
+        if (!gdecode(A.gbuf[pix]).valid) {  // PT_1 wrote the zero reservoir
+            A.nbr_out[pix] = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
         uint4 *rv = A.cur + 8u * (size_t)pix;
         const uint4 *hv = A.hist + 8u * (size_t)pix;
         uint32_t seed = reuse_seed(sc, x, y, SALT_TEMPORAL);
@@ -322,6 +333,10 @@ __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, Re
         if (wrs_update(w_sum, wc, seed)) { from_hist = false; p_sel = ec.x; q_sel = ec.y; }
         if (wrs_update(w_sum, wp, seed)) { from_hist = true; p_sel = pp; q_sel = qp; }
         write_reused(rv, from_hist ? hv : rv, p_sel, q_sel, from_hist ? stored_f(hv) : job_f(er), w_sum, 1u + Cp);
+        // the spatial pass's summary of the output (words 23, 24, 25, 28, 29 as written above)
+        const float W = p_sel > 0.0f ? w_sum / p_sel : 0.0f;
+        A.nbr_out[pix] = nbr_pack(true, make_uint4(0u, 0u, 0u, from_hist ? h5.w : r5.w),
+                                  make_uint4(asu(p_sel), asu(q_sel), 0u, 0u), make_uint4(asu(W), 1u + Cp, 0u, 0u));
     }
 }
 
@@ -348,7 +363,6 @@ __device__ __forceinline__ int32_t band_index(const Scene &sc, uint32_t x, uint3
 // spatial jobs start): {p_hat (word 24), q (25), W (28), G-buffer valid << 31 | length << 24 |
 // C}, or w = kNbrEscape when length or C does not fit (then read the reservoir itself).  A
 // neighbour costs one 16-byte gather instead of a G-buffer line and a reservoir line.
-constexpr uint32_t kNbrEscape = 0xFFFFFFFFu;
 struct Nbr { bool valid; uint32_t length, C; float p, q, W; };
 __device__ __forceinline__ Nbr nbr_at(const ReuseArgs &A, int32_t idx) {
     const uint4 v = A.nbr[idx];
@@ -362,11 +376,7 @@ __global__ __launch_bounds__(WB) void wnbr_summary(const uint4 *gbuf, const uint
     const size_t i = (size_t)blockIdx.x * WB + threadIdx.x;
     if (i >= npx) return;
     const uint4 *rv = res + 8u * i;
-    const uint32_t valid = gbuf[i].x >> 31;
-    const uint4 r5 = rv[5], r6 = rv[6], r7 = rv[7];
-    uint32_t w = 0u;
-    if (valid) w = (r5.w > 0x7fu || r7.y > 0xfffffeu) ? kNbrEscape : (1u << 31) | (r5.w << 24) | r7.y;
-    nbr[i] = make_uint4(r6.x, r6.y, r7.x, w);
+    nbr[i] = nbr_pack((gbuf[i].x >> 31) != 0u, rv[5], rv[6], rv[7]);
 }
 hipError_t wave_reuse_summary(const uint4 *gbuf, const uint4 *res, uint4 *nbr, size_t npx, hipStream_t s) {
     if (npx == 0) return hipSuccess;
