@@ -50,7 +50,7 @@ struct ptx_handle {
     std::vector<uint32_t> scene, geometry, accel;
     DevBuf d_scene, d_geometry;
     // derived MI355X layout
-    DevBuf d_tris, d_nodes, d_subs, d_insts, d_mats;
+    DevBuf d_tris, d_nodes, d_subs, d_insts, d_mats, d_tverts;
     uint32_t n_tris = 0, n_nodes = 0, n_inst = 0, n_subs = 0, max_depth = 0, stack_depth = 0;
     uint32_t layout_key[8] = {0};
     bool layout_valid = false;
@@ -167,6 +167,7 @@ static int build_layout(ptx_handle *h) {
     std::vector<NodePair> nodes;
     std::vector<float> tris;  // 12 floats per triangle
     std::vector<float> mats;  // 8 floats per sub-mesh, in SubRoot order (Scene::mats)
+    std::vector<float> tverts;  // 20 floats per triangle, triangle-table order (Scene::tverts)
     std::vector<uint32_t> mesh_sub_base(n_mesh), mesh_nsub(n_mesh), mesh_tri_base(n_mesh);
     uint32_t max_depth = 0;
 
@@ -261,6 +262,15 @@ static int build_layout(ptx_handle *h) {
             const float e2[3] = {P[2][0] - P[0][0], P[2][1] - P[0][1], P[2][2] - P[0][2]};
             const float rec[12] = {P[0][0], P[0][1], P[0][2], e1[0], e1[1], e1[2], e2[0], e2[1], e2[2], 0, 0, 0};
             tris.insert(tris.end(), rec, rec + 12);
+            float N[3][3];
+            for (int v = 0; v < 3; ++v) {
+                const size_t vi = (size_t)off_vertex + STRIDE_VERTEX * G[ii + v];
+                if (vi + 6 > G.size()) return fail(h, PTX_E_SCENE, "vertex normal out of range");
+                for (int k = 0; k < 3; ++k) N[v][k] = as_f32(G[vi + 3 + k]);
+            }
+            const float tv[20] = {P[0][0], P[0][1], P[0][2], N[0][0], N[0][1], N[0][2], P[1][0], P[1][1], P[1][2], N[1][0],
+                                  N[1][1], N[1][2], P[2][0], P[2][1], P[2][2], N[2][0], N[2][1], N[2][2], 0.0f, 0.0f};
+            tverts.insert(tverts.end(), tv, tv + 20);
         }
     }
     std::vector<Inst> insts(n_inst);
@@ -276,6 +286,7 @@ static int build_layout(ptx_handle *h) {
         I.tri_base = mesh_tri_base[I.mesh];
     }
     if (tris.empty()) tris.resize(12, 0.0f);
+    if (tverts.empty()) tverts.resize(20, 0.0f);
     if (nodes.empty()) nodes.resize(1);
     if (subs.empty()) subs.resize(1);
     if (mats.empty()) mats.resize(8, 0.0f);
@@ -285,6 +296,7 @@ static int build_layout(ptx_handle *h) {
     h->n_subs = (uint32_t)subs.size();
     if (int rc = upload(h, h->d_insts, insts.data(), std::max<size_t>(1, insts.size()) * sizeof(Inst))) return rc;
     if (int rc = upload(h, h->d_mats, mats.data(), mats.size() * sizeof(float))) return rc;
+    if (int rc = upload(h, h->d_tverts, tverts.data(), tverts.size() * sizeof(float))) return rc;
     h->n_tris = (uint32_t)(tris.size() / 12);
     h->n_nodes = (uint32_t)nodes.size();
     h->n_inst = n_inst;
@@ -306,6 +318,7 @@ static Scene make_scene(ptx_handle *h) {
     sc.subs = (const SubRoot *)h->d_subs.p;
     sc.insts = (const Inst *)h->d_insts.p;
     sc.mats = (const float4 *)h->d_mats.p;
+    sc.tverts = (const float4 *)h->d_tverts.p;
     sc.n_inst = h->n_inst;
     sc.n_subs = h->n_subs;
     sc.width = h->cfg.width;
@@ -980,7 +993,7 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
     out->instances = h->n_inst;
     out->max_bvh_depth = h->max_depth;
     out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
-                        h->d_subs.bytes + h->d_insts.bytes + h->d_mats.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
+                        h->d_subs.bytes + h->d_insts.bytes + h->d_mats.bytes + h->d_tverts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
                         h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_nbr.bytes + h->d_direct.bytes;
     return PTX_OK;
 }
@@ -1078,7 +1091,7 @@ int ptx_destroy(ptx_handle *h) {
         if (t.start) (void)hipEventDestroy(t.start);
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
-    for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_gbuf,
+    for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
                       &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_direct})

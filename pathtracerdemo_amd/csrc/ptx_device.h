@@ -74,6 +74,7 @@ struct Scene {
     const SubRoot *subs;
     const Inst *insts;
     const float4 *mats;   // 2 float4 per sub-mesh (SubRoot numbering): GetMaterial, pre-applied
+    const float4 *tverts; // 5 float4 per triangle (triangle-table order): its 3 vertices' position + normal
     uint32_t n_inst, n_subs;
     uint32_t width, height, row_begin, row_end;
     unsigned long long *counters;  // nullptr unless PTX_FLAG_COUNT_WORK
@@ -237,6 +238,20 @@ __device__ __forceinline__ f3 vtx_nrm(const Scene &sc, const uint32_t *desc, uin
     return mk(asf(p[3]), asf(p[4]), asf(p[5]));
 }
 
+// The three vertices (object-space position + normal, the GeometryBuffer's f32 values) of
+// triangle `tri` = Inst::tri_base + prim: one 80-byte record instead of the descriptor ->
+// index -> vertex chain (GetTriangleWorldSpace, SH/PT_1_InitPass.wgsl:390-407).
+struct TriVerts { f3 p[3], n[3]; };
+__device__ __forceinline__ TriVerts tri_verts(const Scene &sc, uint32_t tri) {
+    const float4 *q = sc.tverts + 5u * (size_t)tri;
+    const float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
+    TriVerts t;
+    t.p[0] = mk(a.x, a.y, a.z); t.n[0] = mk(a.w, b.x, b.y);
+    t.p[1] = mk(b.z, b.w, c.x); t.n[1] = mk(c.y, c.z, c.w);
+    t.p[2] = mk(d.x, d.y, d.z); t.n[2] = mk(d.w, e.x, e.y);
+    return t;
+}
+
 // GetBaryCentricWeights (SH/PT_1_InitPass.wgsl:549-575): returns (w,u) = bary.xy
 __device__ __forceinline__ void barycentric(f3 P, f3 A, f3 B, f3 C, float eps, float &bx, float &by) {
     f3 v0 = B - A, v1 = C - A, v2 = P - A;
@@ -255,12 +270,10 @@ __device__ __forceinline__ void barycentric(f3 P, f3 A, f3 B, f3 C, float eps, f
 __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, PassEps eps, Hit &best) {
     best.s.valid = 1u;
     const Inst &I = sc.insts[best.s.inst];
-    const uint32_t *desc = desc_ptr(sc, I.mesh);
-    uint32_t id[3];
-    tri_vertex_ids(sc, desc, best.s.prim, id);
-    f3 A = xform_point(I.m, vtx_pos(sc, desc, id[0]));
-    f3 B = xform_point(I.m, vtx_pos(sc, desc, id[1]));
-    f3 C = xform_point(I.m, vtx_pos(sc, desc, id[2]));
+    const TriVerts tv = tri_verts(sc, I.tri_base + best.s.prim);
+    f3 A = xform_point(I.m, tv.p[0]);
+    f3 B = xform_point(I.m, tv.p[1]);
+    f3 C = xform_point(I.m, tv.p[2]);
     f3 P = ray.o + ray.d * best.t;
     barycentric(P, A, B, C, eps.bary_eps, best.s.bu, best.s.bv);
     const float U = best.s.bu, V = best.s.bv, W = 1.0f - U - V;

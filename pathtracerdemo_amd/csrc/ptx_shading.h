@@ -32,17 +32,15 @@ __device__ __forceinline__ float get_transmission(const Scene &sc, uint32_t inst
 // GetSurface (SH/PT_1_InitPass.wgsl:438-467) with GetTriangleWorldSpace (:390-407)
 __device__ __forceinline__ Surface get_surface(const Scene &sc, Compact x) {
     const Inst &I = sc.insts[x.inst];
-    const uint32_t *desc = desc_ptr(sc, I.mesh);
     Surface s;
     s.mat = material_at(sc, I.sub_base + x.mat);
-    uint32_t id[3];
-    tri_vertex_ids(sc, desc, x.prim, id);
-    f3 p0 = xform_point(I.m, vtx_pos(sc, desc, id[0]));
-    f3 n0 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[0]));
-    f3 p1 = xform_point(I.m, vtx_pos(sc, desc, id[1]));
-    f3 n1 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[1]));
-    f3 p2 = xform_point(I.m, vtx_pos(sc, desc, id[2]));
-    f3 n2 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[2]));
+    const TriVerts tv = tri_verts(sc, I.tri_base + x.prim);
+    f3 p0 = xform_point(I.m, tv.p[0]);
+    f3 n0 = xform_point_t(I.minv, tv.n[0]);
+    f3 p1 = xform_point(I.m, tv.p[1]);
+    f3 n1 = xform_point_t(I.minv, tv.n[1]);
+    f3 p2 = xform_point(I.m, tv.p[2]);
+    f3 n2 = xform_point_t(I.minv, tv.n[2]);
     float U = x.bu, V = x.bv, W = 1.0f - U - V;
     s.nrm = normalize((n0 * U + n1 * V) + n2 * W);
     s.pos = (p0 * U + p1 * V) + p2 * W;
@@ -52,14 +50,12 @@ __device__ __forceinline__ Surface get_surface(const Scene &sc, Compact x) {
 // (the position is bit-identical: same world-space vertices and barycentrics).
 __device__ __forceinline__ Surface surface_at(const Scene &sc, const Compact &x, f3 pos) {
     const Inst &I = sc.insts[x.inst];
-    const uint32_t *desc = desc_ptr(sc, I.mesh);
     Surface s;
     s.mat = material_at(sc, I.sub_base + x.mat);
-    uint32_t id[3];
-    tri_vertex_ids(sc, desc, x.prim, id);
-    f3 n0 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[0]));
-    f3 n1 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[1]));
-    f3 n2 = xform_point_t(I.minv, vtx_nrm(sc, desc, id[2]));
+    const TriVerts tv = tri_verts(sc, I.tri_base + x.prim);
+    f3 n0 = xform_point_t(I.minv, tv.n[0]);
+    f3 n1 = xform_point_t(I.minv, tv.n[1]);
+    f3 n2 = xform_point_t(I.minv, tv.n[2]);
     float U = x.bu, V = x.bv, W = 1.0f - U - V;
     s.nrm = normalize((n0 * U + n1 * V) + n2 * W);
     s.pos = pos;
@@ -68,12 +64,10 @@ __device__ __forceinline__ Surface surface_at(const Scene &sc, const Compact &x,
 // Position-only GetSurface for Visibility restarts (the normal is unused there).
 __device__ __forceinline__ f3 get_surface_pos(const Scene &sc, Compact x) {
     const Inst &I = sc.insts[x.inst];
-    const uint32_t *desc = desc_ptr(sc, I.mesh);
-    uint32_t id[3];
-    tri_vertex_ids(sc, desc, x.prim, id);
-    f3 p0 = xform_point(I.m, vtx_pos(sc, desc, id[0]));
-    f3 p1 = xform_point(I.m, vtx_pos(sc, desc, id[1]));
-    f3 p2 = xform_point(I.m, vtx_pos(sc, desc, id[2]));
+    const TriVerts tv = tri_verts(sc, I.tri_base + x.prim);
+    f3 p0 = xform_point(I.m, tv.p[0]);
+    f3 p1 = xform_point(I.m, tv.p[1]);
+    f3 p2 = xform_point(I.m, tv.p[2]);
     float U = x.bu, V = x.bv, W = 1.0f - U - V;
     return (p0 * U + p1 * V) + p2 * W;
 }
