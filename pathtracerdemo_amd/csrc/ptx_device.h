@@ -267,9 +267,11 @@ __device__ __forceinline__ void barycentric(f3 P, f3 A, f3 B, f3 C, float eps, f
 }
 
 // Barycentrics and world position of a closest hit whose inst/prim/t are set.
-__device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, PassEps eps, Hit &best) {
+// (`insts`: the instance table, or the trace kernel's LDS copy of it)
+__device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, PassEps eps, Hit &best,
+                                             const Inst *insts = nullptr) {
     best.s.valid = 1u;
-    const Inst &I = sc.insts[best.s.inst];
+    const Inst &I = (insts ? insts : sc.insts)[best.s.inst];
     const TriVerts tv = tri_verts(sc, I.tri_base + best.s.prim);
     f3 A = xform_point(I.m, tv.p[0]);
     f3 B = xform_point(I.m, tv.p[1]);
@@ -513,7 +515,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     }
     if (best.valid) {
         best.t = vy;
-        if (!ANY) complete_hit(sc, ray, eps, best);
+        if (!ANY) complete_hit(sc, ray, eps, best, insts);
     }
     return best;
 }
