@@ -64,6 +64,7 @@ struct WaveBufs {
     uint32_t *act[2];    // active pixel / job lists (nseg * act_stride), ping-pong
     uint32_t act_stride; // list entries per segment (seg_px; seg_px * jobs per pixel for reuse)
     uint32_t *cnt;       // 2 * kWaveMaxRounds * nseg counts
+    uint32_t trace_waves;  // trace_queue occupancy target (waves per SIMD; 4 or 5, per pipeline)
 };
 // occ_only: every query of the round is Q_OCC (any-hit kernel instance)
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t stack_depth,

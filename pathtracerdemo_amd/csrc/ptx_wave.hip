@@ -943,11 +943,13 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
     else if (sc.counters)
         hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     else {
-        // A/B switches (profiling only): occupancy target, LDS-staged tables.  Measured at
-        // 1080p C1: 5 waves/SIMD (96 VGPRs; since the cooperative leaf phase 48 B/lane spill,
-        // which 4 waves would avoid: +0.5 %, noise) with LDS tables is fastest; capping
-        // registers lower spills in the traversal loop.
-        static const int occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 5;
+        // Occupancy target per pipeline (WaveBufs::trace_waves), LDS-staged tables; A/B
+        // switches PTX_TRACE_OCC / PTX_TRACE_NOLDS.  Measured at 1080p: 5 waves/SIMD (96 VGPRs,
+        // 48-64 B/lane spill since the cooperative leaf phase) is fastest for the reuse and GI
+        // pipelines on C3, 4 (no spill) for the reference pipeline and TEST_MCPT on C1
+        // (+2.2 % / +2.6 %); 6+ spills in the traversal loop.
+        static const int env_occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 0;
+        const int occ = env_occ ? env_occ : w.trace_waves == 4u ? 4 : 5;
         const bool tables_fit = sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts && !getenv("PTX_TRACE_NOLDS");
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
                  : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
