@@ -47,7 +47,7 @@ constexpr uint32_t kWaveStateSlots = 10u;  // float4 per pixel (PT_1 needs the m
 // PT_1 state slots the reuse pipeline's temporal pass reads (vertex 2 / 3 hit compacts, the
 // selected NEE candidate's Visibility or -1 for an env candidate): ptx_wave.hip IS_*
 constexpr uint32_t kStateCs2 = 7u, kStateCs3 = 8u, kStateTsel = 9u;
-constexpr uint32_t kWaveSegPixels = 512u;  // padded pixels per segment (8 8x8 tiles); 512 > 1024 > 256
+constexpr uint32_t kWaveSegPixels = 768u;  // padded pixels per segment (12 8x8 tiles); 768 > 512 > 1024 > 256
 constexpr int kWaveRoundsInit = 3, kWaveRoundsFinal = 3, kWaveRoundsMcpt = 4;
 constexpr int kWaveMaxRounds = 5;
 struct WaveBufs {

@@ -77,7 +77,8 @@ __device__ __forceinline__ void seg_end(const WaveBufs &w, const Seg &g) {
 // shades one coherent tile, while every segment -- and so every trace workgroup -- sees a
 // sample of the whole image, which keeps the per-segment trace cost even.  Measured at
 // 1080p: spreading beats clustering adjacent tiles (cluster 4: -5 %, 16: -33 %), and
-// 512-pixel segments beat 1024 (+1-3 %), 256 (-9 %) and 2048 (-11 %).
+// 512-pixel segments beat 1024 (+1-3 %), 256 (-9 %) and 2048 (-11 %); since the split active
+// lists and the cooperative traversal, 768 beats 512 (+1 to +4 % per pipeline).
 __device__ __forceinline__ uint32_t seg_pixel(const WaveBufs &w, uint32_t j, uint32_t k) {
     const uint32_t s = (k + threadIdx.x) >> 6;  // tile slot within the segment (seg_px / 64)
     const uint32_t cl = w.cluster;              // runs of `cl` adjacent tiles

@@ -17,7 +17,7 @@ for wl, _ in cols:
     lines[wl] = json.loads(open(os.path.join(d, "bench_line.json")).read())
     calls = total = 0
     for r in csv.DictReader(open(os.path.join(d, "kernel_stats.csv"))):
-        if r["Name"].startswith("void ptx::trace_queue<false, 5"):  # every timed instance (GI: + occlusion)
+        if r["Name"].startswith("void ptx::trace_queue<false, "):  # every timed instance (GI: + occlusion)
             calls += int(r["Calls"])
             total += float(r["TotalDurationNs"])
     if calls:
