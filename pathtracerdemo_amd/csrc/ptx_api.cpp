@@ -381,9 +381,9 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     // streams (e.g. one half's spatial pass beside the other half's PT_4)
     w.act_stride = (uint32_t)(seg_px * jpp);
     w.cnt = (uint32_t *)h->d_wctr.p;
-    // measured per pipeline: the reference's pipeline and TEST_MCPT on C1
-    // trace fastest at 4 waves per SIMD (no spill), the reuse / GI pipelines on C3 at 5
-    w.trace_waves = h->cfg.pipeline == PTX_PIPELINE_RESTIR ? 4u : 5u;
+    // measured per pipeline: 4 waves per SIMD (no spill) for the reference
+    // pipeline / TEST_MCPT and the reuse pipeline, 5 for ReSTIR GI
+    w.trace_waves = h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI ? 5u : 4u;
     w.seg_base = 0;
     w.seg_count = w.nseg;
     static const uint32_t cl = getenv("PTX_SEG_CLUSTER") ? (uint32_t)atoi(getenv("PTX_SEG_CLUSTER")) : 1u;  // A/B

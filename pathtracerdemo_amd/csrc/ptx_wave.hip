@@ -944,10 +944,10 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
         hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     else {
         // Occupancy target per pipeline (WaveBufs::trace_waves), LDS-staged tables; A/B
-        // switches PTX_TRACE_OCC / PTX_TRACE_NOLDS.  Measured at 1080p: 5 waves/SIMD (96 VGPRs,
-        // 48-64 B/lane spill since the cooperative leaf phase) is fastest for the reuse and GI
-        // pipelines on C3, 4 (no spill) for the reference pipeline and TEST_MCPT on C1
-        // (+2.2 % / +2.6 %); 6+ spills in the traversal loop.
+        // switches PTX_TRACE_OCC / PTX_TRACE_NOLDS.  Measured at 1080p with 768-pixel segments:
+        // 4 waves/SIMD (no spill) is fastest for the reference pipeline, TEST_MCPT and reuse
+        // (+2 %, +0-2.6 %, +1.7 % over 5), 5 (96 VGPRs, 48-64 B/lane spill) for ReSTIR GI
+        // (+1.7 % over 4); 6+ spills in the traversal loop.
         static const int env_occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 0;
         const int occ = env_occ ? env_occ : w.trace_waves == 4u ? 4 : 5;
         const bool tables_fit = sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts && !getenv("PTX_TRACE_NOLDS");
