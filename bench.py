@@ -13,11 +13,19 @@ Workload (BASELINE.json configs):
     (build-defined).
   restir / mcpt default to DUMMY_SCENE_1 (Cornell-style room, 22 294 triangles, 3 lights).
 A step = one frame (all passes) over the whole band; inputs (scene, uniform) are resident
-in HBM before the timed region.  Multi-GPU (torchrun): weak scaling, rank r renders rows
-[r*H, (r+1)*H) of a W x (H*N) frame with global pixel coordinates.  restir / mcpt have no
-collective on the data path; reuse swaps reuse_radius halo rows (G-buffer + reservoirs)
-with the neighbouring bands every frame over RCCL (pathtracerdemo_amd/bands.py).  Timing:
-barrier + max-reduce of the elapsed time.
+in HBM before the timed region.
+
+Multi-GPU (`--gpus N`, N > 1): configs[3] by default -- the C3 reuse frame at 3840x2160
+split into N row bands (strong scaling), one process per GPU.  Under torchrun the ranks come
+from the environment; started directly, bench.py spawns the N ranks itself (before anything
+touches a GPU) and exits with their status.  Each rank takes a work census of the full frame
+(counting build, PTX_FLAG_ROW_CENSUS), cuts cost-balanced bands from it
+(pathtracerdemo_amd/bands.py), and renders its band through a handle that owns an RCCL
+communicator: the spatial-reuse halo (reuse_radius rows of G-buffer + reservoirs to and from
+the neighbouring bands) moves by grouped ncclSend/ncclRecv on the handle's stream every
+frame, no host wait (pathtracerdemo_amd/csrc/ptx_comm.cpp).  `--weak` keeps the per-GPU frame
+fixed instead (rank r renders rows [r*H, (r+1)*H) of a W x (H*N) frame).  Timing: barrier +
+max-reduce of the elapsed time.
 """
 from __future__ import annotations
 
@@ -59,7 +67,8 @@ def ray_bytes(c: dict) -> int:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one GPU each); spawned by bench.py itself unless run under torchrun")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["reuse", "restir", "mcpt", "gi"], default="reuse")
@@ -67,8 +76,17 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frame", default=None,
                     help="strong scaling: one fixed WxH frame split into row bands over the ranks "
-                         "(configs[3]: --workload reuse --frame 3840x2160); default: weak scaling, "
-                         "every rank renders --width x --height rows of a taller frame")
+                         "(default with --gpus > 1: 3840x2160, configs[3]); at N = 1 the frame is "
+                         "--width x --height (configs[2])")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling instead: every rank renders --width x --height rows of a taller frame")
+    ap.add_argument("--bands", choices=["balanced", "equal"], default="balanced",
+                    help="strong scaling: band boundaries from the GPU work census, or equal heights")
+    ap.add_argument("--halo", choices=["rccl", "torch"], default="rccl",
+                    help="halo exchange: the handle's own RCCL communicator, or torch.distributed "
+                         "(host-driven, the CPU tests' path)")
+    ap.add_argument("--halo-overlap", action="store_true",
+                    help="spatial pass of the interior rows while the halo is in flight")
     ap.add_argument("--scene", default=None, help="default: c3_interior_32 (reuse), dummy_scene_1 (others)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -77,10 +95,65 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torchrun: start N rank processes of this script (nothing in
+    this process has touched a GPU) and return their worst exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+def census(cs, W, H, pipeline, device, passes):
+    """GPU work census of the full W x H frame (counting build, PTX_FLAG_ROW_CENSUS): frame 1,
+    then frame 2 (history valid, as in the timed region) pass by pass; per pass the (tile rows,
+    5) counters {rays, instance transforms, AABB tests, triangle tests, hits} of ptx_row_census."""
+    from pathtracerdemo_amd import _native as N
+    from pathtracerdemo_amd.renderer import Renderer
+    pid = {"gbuffer": N.PTX_PASS_GBUFFER, "init": N.PTX_PASS_INIT, "final": N.PTX_PASS_FINAL,
+           "mcpt": N.PTX_PASS_MCPT, "temporal": N.PTX_PASS_TEMPORAL, "spatial": N.PTX_PASS_SPATIAL}
+    rc = Renderer(W, H, device=device, pipeline=pipeline, row_census=True)
+    rc.Initialize(cs)
+    rc.Update()
+    rc.Render()
+    rc.Update()
+    out = {}
+    for p in passes:
+        rc.reset_stats()
+        rc.run_pass(pid[p])
+        out[p] = rc.row_census().astype(np.float64)
+    rc.close()
+    return out
+
+
+def band_work(tile_census: np.ndarray, row_begin: int, row_end: int) -> dict:
+    """The counters of rows [row_begin, row_end) from a full-frame tile-row census (a tile row
+    cut by the band counts by its share of rows)."""
+    T = tile_census.shape[0]
+    frac = np.clip(np.minimum(np.arange(1, T + 1) * 8, row_end) - np.maximum(np.arange(T) * 8, row_begin), 0, 8) / 8.0
+    tot = frac @ tile_census
+    keys = ("rays", "instance_xforms", "aabb_tests", "tri_tests", "hits")
+    return {k: int(round(v)) for k, v in zip(keys, tot)}
+
+
 def main():
     args = parse()
-    args.scene = args.scene or DEFAULT_SCENE[args.workload]
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    args.scene = args.scene or DEFAULT_SCENE[args.workload]
+    if world > 1 and not args.weak and not args.frame:
+        args.frame = "3840x2160"  # configs[3]
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -96,26 +169,52 @@ def main():
 
     from pathtracerdemo_amd.renderer import Renderer
     from pathtracerdemo_amd.scene.world import compile_scene
-    from pathtracerdemo_amd.scene.camera import Camera
+    from pathtracerdemo_amd import bands as B
 
     cs = compile_scene(args.scene)
-    if args.frame:  # strong scaling (configs[3]): the ranks share one frame
-        from pathtracerdemo_amd.bands import band
-        W, H = (int(v) for v in args.frame.lower().split("x"))
-        row_begin, row_end = band(H, world, rank)
-        Hb = row_end - row_begin
-    else:  # weak scaling: rank r renders rows [r*Hb, (r+1)*Hb) of a W x (Hb*N) frame
-        W, Hb = args.width, args.height
-        H = Hb * world
-        row_begin, row_end = rank * Hb, (rank + 1) * Hb
     pipeline = args.workload
-    r = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
-                 variant=args.variant)
-    r.Initialize(cs)
-    band_drv = None
-    if pipeline in ("reuse", "gi") and world > 1:
-        from pathtracerdemo_amd.bands import ReuseBand
-        band_drv = ReuseBand(r, rank, world, device=f"cuda:{device}" if backend == "nccl" else "cpu")
+    passes = PASSES[pipeline]
+    strong = bool(args.frame) and not args.weak
+    if strong:  # configs[3]: the ranks share one frame
+        W, H = (int(v) for v in args.frame.lower().split("x"))
+    else:  # weak scaling: rank r renders rows [r*Hb, (r+1)*Hb) of a W x (Hb*N) frame
+        W, H = args.width, args.height * world
+    # work census of the exact frame (counting build, untimed): algorithmic bytes, and the
+    # cost-balanced bands of a strong-scaled frame
+    cen = census(cs, W, H, pipeline, device, passes)
+    radius = 30
+    if strong and world > 1:
+        if args.bands == "balanced":
+            total = sum(cen.values())
+            costs = B.row_costs(total, W, H)
+            all_bands = B.balanced_bands(costs, world, min_rows=radius)
+        else:
+            all_bands = [B.band(H, world, r) for r in range(world)]
+            costs = B.row_costs(sum(cen.values()), W, H)
+        balance = B.band_balance(costs, all_bands)
+    else:
+        all_bands = [B.weak_band(H // world, r) for r in range(world)]
+        balance = 1.0
+    row_begin, row_end = all_bands[rank]
+    Hb = row_end - row_begin
+    reuse = pipeline in ("reuse", "gi")
+    use_comm = reuse and world > 1 and args.halo == "rccl"
+
+    def make(**kw):
+        r = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
+                     variant=args.variant, halo_overlap=args.halo_overlap, **kw)
+        r.Initialize(cs)
+        drv = None
+        if use_comm:  # the handle's own RCCL communicator: ptx_render exchanges the halo
+            obj = [Renderer.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            r.comm_init(obj[0], rank, world)
+        elif reuse and world > 1:
+            from pathtracerdemo_amd.bands import ReuseBand
+            drv = ReuseBand(r, rank, world, device=f"cuda:{device}" if backend == "nccl" else "cpu")
+        return r, drv
+
+    r, band_drv = make()
 
     def frame(rr, drv):
         rr.Update()
@@ -124,22 +223,10 @@ def main():
         else:
             drv.render_frame()
 
-    # work census of the exact frame (counting build, untimed): algorithmic bytes
-    rc = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
-                  count_work=True, variant=args.variant)
-    rc.Initialize(cs)
-    rc.Update()
-    passes = PASSES[pipeline]
-    counts = {}
     from pathtracerdemo_amd import _native as N
     pid = {"gbuffer": N.PTX_PASS_GBUFFER, "init": N.PTX_PASS_INIT, "final": N.PTX_PASS_FINAL,
            "mcpt": N.PTX_PASS_MCPT, "temporal": N.PTX_PASS_TEMPORAL, "spatial": N.PTX_PASS_SPATIAL}
-    for p in passes:
-        rc.reset_stats()
-        rc.run_pass(pid[p])
-        rc.synchronize()
-        counts[p] = rc.read_counters()
-    rc.close()
+    counts = {p: band_work(cen[p], row_begin, row_end) for p in passes}
     px = W * Hb
     pio = PASS_IO_GI if pipeline == "gi" else PASS_IO
     alg_bytes = {p: ray_bytes(counts[p]) + pio[p] * px for p in passes}
@@ -160,6 +247,7 @@ def main():
     r.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    own_elapsed = elapsed
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}" if backend == "nccl" else "cpu")
@@ -168,22 +256,17 @@ def main():
     st = r.stats()
     img = r.read_image()
     nonfinite = int((~np.isfinite(img[..., :3])).sum())
+    r.close()
 
     # Second timed region, same K steps, with HIP events around every wavefront launch
     # (PTX_FLAG_TIME_LAUNCHES costs ~5% of a frame, so the headline region above runs
     # without them): per-launch durations of the dominant kernel for the roofline.  It runs
-    # as ONE launch sequence (PTX_FLAG_SINGLE_STREAM): in the two-stream production frame
-    # two kernels share the GPU and a launch's duration measures the share, not the kernel;
+    # as ONE launch sequence (PTX_FLAG_SINGLE_STREAM): in the multi-stream production frame
+    # kernels share the GPU and a launch's duration measures the share, not the kernel;
     # the overlap's gain is in `value` and in roofline.frame.
     st_k = None
     if args.variant == "wave":
-        rk = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
-                      variant=args.variant, time_launches=True, single_stream=True)
-        rk.Initialize(cs)
-        drv_k = None
-        if band_drv is not None:
-            from pathtracerdemo_amd.bands import ReuseBand
-            drv_k = ReuseBand(rk, rank, world, device=f"cuda:{device}" if backend == "nccl" else "cpu")
+        rk, drv_k = make(time_launches=True, single_stream=True)
         for _ in range(max(1, args.warmup)):
             frame(rk, drv_k)
         rk.synchronize()
@@ -196,6 +279,14 @@ def main():
         st_k = rk.stats()
         rk.close()
 
+    # per-rank band times (rank 0 reports them all)
+    band_ms = [own_elapsed / args.steps * 1e3]
+    if dist is not None:
+        import torch
+        t = torch.zeros(world, dtype=torch.float64, device=f"cuda:{device}" if backend == "nccl" else "cpu")
+        t[rank] = own_elapsed / args.steps * 1e3
+        dist.all_reduce(t)
+        band_ms = [round(float(v), 4) for v in t.tolist()]
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -204,10 +295,10 @@ def main():
     value = samples / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
     if st["kernel_launches"][N.PTX_STAT_FRAME]:
-        # the wavefront ReSTIR frame overlaps its passes on two streams: timed as a whole
+        # the wavefront frame overlaps its passes on several streams: timed as a whole
         kms = {"frame": st["kernel_ms_total"][N.PTX_STAT_FRAME] / st["kernel_launches"][N.PTX_STAT_FRAME]}
     elif st["kernel_launches"][N.PTX_STAT_PASS_GROUP]:
-        # a reuse band: two pass groups around the halo exchange, per frame
+        # a reuse band driven from Python: two pass groups around the halo exchange, per frame
         kms = {"pass_groups": st["kernel_ms_total"][N.PTX_STAT_PASS_GROUP] / args.steps}
     else:
         kms = {p: st["kernel_ms_total"][pid[p]] / max(1, st["kernel_launches"][pid[p]]) for p in passes}
@@ -248,13 +339,18 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads)
         ts_cpu = ts_cpu_baseline(cs, args.scene, W, Hb, args.cpu_threads)
+    if world > 1:
+        workload = (f"{args.scene} {pipeline} {W}x{H} split over {world} GPUs, 1 spp/frame (configs[3])"
+                    if strong else f"{args.scene} {pipeline} {W}x{Hb} per GPU, 1 spp/frame")
+    else:
+        workload = f"{args.scene} {pipeline} {W}x{H}, 1 spp/frame" + (" (configs[2])" if pipeline == "reuse" and
+                                                                        (W, H) == (1920, 1080) else "")
     line = {
         "metric": "Msamples/sec at 1920x1080, 1 spp ReSTIR DI; per-pixel L2 vs WebGPU ref",
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "strong" if args.frame else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": (f"{args.scene} {pipeline} {W}x{H} split over {world} GPU(s), 1 spp/frame"
-                                if args.frame else f"{args.scene} {pipeline} {W}x{Hb} per GPU, 1 spp/frame"),
+        "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": workload,
                    "pipeline": {"restir": "PT_01 gbuffer -> PT_1 init -> PT_4 final",
                                 "reuse": "PT_01 gbuffer -> PT_1 init -> temporal -> spatial (3 neighbours, "
                                          "radius 30, pairwise MIS) -> PT_4 final",
@@ -263,7 +359,10 @@ def main():
                                       "spatial (3 neighbours, radius 30, reconnection shift, pairwise MIS) -> "
                                       "GI shade"}[pipeline],
                    "frame": f"{W}x{H}", "band_rows_per_gpu": Hb,
-                   "parallelism": f"row-bands x{world}"},
+                   "parallelism": f"row-bands x{world}" + (
+                       f", halo over {'the handles RCCL communicators' if use_comm else 'torch.distributed'}"
+                       + (" overlapped with the interior spatial pass" if args.halo_overlap else "")
+                       if reuse and world > 1 else "")},
         "kernel_ms": {p: round(v, 4) for p, v in kms.items()},
         "nonfinite_px": nonfinite,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -276,6 +375,9 @@ def main():
         "cpu_baseline": cpu,
         "ts_cpu_baseline": ts_cpu,
     }
+    if world > 1:
+        line["bands"] = {"rows": [list(b) for b in all_bands], "split": args.bands if strong else "weak",
+                         "predicted_max_over_mean": round(balance, 4), "ms_per_frame_by_rank": band_ms}
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PTX_ABI_VERSION 3
+#define PTX_ABI_VERSION 4
 
 #define PTX_OK 0
 #define PTX_E_INVALID (-1)  /* bad argument / state                  */
@@ -93,6 +93,11 @@ extern "C" {
                                         PTX_STAT_WAVE_*); costs ~5% of frame time            */
 #define PTX_FLAG_SINGLE_STREAM 32u   /* run the wavefront passes as one launch sequence (no
                                         two-stream overlap): isolated per-kernel timings     */
+#define PTX_FLAG_ROW_CENSUS 64u    /* counting build (implies PTX_FLAG_COUNT_WORK) that also keeps the
+                                        work per 8-row tile row of the band, for ptx_row_census;
+                                        the totals of PTX_BUF_COUNTERS stay zero              */
+#define PTX_FLAG_HALO_OVERLAP 128u /* band frames: the spatial pass of the interior rows runs while
+                                        the halo is exchanged, the edge rows after it         */
 /* no variant flag: the wavefront pipeline (compacted ray queues, one trace round per
    path vertex) -- the default */
 
@@ -144,6 +149,34 @@ int ptx_run_passes(ptx_handle *h, const int *passes, int n);
 int ptx_halo_rows(ptx_handle *h, uint32_t *rows_top, uint32_t *rows_bottom, size_t *bytes_per_row);
 int ptx_halo_pack(ptx_handle *h, void *dev_top, void *dev_bottom);
 int ptx_halo_unpack(ptx_handle *h, const void *dev_top, const void *dev_bottom);
+/* ---- multi-GPU: the frame split into row bands, one handle per band.
+ * The one exchange is the spatial-reuse halo: between the temporal and spatial passes a band
+ * receives the G-buffer + reservoir rows of its neighbours (rows_top from the band above,
+ * rows_bottom from the band below; ptx_halo_rows).  The handle owns the RCCL communicator:
+ *   ptx_comm_unique_id  <- ncclGetUniqueId on one rank; the caller ships the 128 bytes to the
+ *                          others (e.g. a torch.distributed broadcast)
+ *   ptx_comm_init       <- ncclCommInitRank for a band handle: rank r is the band above rank
+ *                          r + 1; ptx_render then runs the whole frame, halo included
+ *                          (grouped ncclSend / ncclRecv from the band's edge rows straight into
+ *                          the neighbours' halo rows on the handle's streams, no host wait)
+ *   ptx_comm_init_all   <- ncclCommInitAll: every band handle of ONE process (one per GPU)
+ *   ptx_render_bands    <- one frame over n band handles of one process, in band order
+ *                          (row_end of band i == row_begin of band i + 1): the halo moves over
+ *                          their communicators, or by peer copies when they have none (several
+ *                          bands may then share a GPU); rgba_out (optional) receives the bands'
+ *                          accumulated rows in order (blocking)
+ * Seeds and neighbour offsets use global pixel coordinates: any split renders the single
+ * handle's frame bit for bit. */
+#define PTX_COMM_ID_BYTES 128
+int ptx_comm_unique_id(void *id_out, size_t bytes);
+int ptx_comm_init(ptx_handle *h, const void *unique_id, size_t bytes, int rank, int world);
+int ptx_comm_init_all(ptx_handle *const *handles, int n);
+int ptx_render_bands(ptx_handle *const *handles, int n, float *rgba_out);
+/* Work census of a PTX_FLAG_ROW_CENSUS handle since the last ptx_reset_stats: per 8-row tile
+ * row of the band, 5 u64 {rays, instance transforms, AABB tests, triangle tests, hits} of every
+ * query traced for that row's pixels (the §8(d) algorithmic-bytes counters).  Cost-balanced
+ * band boundaries come from it (pathtracerdemo_amd/bands.py). */
+int ptx_row_census(ptx_handle *h, uint64_t *tile_row_counts, size_t n_tile_rows);
 int ptx_reset_accumulation(ptx_handle *h);
 int ptx_synchronize(ptx_handle *h);
 int ptx_get_stats(ptx_handle *h, ptx_stats *out);

@@ -166,6 +166,23 @@ class Frame:
         self.hist_valid = True
 
 
+    def run_reuse_frame_census(self, threads: int = 0) -> np.ndarray:
+        """run_reuse_frame, pass by pass over one 8-row tile row at a time: returns the
+        (tile rows, 5) work {rays, instance transforms, AABB tests, triangle tests, hits} of
+        every query traced for each tile row's pixels (ptx_row_census's counters).  Every
+        pass reads only the previous passes' complete outputs (the spatial pass the temporal
+        output of all rows), so the frame is the same as run_reuse_frame's."""
+        T = (self.H + 7) // 8
+        out = np.zeros((T, 5), dtype=np.uint64)
+        keys = ("rays", "instance_xforms", "aabb_tests", "tri_tests", "hits")
+        for p in (PASS_GBUFFER, PASS_INIT, PASS_TEMPORAL, PASS_SPATIAL, PASS_FINAL):
+            for t in range(T):
+                rect = (0, 8 * t, self.W, min(self.H, 8 * t + 8))
+                c = self.run(p, threads, rect, reservoir=self.res_hist if p == PASS_FINAL else None)
+                out[t] += np.array([c[k] for k in keys], dtype=np.uint64)
+        self.hist_valid = True
+        return out
+
     def _inputs(self):
         return Inputs(self.uniform.ctypes.data, self.scene.ctypes.data, self.geometry.ctypes.data,
                       self.accel.ctypes.data)

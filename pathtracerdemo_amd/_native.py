@@ -13,7 +13,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTX_LIB_PATH") or os.path.join(PKG_DIR, "libptx.so")
 
 PTX_OK = 0
-PTX_ABI_VERSION = 3
+PTX_ABI_VERSION = 4
 PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT, PTX_PIPELINE_RESTIR_REUSE, PTX_PIPELINE_RESTIR_GI = 0, 1, 2, 3
 PIPELINES = {"restir": PTX_PIPELINE_RESTIR, "mcpt": PTX_PIPELINE_MCPT, "reuse": PTX_PIPELINE_RESTIR_REUSE,
              "gi": PTX_PIPELINE_RESTIR_GI}
@@ -29,6 +29,9 @@ PTX_FLAG_PERSISTENT_LANES = 4
 PTX_FLAG_TILED_EXCHANGE = 8
 PTX_FLAG_TIME_LAUNCHES = 16
 PTX_FLAG_SINGLE_STREAM = 32
+PTX_FLAG_ROW_CENSUS = 64
+PTX_FLAG_HALO_OVERLAP = 128
+PTX_COMM_ID_BYTES = 128
 VARIANT_FLAGS = {"wave": 0, "tiled": PTX_FLAG_TILED_EXCHANGE, "persistent": PTX_FLAG_PERSISTENT_LANES,
                  "simple": PTX_FLAG_SIMPLE_KERNELS}
 
@@ -37,7 +40,8 @@ EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame"
             "ptx_reset_accumulation", "ptx_synchronize", "ptx_get_stats", "ptx_reset_stats", "ptx_read_buffer",
             "ptx_write_buffer", "ptx_device_pointer", "ptx_set_stream", "ptx_destroy", "ptx_last_error",
             "ptx_trace", "ptx_trace_device", "ptx_run_passes", "ptx_halo_rows", "ptx_halo_pack",
-            "ptx_halo_unpack"]
+            "ptx_halo_unpack", "ptx_comm_unique_id", "ptx_comm_init", "ptx_comm_init_all", "ptx_render_bands",
+            "ptx_row_census"]
 
 
 class PtxConfig(ctypes.Structure):
@@ -110,6 +114,11 @@ def load(path: str = LIB_PATH):
                                   ctypes.POINTER(ctypes.c_size_t)]
     lib.ptx_halo_pack.argtypes = [H, P, P]
     lib.ptx_halo_unpack.argtypes = [H, P, P]
+    lib.ptx_comm_unique_id.argtypes = [P, ctypes.c_size_t]
+    lib.ptx_comm_init.argtypes = [H, P, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+    lib.ptx_comm_init_all.argtypes = [ctypes.POINTER(H), ctypes.c_int]
+    lib.ptx_render_bands.argtypes = [ctypes.POINTER(H), ctypes.c_int, P]
+    lib.ptx_row_census.argtypes = [H, P, ctypes.c_size_t]
     lib.ptx_destroy.argtypes = [H]
     lib.ptx_last_error.argtypes = [H]
     lib.ptx_last_error.restype = ctypes.c_char_p

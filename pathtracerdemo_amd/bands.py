@@ -14,6 +14,8 @@ nccl backend, gloo on CPU.  `ReuseBand` drives one frame of a band through that.
 """
 from __future__ import annotations
 
+import numpy as np
+
 
 def band(height: int, world: int, rank: int) -> tuple[int, int]:
     """Strong scaling: rows [begin, end) of a fixed image for `rank` of `world` (balanced)."""
@@ -22,6 +24,70 @@ def band(height: int, world: int, rank: int) -> tuple[int, int]:
     base, extra = divmod(height, world)
     begin = rank * base + min(rank, extra)
     return begin, begin + base + (1 if rank < extra else 0)
+
+
+# SURVEY.md §8(d)'s algorithmic bytes per counted unit of traversal work: AABB test, triangle
+# test, instance transform, hit reconstruction, and the 64-byte ray + hit record per query
+CENSUS_BYTES = np.array([64, 48, 32, 36, 48], dtype=np.float64)  # rays, inst, aabb, tri, hits
+# fixed per-pixel pass IO of the reuse pipeline (bench.py PASS_IO: G-buffer, PT_1, temporal,
+# spatial, PT_4)
+REUSE_PIXEL_BYTES = 16 + (16 + 128) + (16 + 3 * 128) + (4 * (16 + 128) + 128) + (16 + 128 + 16 + 16)
+
+
+def row_costs(tile_census: np.ndarray, width: int, height: int, pixel_bytes: float = REUSE_PIXEL_BYTES) -> np.ndarray:
+    """Predicted cost (algorithmic bytes) of every pixel row of a `height`-row frame from a
+    tile-row census ((T, 5) counters per 8-row tile row, ptx_row_census / the oracle's
+    run_reuse_frame_census) taken on a frame of T*8 >= census rows: each tile row's work is
+    spread evenly over its rows, and a census of another height is resampled (same camera,
+    so census row r covers frame rows r * height / census_rows ...)."""
+    tc = np.asarray(tile_census, dtype=np.float64).reshape(-1, 5) @ CENSUS_BYTES
+    per_row = np.repeat(tc / 8.0, 8)  # census pixel rows (the last tile row may be partial)
+    n = len(per_row)
+    # cumulative cost at census-row boundaries, resampled linearly onto the frame's rows
+    cum = np.concatenate([[0.0], np.cumsum(per_row)])
+    edges = np.linspace(0.0, n, height + 1)
+    cum_f = np.interp(edges, np.arange(n + 1), cum)
+    return np.diff(cum_f) + pixel_bytes * width
+
+
+def balanced_bands(costs, world: int, min_rows: int = 1) -> list[tuple[int, int]]:
+    """Row bands [begin, end) covering len(costs) rows that minimise the largest band cost,
+    every band holding >= min_rows rows (a reuse band must hold the halo radius).  Exact
+    dynamic program over the prefix sums (world x H x H, vectorised over the split row)."""
+    c = np.asarray(costs, dtype=np.float64)
+    H = len(c)
+    if world < 1 or min_rows * world > H:
+        raise ValueError(f"cannot split {H} rows into {world} bands of >= {min_rows} rows")
+    P = np.concatenate([[0.0], np.cumsum(c)])
+    INF = np.inf
+    best = np.full(H + 1, INF)  # best[i]: the smallest max-cost covering rows [0, i) with k bands
+    best[min_rows:] = P[min_rows:]
+    choice = [np.zeros(H + 1, dtype=np.int64)]
+    for k in range(2, world + 1):
+        nb = np.full(H + 1, INF)
+        ch = np.zeros(H + 1, dtype=np.int64)
+        for i in range(k * min_rows, H + 1):
+            j = np.arange((k - 1) * min_rows, i - min_rows + 1)
+            v = np.maximum(best[j], P[i] - P[j])
+            a = int(np.argmin(v))
+            nb[i], ch[i] = v[a], j[a]
+        best = nb
+        choice.append(ch)
+    bounds = [H]
+    i = H
+    for k in range(world, 1, -1):
+        i = int(choice[k - 1][i])
+        bounds.append(i)
+    bounds.append(0)
+    bounds = bounds[::-1]
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def band_balance(costs, bands) -> float:
+    """max / mean predicted band cost (1.0 = perfect)."""
+    c = np.asarray(costs, dtype=np.float64)
+    v = np.array([c[b:e].sum() for b, e in bands])
+    return float(v.max() / v.mean())
 
 
 def weak_band(rows_per_rank: int, rank: int) -> tuple[int, int]:

@@ -16,85 +16,12 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/ptx.h"
-#include "ptx_launch.h"
+#include "ptx_internal.h"
 
-using namespace ptx;
+namespace ptx {
 
-namespace {
 
-constexpr int kPasses = 16;
-constexpr int kEventRing = 256;  // ~15 event pairs per wavefront frame
-
-struct DevBuf {
-    void *p = nullptr;
-    size_t bytes = 0;
-};
-
-struct TimedLaunch {
-    hipEvent_t start = nullptr, stop = nullptr;
-    int pass = -1;
-    bool pending = false;
-};
-
-}  // namespace
-
-struct ptx_handle {
-    ptx_config cfg{};
-    int device = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    std::string err;
-
-    // reference arrays (host copies: the derived layout is rebuilt when offsets change)
-    std::vector<uint32_t> scene, geometry, accel;
-    DevBuf d_scene, d_geometry;
-    // derived MI355X layout
-    DevBuf d_tris, d_nodes, d_subs, d_insts, d_mats, d_tverts;
-    uint32_t n_tris = 0, n_nodes = 0, n_inst = 0, n_subs = 0, max_depth = 0, stack_depth = 0;
-    uint32_t layout_key[8] = {0};
-    bool layout_valid = false;
-    bool scene_loaded = false;
-    // frame
-    uint32_t uniform[PTX_UNIFORM_WORDS] = {0};
-    bool frame_set = false;
-    // band buffers; the G-buffer and PT_1 reservoirs carry halo_top / halo_bot extra rows
-    // (reuse pipeline on a band: the spatial pass reads neighbours up to reuse_radius away)
-    uint32_t band_h = 0, halo_top = 0, halo_bot = 0;
-    DevBuf d_gbuf, d_res, d_accum, d_counters, d_queue;
-    // reuse pipeline: spatial output / history, shift-job state and results
-    DevBuf d_hist, d_jstate, d_jres, d_nbr;
-    // reservoir size in uint4 (8: the reference's 128-byte Reservoir; 4: the GI reservoir)
-    // and the GI pipeline's per-pixel direct light
-    uint32_t res_u4 = 8;
-    DevBuf d_direct;
-    // the wave state holds the PT_1 pass of the reservoirs in d_res (enqueued, nothing since
-    // rewrote them): the reuse temporal pass may read its path hits instead of re-tracing
-    bool init_state_valid = false;
-    // d_nbr holds the summaries of the band's reservoirs as the temporal pass left them
-    // (set by that pass, dropped by anything else that rewrites G-buffer or reservoirs)
-    bool nbr_valid = false;
-    uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
-    bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
-    uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
-    DevBuf d_qrays, d_qhits;  // staging for ptx_trace (host arrays)
-    // wavefront variant: pixel state, ray queue + ping-pong results / active lists, counters
-    DevBuf d_wstate, d_wrays, d_wres0, d_wres1, d_wact0, d_wact1, d_wctr;
-    size_t wave_ray_cap = 0;
-    // second stream: the two halves of the segments run as independent launch sequences so
-    // one half's latency-bound traces overlap the other's ALU-bound shading
-    static constexpr int kMaxSplit = 4;  // GPU_MAX_HW_QUEUES is 4 on the target boxes
-    hipStream_t sub[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};  // sub[0] unused (= stream)
-    hipEvent_t ev_fork = nullptr, ev_join[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
-    // stats
-    TimedLaunch ring[kEventRing];
-    int ring_pos = 0;
-    double ms_total[kPasses] = {};
-    uint64_t launches[kPasses] = {};
-    uint64_t frames = 0;
-};
-
-static int fail(ptx_handle *h, int code, const char *fmt, ...) {
+int fail(ptx_handle *h, int code, const char *fmt, ...) {
     if (h) {
         char buf[512];
         va_list ap;
@@ -105,19 +32,12 @@ static int fail(ptx_handle *h, int code, const char *fmt, ...) {
     }
     return code;
 }
-#define HIP_CHECK(h, expr)                                                                                   \
-    do {                                                                                                     \
-        hipError_t e_ = (expr);                                                                              \
-        if (e_ != hipSuccess) return fail((h), PTX_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
-                                          __FILE__, __LINE__);                                               \
-    } while (0)
-
-static void free_buf(DevBuf &b) {
+void free_buf(DevBuf &b) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
 }
-static int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
+int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
     if (b.bytes == bytes && b.p) return PTX_OK;
     free_buf(b);
     if (bytes == 0) return PTX_OK;
@@ -134,10 +54,10 @@ static int upload(ptx_handle *h, DevBuf &b, const void *src, size_t bytes) {
 }
 
 // first band row of the halo-extended G-buffer / reservoir allocations
-static uint4 *gbuf_band(ptx_handle *h) { return (uint4 *)h->d_gbuf.p + (size_t)h->halo_top * h->cfg.width; }
-static uint4 *res_band(ptx_handle *h) { return (uint4 *)h->d_res.p + h->res_u4 * (size_t)h->halo_top * h->cfg.width; }
+uint4 *gbuf_band(ptx_handle *h) { return (uint4 *)h->d_gbuf.p + (size_t)h->halo_top * h->cfg.width; }
+uint4 *res_band(ptx_handle *h) { return (uint4 *)h->d_res.p + h->res_u4 * (size_t)h->halo_top * h->cfg.width; }
 // pipelines with the build-defined temporal / spatial passes (DI reuse, GI)
-static bool has_reuse(const ptx_handle *h) {
+bool has_reuse(const ptx_handle *h) {
     return h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE || h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI;
 }
 
@@ -151,7 +71,7 @@ static inline float as_f32(uint32_t u) {
 // Walks the reference's per-sub-mesh BLAS (three-mesh-bvh node format, GC/Structs.ts:73-80;
 // read by GetBlasNode, SH/PT_01_GBufferPass.wgsl:310-322) and emits the child-pair node
 // records, the edge-form triangle table and the instance table of ptx_device.h.
-static int build_layout(ptx_handle *h) {
+int build_layout(ptx_handle *h) {
     const uint32_t *U = h->uniform;
     const auto &S = h->scene, &G = h->geometry, &A = h->accel;
     const uint32_t off_desc = U[U_OFF_DESC], off_mat = U[U_OFF_MAT], off_index = U[U_OFF_INDEX];
@@ -308,7 +228,7 @@ static int build_layout(ptx_handle *h) {
     return PTX_OK;
 }
 
-static Scene make_scene(ptx_handle *h) {
+Scene make_scene(ptx_handle *h) {
     Scene sc{};
     std::memcpy(sc.U, h->uniform, sizeof sc.U);
     sc.S = (const uint32_t *)h->d_scene.p;
@@ -326,10 +246,11 @@ static Scene make_scene(ptx_handle *h) {
     sc.row_begin = h->cfg.row_begin;
     sc.row_end = h->cfg.row_end;
     sc.counters = (h->cfg.flags & PTX_FLAG_COUNT_WORK) ? (unsigned long long *)h->d_counters.p : nullptr;
+    sc.census = (h->cfg.flags & PTX_FLAG_ROW_CENSUS) ? (unsigned long long *)h->d_census.p : nullptr;
     return sc;
 }
 
-static void resolve_event(TimedLaunch &t, ptx_handle *h) {
+void resolve_event(TimedLaunch &t, ptx_handle *h) {
     if (!t.pending) return;
     float ms = 0.0f;
     if (hipEventSynchronize(t.stop) == hipSuccess && hipEventElapsedTime(&ms, t.start, t.stop) == hipSuccess) {
@@ -341,7 +262,7 @@ static void resolve_event(TimedLaunch &t, ptx_handle *h) {
 
 // Wavefront buffers, sized for the largest round: PT_1 emits <= 2 rays per pixel, PT_4
 // <= 1, TEST_MCPT <= LightCount + 1 (all shadow rays of a vertex + the next path ray).
-static int wave_buffers(ptx_handle *h, WaveBufs &w) {
+int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t npix = (size_t)h->band_h * h->cfg.width;
     const uint32_t nl = h->uniform[U_LIGHT_COUNT];
     const size_t jpp = has_reuse(h) ? 2u * h->reuse_neighbors : 1u;
@@ -350,12 +271,15 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     static const uint32_t env_px = getenv("PTX_SEG_PX") ? (uint32_t)atoi(getenv("PTX_SEG_PX")) : 0u;  // A/B
     const uint32_t seg_px = (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) ? env_px : kWaveSegPixels;
     const size_t nseg = (padded + seg_px - 1u) / seg_px;
-    const size_t cap = per_px * seg_px * nseg;
+    // queue slots: the whole band, or two tile sets in flight at once (interior + edge rows of
+    // a band's spatial pass: ceil(a/s) + ceil(b/s) <= ceil((a+b)/s) + 1)
+    const size_t slots = nseg + 1u;
+    const size_t cap = per_px * seg_px * slots;
     if (!h->d_wstate.p) {
         if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wact0, nseg * seg_px * jpp * 4u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wact1, nseg * seg_px * jpp * 4u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wctr, 2u * kWaveMaxRounds * nseg * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wact0, slots * seg_px * jpp * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wact1, slots * seg_px * jpp * 4u)) return rc;
+        if (int rc = alloc_buf(h, h->d_wctr, 2u * kWaveMaxRounds * slots * 4u)) return rc;
     }
     if (cap > h->wave_ray_cap) {
         free_buf(h->d_wrays);
@@ -388,6 +312,15 @@ static int wave_buffers(ptx_handle *h, WaveBufs &w) {
     w.seg_count = w.nseg;
     static const uint32_t cl = getenv("PTX_SEG_CLUSTER") ? (uint32_t)atoi(getenv("PTX_SEG_CLUSTER")) : 1u;  // A/B
     w.cluster = (cl == 2u || cl == 4u || cl == 8u || cl == 16u) ? cl : 1u;
+    // row census: a segment is seg_px / 64 tiles adjacent in raster order, so its queue
+    // slot's work belongs to one tile row (two where a tile row's width is not a multiple)
+    if (h->cfg.flags & PTX_FLAG_ROW_CENSUS) w.cluster = seg_px / 64u;
+    w.tile0 = 0;
+    w.ntile0 = (uint32_t)(padded / 64u);
+    w.tile1 = w.ntile1 = 0;
+    w.seg_phys = 0;
+    w.cnt_stride = (uint32_t)slots;
+    h->wave_slots = (uint32_t)slots;
     return PTX_OK;
 }
 
@@ -409,7 +342,7 @@ static void event_end(TimedLaunch *t, hipStream_t st) {
 static size_t px_with_halo(const ptx_handle *h) {
     return (size_t)(h->halo_top + h->band_h + h->halo_bot) * h->cfg.width;
 }
-static int reuse_buffers(ptx_handle *h) {
+int reuse_buffers(ptx_handle *h) {
     const size_t njobs = (size_t)h->band_h * h->cfg.width * 2u * h->reuse_neighbors;
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) return alloc_buf(h, h->d_jres, njobs * 4u);  // ray index per job
     if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
@@ -521,37 +454,44 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
 // over its own segments (a frame: G-buffer -> init -> final per part, nothing shared).
 // PTX_WAVE_STREAMS=1..4 overrides K (A/B: 3 measured best since the cooperative traversal,
 // +2.5 % over 2 on reuse / ReSTIR; 4 oversubscribes the 4 hardware queues).
-static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes,
-                                   int npasses) {
+hipError_t spatial_summaries(ptx_handle *h, hipStream_t st) {
+    if (h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) return hipSuccess;  // GI gathers the buffers
+    const size_t W = h->cfg.width, top = h->halo_top * W, band = (size_t)h->band_h * W;
+    const uint4 *gb = (const uint4 *)h->d_gbuf.p, *rs = (const uint4 *)h->d_res.p;
+    uint4 *nb = (uint4 *)h->d_nbr.p;
+    TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
+    hipError_t e;
+    if (!h->nbr_valid) {
+        e = wave_reuse_summary(gb, rs, nb, px_with_halo(h), st);
+    } else {
+        e = top ? wave_reuse_summary(gb, rs, nb, top, st) : hipSuccess;
+        const size_t b0 = top + band;
+        if (e == hipSuccess && px_with_halo(h) > b0)
+            e = wave_reuse_summary(gb + b0, rs + 8u * b0, nb + b0, px_with_halo(h) - b0, st);
+    }
+    event_end(t, st);
+    return e;
+}
+
+hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes, int npasses,
+                             bool summaries, const WaveBufs *then, hipEvent_t then_wait) {
     static const int env_k = getenv("PTX_WAVE_STREAMS") ? atoi(getenv("PTX_WAVE_STREAMS")) : 0;
     int k = env_k > 0 ? env_k : 3;
     if (h->cfg.flags & PTX_FLAG_SINGLE_STREAM) k = 1;
     k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
-    if ((uint32_t)k > w.nseg) k = (int)w.nseg;
+    if ((uint32_t)k > std::max(w.nseg, then ? then->nseg : 0u)) k = (int)std::max(w.nseg, then ? then->nseg : 0u);
     hipError_t e = hipSuccess;
     // the spatial pass gathers neighbours (halo rows included) through their summaries: the
-    // temporal pass wrote the band's; halo rows (just unpacked) or a band whose buffers were
+    // temporal pass wrote the band's; halo rows (just received) or a band whose buffers were
     // written since get them here
     for (int i = 0; i < npasses; ++i) {
-        if (passes[i] == PTX_PASS_SPATIAL && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
-            const size_t W = h->cfg.width, top = h->halo_top * W, band = (size_t)h->band_h * W;
-            const uint4 *gb = (const uint4 *)h->d_gbuf.p, *rs = (const uint4 *)h->d_res.p;
-            uint4 *nb = (uint4 *)h->d_nbr.p;
-            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, h->stream);
-            if (!h->nbr_valid) {
-                e = wave_reuse_summary(gb, rs, nb, px_with_halo(h), h->stream);
-            } else {
-                e = wave_reuse_summary(gb, rs, nb, top, h->stream);
-                const size_t b0 = top + band;
-                if (e == hipSuccess)
-                    e = wave_reuse_summary(gb + b0, rs + 8u * b0, nb + b0, px_with_halo(h) - b0, h->stream);
-            }
-            event_end(t, h->stream);
-            if (e != hipSuccess) return e;
+        if (passes[i] == PTX_PASS_SPATIAL) {
+            if (summaries && (e = spatial_summaries(h, h->stream)) != hipSuccess) return e;
         } else if (passes[i] != PTX_PASS_FINAL && passes[i] != PTX_PASS_TEMPORAL) {
             h->nbr_valid = false;  // G-buffer / PT_1 / MCPT rewrite what the summaries describe
         }
     }
+    if (k == 0) return hipSuccess;  // empty tile set
     if (k > 1) {
         if (!h->ev_fork && (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return e;
         for (int q = 1; q < k; ++q) {
@@ -566,20 +506,25 @@ static hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBu
             if ((e = hipStreamWaitEvent(h->sub[q], h->ev_fork, 0)) != hipSuccess) return e;
     }
     for (int q = 0; q < k; ++q) {
-        WaveBufs part = w;
-        part.seg_base = (uint32_t)((uint64_t)w.nseg * q / k);
-        part.seg_count = (uint32_t)((uint64_t)w.nseg * (q + 1) / k) - part.seg_base;
         hipStream_t st = q ? h->sub[q] : h->stream;
-        for (int i = 0; i < npasses; ++i) {
-            if (passes[i] == PTX_PASS_GBUFFER) {
-                TimedLaunch *t = event_begin(h, PTX_PASS_GBUFFER, st);
-                e = wave_gbuffer(sc, part, gbuf_band(h), h->stack_depth, st);
-                h->init_state_valid = false;  // PT_1's state described the previous G-buffer
-                event_end(t, st);
-            } else {
-                e = launch_wave_seq(h, sc, part, passes[i], st);
+        for (int set = 0; set < (then ? 2 : 1); ++set) {
+            const WaveBufs &ws = set ? *then : w;
+            if (set && then_wait && (e = hipStreamWaitEvent(st, then_wait, 0)) != hipSuccess) return e;
+            WaveBufs part = ws;
+            part.seg_base = (uint32_t)((uint64_t)ws.nseg * q / k);
+            part.seg_count = (uint32_t)((uint64_t)ws.nseg * (q + 1) / k) - part.seg_base;
+            if (!part.seg_count) continue;
+            for (int i = 0; i < npasses; ++i) {
+                if (passes[i] == PTX_PASS_GBUFFER) {
+                    TimedLaunch *t = event_begin(h, PTX_PASS_GBUFFER, st);
+                    e = wave_gbuffer(sc, part, gbuf_band(h), h->stack_depth, st);
+                    h->init_state_valid = false;  // PT_1's state described the previous G-buffer
+                    event_end(t, st);
+                } else {
+                    e = launch_wave_seq(h, sc, part, passes[i], st);
+                }
+                if (e != hipSuccess) return e;
             }
-            if (e != hipSuccess) return e;
         }
     }
     for (int q = 1; q < k; ++q) {
@@ -600,7 +545,7 @@ static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBuf
 
 // The spatial pass just wrote d_hist for the current camera: the next frame's temporal
 // pass may use it (ptx_set_frame drops it when the camera moves).
-static void mark_history(ptx_handle *h) {
+void mark_history(ptx_handle *h) {
     std::memcpy(h->hist_camera, h->uniform + 4, sizeof h->hist_camera);
     h->hist_valid = true;
 }
@@ -734,6 +679,8 @@ static bool buffer_view(ptx_handle *h, int which, DevBuf &v) {
     }
 }
 
+}  // namespace ptx
+
 // ================================================================ exported C ABI
 extern "C" {
 
@@ -747,9 +694,13 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
         (cfg->flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE)))
         return PTX_E_INVALID;  // the reuse passes exist in wavefront form only
     if (cfg->reuse_neighbors > 16u) return PTX_E_INVALID;
+    if ((cfg->flags & PTX_FLAG_ROW_CENSUS) &&
+        (cfg->flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE)))
+        return PTX_E_INVALID;  // the census maps wavefront queue slots to tile rows
     ptx_handle *h = new (std::nothrow) ptx_handle();
     if (!h) return PTX_E_NOMEM;
     h->cfg = *cfg;
+    if (h->cfg.flags & PTX_FLAG_ROW_CENSUS) h->cfg.flags |= PTX_FLAG_COUNT_WORK;
     if (h->cfg.row_begin == 0 && h->cfg.row_end == 0) h->cfg.row_end = h->cfg.height;
     if (h->cfg.row_begin >= h->cfg.row_end || h->cfg.row_end > h->cfg.height) {
         delete h;
@@ -795,6 +746,13 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!rc) rc = alloc_buf(h, h->d_accum, px * 16u);
     if (!rc) rc = alloc_buf(h, h->d_counters, kCounterWords * 8u);
     if (!rc) rc = alloc_buf(h, h->d_queue, 64u);
+    if (!rc && (h->cfg.flags & PTX_FLAG_ROW_CENSUS)) {
+        // G-buffer tile rows + queue slots (segments hold >= 256 padded pixels: <= padded/256 + 2)
+        const size_t tile_rows = (h->band_h + 7u) / 8u, tiles = tile_rows * ((h->cfg.width + 7u) / 8u);
+        h->census_blocks = (uint32_t)(tile_rows + tiles * 64u / 256u + 2u);
+        rc = alloc_buf(h, h->d_census, (size_t)h->census_blocks * kCensusWords * 8u);
+        if (!rc && hipMemset(h->d_census.p, 0, h->d_census.bytes) != hipSuccess) rc = PTX_E_HIP;
+    }
     if (!rc && hipMemset(h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (!rc && hipMemset(h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (!rc && hipMemset(h->d_gbuf.p, 0, h->d_gbuf.bytes) != hipSuccess) rc = PTX_E_HIP;
@@ -810,6 +768,7 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
 int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const uint32_t *geometry,
                      size_t n_geometry, const uint32_t *accel, size_t n_accel) {
     if (!h) return PTX_E_INVALID;
+    HIP_CHECK(h, hipSetDevice(h->device));  // handles of one process may sit on several GPUs
     if (!scene || !geometry || (!accel && n_accel)) return fail(h, PTX_E_INVALID, "null scene array");
     h->scene.assign(scene, scene + n_scene);
     h->geometry.assign(geometry, geometry + n_geometry);
@@ -827,6 +786,7 @@ int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const
 
 int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]) {
     if (!h || !uniform) return PTX_E_INVALID;
+    HIP_CHECK(h, hipSetDevice(h->device));  // handles of one process may sit on several GPUs
     if (uniform[0] != h->cfg.width || uniform[1] != h->cfg.height)
         return fail(h, PTX_E_INVALID, "uniform resolution %ux%u != handle %ux%u", uniform[0], uniform[1],
                     h->cfg.width, h->cfg.height);
@@ -846,12 +806,14 @@ int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]) {
 
 int ptx_run_pass(ptx_handle *h, int pass) {
     if (!h) return PTX_E_INVALID;
+    HIP_CHECK(h, hipSetDevice(h->device));  // handles of one process may sit on several GPUs
     return timed_launch(h, pass);
 }
 
 int ptx_run_passes(ptx_handle *h, const int *passes, int n) {
     if (!h || (!passes && n)) return PTX_E_INVALID;
     if (n < 0 || n > 8) return fail(h, PTX_E_INVALID, "ptx_run_passes: %d passes", n);
+    HIP_CHECK(h, hipSetDevice(h->device));
     for (int i = 0; i < n; ++i) {
         const int p = passes[i];
         const bool ok = p == PTX_PASS_GBUFFER || p == PTX_PASS_INIT || p == PTX_PASS_FINAL || p == PTX_PASS_MCPT ||
@@ -944,15 +906,24 @@ int ptx_halo_unpack(ptx_handle *h, const void *dev_top, const void *dev_bottom) 
 
 int ptx_render(ptx_handle *h, float *rgba_out) {
     if (!h) return PTX_E_INVALID;
+    HIP_CHECK(h, hipSetDevice(h->device));  // handles of one process may sit on several GPUs
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR) {
         int rc = timed_wave_frame(h);
         if (rc < 0) return rc;
         if (rc == 1)  // other variants / counting builds: pass by pass
             for (int p : {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL})
                 if ((rc = timed_launch(h, p))) return rc;
+    } else if (has_reuse(h) && h->comm) {  // a band of a multi-GPU frame: halo over RCCL
+        if (int rc = render_band_nccl(h)) return rc;
+        if (rgba_out) {
+            HIP_CHECK(h, hipMemcpyAsync(rgba_out, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost, h->stream));
+            HIP_CHECK(h, hipStreamSynchronize(h->stream));
+        }
+        return PTX_OK;
     } else if (has_reuse(h)) {
         if (h->halo_top || h->halo_bot)
-            return fail(h, PTX_E_INVALID, "a band of the reuse pipeline renders through ptx_run_passes + ptx_halo_*");
+            return fail(h, PTX_E_INVALID, "a band of the reuse pipeline renders with a communicator "
+                                          "(ptx_comm_init), through ptx_render_bands, or ptx_run_passes + ptx_halo_*");
         int rc = timed_wave_frame(h);
         if (rc < 0) return rc;
         if (rc == 1)  // counting builds: pass by pass
@@ -1008,6 +979,39 @@ int ptx_reset_stats(ptx_handle *h) {
     for (int p = 0; p < kPasses; ++p) { h->ms_total[p] = 0.0; h->launches[p] = 0; }
     h->frames = 0;
     HIP_CHECK(h, hipMemset(h->d_counters.p, 0, h->d_counters.bytes));
+    if (h->d_census.p) HIP_CHECK(h, hipMemset(h->d_census.p, 0, h->d_census.bytes));
+    return PTX_OK;
+}
+
+int ptx_row_census(ptx_handle *h, uint64_t *out, size_t n_tile_rows) {
+    if (!h || !out) return PTX_E_INVALID;
+    if (!(h->cfg.flags & PTX_FLAG_ROW_CENSUS)) return fail(h, PTX_E_INVALID, "handle has no PTX_FLAG_ROW_CENSUS");
+    const uint32_t tile_rows = (h->band_h + 7u) / 8u, tiles_x = (h->cfg.width + 7u) / 8u;
+    if (n_tile_rows != tile_rows) return fail(h, PTX_E_INVALID, "census: %zu tile rows, band has %u", n_tile_rows, tile_rows);
+    std::vector<unsigned long long> c((size_t)h->census_blocks * kCensusWords);
+    HIP_CHECK(h, hipStreamSynchronize(h->stream));
+    HIP_CHECK(h, hipMemcpy(c.data(), h->d_census.p, c.size() * 8u, hipMemcpyDeviceToHost));
+    std::memset(out, 0, (size_t)tile_rows * 5u * sizeof(uint64_t));
+    for (uint32_t r = 0; r < tile_rows; ++r)
+        for (int k = 0; k < 5; ++k) out[5u * r + k] += c[(size_t)kCensusWords * r + k];
+    // queue slot s traced the rays of segment s: tiles [s*m, s*m + m) in raster order
+    // (m = seg_px / 64); a slot spanning two tile rows is split by its tiles in each
+    static const uint32_t env_px = getenv("PTX_SEG_PX") ? (uint32_t)atoi(getenv("PTX_SEG_PX")) : 0u;
+    const uint32_t seg_px = (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) ? env_px : kWaveSegPixels;
+    const uint32_t m = seg_px / 64u, ntiles = tile_rows * tiles_x;
+    for (uint32_t s = 0; tile_rows + s < h->census_blocks && (size_t)s * m < ntiles; ++s) {
+        const unsigned long long *b = c.data() + (size_t)kCensusWords * (tile_rows + s);
+        const uint32_t t0 = s * m, t1 = std::min(ntiles, t0 + m), r0 = t0 / tiles_x, r1 = (t1 - 1u) / tiles_x;
+        for (int k = 0; k < 5; ++k) {
+            uint64_t left = b[k];
+            for (uint32_t r = r0; r <= r1; ++r) {
+                const uint32_t a = std::max(t0, r * tiles_x), z = std::min(t1, (r + 1u) * tiles_x);
+                const uint64_t part = r == r1 ? left : b[k] * (z - a) / (t1 - t0);
+                out[5u * r + k] += part;
+                left -= part;
+            }
+        }
+    }
     return PTX_OK;
 }
 
@@ -1086,6 +1090,8 @@ int ptx_set_stream(ptx_handle *h, void *hip_stream) {
 
 int ptx_destroy(ptx_handle *h) {
     if (!h) return PTX_E_INVALID;
+    (void)hipSetDevice(h->device);
+    comm_destroy(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (hipStream_t q : h->sub)
         if (q) (void)hipStreamSynchronize(q);
@@ -1097,7 +1103,7 @@ int ptx_destroy(ptx_handle *h) {
     for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
-                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_direct})
+                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_direct, &h->d_census})
         free_buf(*b);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

@@ -1,0 +1,429 @@
+// ptx_comm.cpp -- multi-GPU frames of the reuse pipelines: the RCCL
+// communicator a band handle owns, the spatial-reuse halo exchange, and frames split over
+// several band handles of one process.
+//
+// The reference has no exchange: every WGSL pass reads only its own pixel
+// (GC/Renderer_TEST.ts:208-261).  The build-defined spatial pass
+// (docs/theory/ReSTIR_Pipeline.md:354-462) reads neighbours up to reuse_radius rows away, so
+// a row band needs the G-buffer + reservoir rows of the bands above and below between its
+// temporal and spatial passes.  Here that exchange is device to device on the handle's
+// streams, no host synchronisation anywhere in a frame:
+//   * across processes (one rank per GPU): grouped ncclSend / ncclRecv straight from the
+//     band's first / last rows into the neighbour's halo rows (no pack / unpack copies);
+//   * inside one process (ptx_render_bands, e.g. one Node host driving every GPU, or several
+//     bands on one GPU): the same through the handles' communicators, or hipMemcpyPeerAsync
+//     when the handles have none.
+// PTX_FLAG_HALO_OVERLAP splits the spatial pass into the rows whose neighbourhood lies inside
+// the band (run while the halo is in flight) and the edge rows (run when it has landed).
+//
+// RCCL is loaded with dlopen at ptx_comm_init: in a process that already holds one (torch's
+// bundled librccl.so.1) the loader hands back that copy, and libptx.so stays loadable where
+// no RCCL is installed.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "ptx_internal.h"
+
+namespace ptx {
+namespace {
+
+struct Rccl {
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*init_all)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+    bool ok = false;
+    std::string why;
+};
+
+const Rccl &rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!lib) {
+            const char *e = dlerror();
+            r.why = std::string("dlopen librccl.so.1: ") + (e ? e : "not found");
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto &fn, const char *name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
+            if (!fn) {
+                all = false;
+                r.why = std::string("librccl.so.1 lacks ") + name;
+            }
+        };
+        sym(r.get_unique_id, "ncclGetUniqueId");
+        sym(r.init_rank, "ncclCommInitRank");
+        sym(r.init_all, "ncclCommInitAll");
+        sym(r.send, "ncclSend");
+        sym(r.recv, "ncclRecv");
+        sym(r.group_start, "ncclGroupStart");
+        sym(r.group_end, "ncclGroupEnd");
+        sym(r.destroy, "ncclCommDestroy");
+        sym(r.error_string, "ncclGetErrorString");
+        r.ok = all;
+    });
+    return r;
+}
+
+#define NCCL_CHECK(h, expr)                                                                                  \
+    do {                                                                                                     \
+        ncclResult_t r_ = (expr);                                                                            \
+        if (r_ != ncclSuccess)                                                                               \
+            return fail((h), PTX_E_HIP, "%s: %s (%s:%d)", #expr, rccl().error_string(r_), __FILE__, __LINE__); \
+    } while (0)
+
+// Byte ranges of the halo-extended G-buffer and reservoir allocations: rows [r0, r0 + rows)
+// (row 0 = the first top-halo row).
+struct Rows {
+    char *g, *r;
+    size_t gb, rb;
+};
+Rows rows_of(ptx_handle *h, uint32_t r0, uint32_t rows) {
+    const size_t W = h->cfg.width, rpx = 16u * h->res_u4;
+    return Rows{(char *)h->d_gbuf.p + (size_t)r0 * W * 16u, (char *)h->d_res.p + (size_t)r0 * W * rpx,
+                rows * W * 16u, rows * W * rpx};
+}
+// what this band sends up (its first halo_top rows) / down (its last halo_bot rows), and the
+// halo rows it receives into
+Rows send_up(ptx_handle *h) { return rows_of(h, h->halo_top, h->halo_top); }
+Rows send_down(ptx_handle *h) { return rows_of(h, h->halo_top + h->band_h - h->halo_bot, h->halo_bot); }
+Rows recv_top(ptx_handle *h) { return rows_of(h, 0u, h->halo_top); }
+Rows recv_bottom(ptx_handle *h) { return rows_of(h, h->halo_top + h->band_h, h->halo_bot); }
+
+bool overlap(const ptx_handle *h) { return (h->cfg.flags & PTX_FLAG_HALO_OVERLAP) != 0; }
+
+// The band's tile sets: interior rows (neighbourhood inside the band) and edge rows.
+struct BandSets {
+    WaveBufs interior, edge;
+    bool split = false;
+};
+WaveBufs tile_set(const WaveBufs &w, uint32_t t0, uint32_t n0, uint32_t t1, uint32_t n1, uint32_t phys) {
+    WaveBufs s = w;
+    s.tile0 = t0;
+    s.ntile0 = n0;
+    s.tile1 = t1;
+    s.ntile1 = n1;
+    s.nseg = (uint32_t)(((size_t)(n0 + n1) * 64u + w.seg_px - 1u) / w.seg_px);
+    s.seg_base = 0;
+    s.seg_count = s.nseg;
+    s.seg_phys = phys;
+    return s;
+}
+BandSets band_sets(const ptx_handle *h, const WaveBufs &w) {
+    BandSets b;
+    const uint32_t tx = (h->cfg.width + 7u) / 8u, T = (h->band_h + 7u) / 8u, R = h->reuse_radius;
+    // a pixel of band row y reads rows y - R .. y + R: the top edge is rows [0, R) (tile rows
+    // [0, ceil(R/8))), the bottom edge rows [band_h - R, band_h)
+    const uint32_t e_top = h->halo_top ? std::min(T, (R + 7u) / 8u) : 0u;
+    const uint32_t e_bot = h->halo_bot ? T - std::min(T, (h->band_h - std::min(h->band_h, R)) / 8u) : 0u;
+    if (e_top + e_bot >= T || !(e_top || e_bot)) return b;
+    b.split = true;
+    b.interior = tile_set(w, e_top * tx, (T - e_top - e_bot) * tx, 0u, 0u, 0u);
+    b.edge = tile_set(w, 0u, e_top * tx, (T - e_bot) * tx, e_bot * tx, b.interior.nseg);
+    return b;
+}
+
+// Layout, queue and reuse buffers of a band frame; 1 = not a wavefront band frame.
+int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w) {
+    if (!has_reuse(h)) return fail(h, PTX_E_INVALID, "band frames need the reuse or GI pipeline");
+    if (h->cfg.flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE |
+                        PTX_FLAG_COUNT_WORK))
+        return fail(h, PTX_E_INVALID, "band frames run the wavefront kernels (no counting / A-B variants)");
+    if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before rendering");
+    if (!h->layout_valid)
+        if (int rc = build_layout(h)) return rc;
+    sc = make_scene(h);
+    if (!tables_fit_lds(sc)) return fail(h, PTX_E_SCENE, "band frames need the LDS root / instance tables");
+    if (int rc = wave_buffers(h, w)) return rc;
+    if (int rc = reuse_buffers(h)) return rc;
+    hipError_t e = hipSuccess;
+    if (!h->ev_front && (e = hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming)) != hipSuccess)
+        return fail(h, PTX_E_HIP, "event: %s", hipGetErrorString(e));
+    if (!h->ev_halo && (e = hipEventCreateWithFlags(&h->ev_halo, hipEventDisableTiming)) != hipSuccess)
+        return fail(h, PTX_E_HIP, "event: %s", hipGetErrorString(e));
+    if (!h->xstream && (e = hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(h, PTX_E_HIP, "stream: %s", hipGetErrorString(e));
+    return PTX_OK;
+}
+
+// G-buffer -> PT_1 -> temporal over the whole band, then ev_front on h->stream.
+int band_front(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *&frame_t) {
+    frame_t = &h->ring[h->ring_pos];
+    h->ring_pos = (h->ring_pos + 1) % kEventRing;
+    resolve_event(*frame_t, h);
+    HIP_CHECK(h, hipEventRecord(frame_t->start, h->stream));
+    static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_TEMPORAL};
+    const hipError_t e = launch_wave_parts(h, sc, w, front, 3);
+    if (e != hipSuccess) return fail(h, PTX_E_HIP, "band front passes: %s", hipGetErrorString(e));
+    HIP_CHECK(h, hipEventRecord(h->ev_front, h->stream));
+    return PTX_OK;
+}
+
+// The stream the halo of this band is received on: the exchange stream when the spatial pass
+// overlaps it (forked from ev_front), else the band's own stream.
+int exchange_stream(ptx_handle *h, hipStream_t &xs) {
+    xs = h->stream;
+    if (overlap(h)) {
+        xs = h->xstream;
+        HIP_CHECK(h, hipStreamWaitEvent(xs, h->ev_front, 0));
+    }
+    return PTX_OK;
+}
+
+// Enqueue this band's sends / receives on its communicator (inside a group).
+int nccl_halo(ptx_handle *h, hipStream_t xs) {
+    const Rccl &R = rccl();
+    ncclComm_t c = (ncclComm_t)h->comm;
+    if (h->halo_top) {
+        const Rows s = send_up(h), r = recv_top(h);
+        NCCL_CHECK(h, R.send(s.g, s.gb, ncclUint8, h->rank - 1, c, xs));
+        NCCL_CHECK(h, R.send(s.r, s.rb, ncclUint8, h->rank - 1, c, xs));
+        NCCL_CHECK(h, R.recv(r.g, r.gb, ncclUint8, h->rank - 1, c, xs));
+        NCCL_CHECK(h, R.recv(r.r, r.rb, ncclUint8, h->rank - 1, c, xs));
+    }
+    if (h->halo_bot) {
+        const Rows s = send_down(h), r = recv_bottom(h);
+        NCCL_CHECK(h, R.send(s.g, s.gb, ncclUint8, h->rank + 1, c, xs));
+        NCCL_CHECK(h, R.send(s.r, s.rb, ncclUint8, h->rank + 1, c, xs));
+        NCCL_CHECK(h, R.recv(r.g, r.gb, ncclUint8, h->rank + 1, c, xs));
+        NCCL_CHECK(h, R.recv(r.r, r.rb, ncclUint8, h->rank + 1, c, xs));
+    }
+    return PTX_OK;
+}
+
+// After the halo landed on xs: the halo rows' neighbour summaries, then ev_halo.
+int halo_landed(ptx_handle *h, hipStream_t xs) {
+    if (overlap(h)) {
+        const hipError_t e = spatial_summaries(h, xs);
+        if (e != hipSuccess) return fail(h, PTX_E_HIP, "halo summaries: %s", hipGetErrorString(e));
+    }
+    HIP_CHECK(h, hipEventRecord(h->ev_halo, xs));
+    return PTX_OK;
+}
+
+// Spatial + PT_4.  Without overlap: the whole band after the halo (h->stream carries it).
+// With overlap: each of the K streams runs its share of the interior rows, waits for the
+// halo, then its share of the edge rows (disjoint queue slots, so no join in between).
+int band_back(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *frame_t) {
+    static const int back[2] = {PTX_PASS_SPATIAL, PTX_PASS_FINAL};
+    hipError_t e = hipSuccess;
+    const BandSets b = overlap(h) ? band_sets(h, w) : BandSets{};
+    if (!b.split) {
+        if (overlap(h)) HIP_CHECK(h, hipStreamWaitEvent(h->stream, h->ev_halo, 0));
+        // (with overlap the summaries already ran on the exchange stream)
+        e = launch_wave_parts(h, sc, w, back, 2, !overlap(h));
+    } else {
+        e = launch_wave_parts(h, sc, b.interior, back, 2, false, &b.edge, h->ev_halo);
+    }
+    if (e != hipSuccess) return fail(h, PTX_E_HIP, "band spatial / final passes: %s", hipGetErrorString(e));
+    mark_history(h);
+    HIP_CHECK(h, hipEventRecord(frame_t->stop, h->stream));
+    frame_t->pass = PTX_STAT_FRAME;
+    frame_t->pending = true;
+    h->frames++;
+    return PTX_OK;
+}
+
+}  // namespace
+
+// ptx_render of a band handle that owns a communicator: one whole frame, exchange included.
+int render_band_nccl(ptx_handle *h) {
+    Scene sc{};
+    WaveBufs w{};
+    if (int rc = band_prepare(h, sc, w)) return rc;
+    TimedLaunch *ft = nullptr;
+    if (int rc = band_front(h, sc, w, ft)) return rc;
+    hipStream_t xs;
+    if (int rc = exchange_stream(h, xs)) return rc;
+    NCCL_CHECK(h, rccl().group_start());
+    const int rc = nccl_halo(h, xs);
+    NCCL_CHECK(h, rccl().group_end());
+    if (rc) return rc;
+    if (int r2 = halo_landed(h, xs)) return r2;
+    return band_back(h, sc, w, ft);
+}
+
+}  // namespace ptx
+
+extern "C" {
+
+int ptx_comm_unique_id(void *id_out, size_t bytes) {
+    if (!id_out || bytes != PTX_COMM_ID_BYTES) return PTX_E_INVALID;
+    const Rccl &R = rccl();
+    if (!R.ok) return PTX_E_HIP;
+    ncclUniqueId id;
+    if (R.get_unique_id(&id) != ncclSuccess) return PTX_E_HIP;
+    std::memcpy(id_out, &id, sizeof id);
+    return PTX_OK;
+}
+
+int ptx_comm_init(ptx_handle *h, const void *unique_id, size_t bytes, int rank, int world) {
+    if (!h) return PTX_E_INVALID;
+    if (!unique_id || bytes != PTX_COMM_ID_BYTES || world < 1 || rank < 0 || rank >= world)
+        return fail(h, PTX_E_INVALID, "ptx_comm_init: bad id / rank %d / world %d", rank, world);
+    if (h->comm) return fail(h, PTX_E_INVALID, "ptx_comm_init: the handle already owns a communicator");
+    if ((h->halo_top && rank == 0) || (h->halo_bot && rank == world - 1))
+        return fail(h, PTX_E_INVALID, "ptx_comm_init: band rows [%u,%u) need neighbours rank %d of %d cannot have",
+                    h->cfg.row_begin, h->cfg.row_end, rank, world);
+    const Rccl &R = rccl();
+    if (!R.ok) return fail(h, PTX_E_HIP, "RCCL unavailable: %s", R.why.c_str());
+    HIP_CHECK(h, hipSetDevice(h->device));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof id);
+    ncclComm_t c = nullptr;
+    NCCL_CHECK(h, R.init_rank(&c, world, id, rank));
+    h->comm = c;
+    h->rank = rank;
+    h->world = world;
+    return PTX_OK;
+}
+
+int ptx_comm_init_all(ptx_handle *const *hs, int n) {
+    if (!hs || n < 1 || n > 64) return PTX_E_INVALID;
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) {
+        if (!hs[i]) return PTX_E_INVALID;
+        if (hs[i]->comm) return fail(hs[i], PTX_E_INVALID, "ptx_comm_init_all: the handle already owns a communicator");
+        devs[i] = hs[i]->device;
+        for (int k = 0; k < i; ++k)
+            if (devs[k] == devs[i])
+                return fail(hs[i], PTX_E_INVALID, "ptx_comm_init_all: two handles on device %d (RCCL needs one rank per GPU)",
+                            devs[i]);
+    }
+    const Rccl &R = rccl();
+    if (!R.ok) return fail(hs[0], PTX_E_HIP, "RCCL unavailable: %s", R.why.c_str());
+    std::vector<ncclComm_t> comms(n);
+    NCCL_CHECK(hs[0], R.init_all(comms.data(), n, devs.data()));
+    for (int i = 0; i < n; ++i) {
+        hs[i]->comm = comms[i];
+        hs[i]->rank = i;
+        hs[i]->world = n;
+    }
+    return PTX_OK;
+}
+
+int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
+    if (!hs || n < 1 || n > 64) return PTX_E_INVALID;
+    for (int i = 0; i < n; ++i)
+        if (!hs[i]) return PTX_E_INVALID;
+    ptx_handle *h0 = hs[0];
+    const bool nccl = h0->comm != nullptr;
+    for (int i = 0; i < n; ++i) {
+        ptx_handle *h = hs[i];
+        if (h->cfg.width != h0->cfg.width || h->cfg.height != h0->cfg.height || h->cfg.pipeline != h0->cfg.pipeline)
+            return fail(h, PTX_E_INVALID, "ptx_render_bands: band %d differs in size or pipeline", i);
+        if ((h->comm != nullptr) != nccl)
+            return fail(h, PTX_E_INVALID, "ptx_render_bands: either every band owns a communicator or none");
+        if (nccl && (h->rank != i || h->world != n))
+            return fail(h, PTX_E_INVALID, "ptx_render_bands: band %d is rank %d of %d", i, h->rank, h->world);
+        if (i && hs[i - 1]->cfg.row_end != h->cfg.row_begin)
+            return fail(h, PTX_E_INVALID, "ptx_render_bands: band %d does not start where band %d ends", i, i - 1);
+        if ((i == 0 && h->halo_top) || (i == n - 1 && h->halo_bot))
+            return fail(h, PTX_E_INVALID, "ptx_render_bands: the bands do not cover the halo rows of the ends");
+        if (h->band_h < h->reuse_radius && n > 1)
+            return fail(h, PTX_E_INVALID, "ptx_render_bands: band %d has fewer rows than the reuse radius", i);
+    }
+    std::vector<Scene> sc(n);
+    std::vector<WaveBufs> w(n);
+    std::vector<TimedLaunch *> ft(n);
+    std::vector<hipStream_t> xs(n);
+    for (int i = 0; i < n; ++i) {
+        HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
+        if (int rc = band_prepare(hs[i], sc[i], w[i])) return rc;
+        if (int rc = band_front(hs[i], sc[i], w[i], ft[i])) return rc;
+    }
+    for (int i = 0; i < n; ++i)
+        if (int rc = exchange_stream(hs[i], xs[i])) return rc;
+    if (nccl) {
+        NCCL_CHECK(h0, rccl().group_start());
+        int rc = PTX_OK;
+        for (int i = 0; i < n && !rc; ++i) rc = nccl_halo(hs[i], xs[i]);
+        NCCL_CHECK(h0, rccl().group_end());
+        if (rc) return rc;
+    } else {
+        // peer copies: band i pulls its halo rows from its neighbours' band rows once their
+        // front passes are done
+        for (int i = 0; i < n; ++i) {
+            ptx_handle *h = hs[i];
+            HIP_CHECK(hs[i], hipSetDevice(h->device));
+            if (i > 0 && h->halo_top) {
+                ptx_handle *a = hs[i - 1];
+                const Rows s = send_down(a), r = recv_top(h);
+                if (a->halo_bot != h->halo_top || s.gb != r.gb || s.rb != r.rb)
+                    return fail(h, PTX_E_INVALID, "halo of band %d does not match band %d", i, i - 1);
+                HIP_CHECK(h, hipStreamWaitEvent(xs[i], a->ev_front, 0));
+                HIP_CHECK(h, hipMemcpyPeerAsync(r.g, h->device, s.g, a->device, r.gb, xs[i]));
+                HIP_CHECK(h, hipMemcpyPeerAsync(r.r, h->device, s.r, a->device, r.rb, xs[i]));
+            }
+            if (i + 1 < n && h->halo_bot) {
+                ptx_handle *b = hs[i + 1];
+                const Rows s = send_up(b), r = recv_bottom(h);
+                if (b->halo_top != h->halo_bot || s.gb != r.gb || s.rb != r.rb)
+                    return fail(h, PTX_E_INVALID, "halo of band %d does not match band %d", i, i + 1);
+                HIP_CHECK(h, hipStreamWaitEvent(xs[i], b->ev_front, 0));
+                HIP_CHECK(h, hipMemcpyPeerAsync(r.g, h->device, s.g, b->device, r.gb, xs[i]));
+                HIP_CHECK(h, hipMemcpyPeerAsync(r.r, h->device, s.r, b->device, r.rb, xs[i]));
+            }
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
+        if (int rc = halo_landed(hs[i], xs[i])) return rc;
+    }
+    for (int i = 0; i < n; ++i) {
+        HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
+        if (int rc = band_back(hs[i], sc[i], w[i], ft[i])) return rc;
+    }
+    if (!nccl) {  // the next frame's front passes must not overwrite rows a neighbour still copies
+        for (int i = 0; i < n; ++i) {
+            HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
+            if (i > 0) HIP_CHECK(hs[i], hipStreamWaitEvent(hs[i]->stream, hs[i - 1]->ev_halo, 0));
+            if (i + 1 < n) HIP_CHECK(hs[i], hipStreamWaitEvent(hs[i]->stream, hs[i + 1]->ev_halo, 0));
+        }
+    }
+    if (rgba_out) {  // the bands' accumulated images, in order (rows row_begin(0) .. row_end(n-1))
+        size_t off = 0;
+        for (int i = 0; i < n; ++i) {
+            ptx_handle *h = hs[i];
+            HIP_CHECK(hs[i], hipSetDevice(h->device));
+            HIP_CHECK(h, hipMemcpyAsync((char *)rgba_out + off, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost,
+                                        h->stream));
+            off += h->d_accum.bytes;
+        }
+        for (int i = 0; i < n; ++i) HIP_CHECK(hs[i], hipStreamSynchronize(hs[i]->stream));
+    }
+    return PTX_OK;
+}
+
+}  // extern "C"
+
+namespace ptx {
+void comm_destroy(ptx_handle *h) {
+    if (h->comm && rccl().ok) (void)rccl().destroy((ncclComm_t)h->comm);
+    h->comm = nullptr;
+    if (h->xstream) {
+        (void)hipStreamSynchronize(h->xstream);
+        (void)hipStreamDestroy(h->xstream);
+    }
+    h->xstream = nullptr;
+    if (h->ev_front) (void)hipEventDestroy(h->ev_front);
+    if (h->ev_halo) (void)hipEventDestroy(h->ev_halo);
+    h->ev_front = h->ev_halo = nullptr;
+}
+}  // namespace ptx

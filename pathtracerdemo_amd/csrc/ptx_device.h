@@ -78,6 +78,11 @@ struct Scene {
     uint32_t n_inst, n_subs;
     uint32_t width, height, row_begin, row_end;
     unsigned long long *counters;  // nullptr unless PTX_FLAG_COUNT_WORK
+    // PTX_FLAG_ROW_CENSUS (counting builds): the work counters go to per-region blocks of
+    // kCensusWords instead -- block r < census_tile_rows(): G-buffer rays of band tile row r
+    // (8 pixel rows); block census_tile_rows() + s: every query of trace-queue slot s
+    // (segments of contiguous tiles in census mode, so the host maps them to tile rows)
+    unsigned long long *census;
 };
 
 // ------------------------------------------------------------------ f32 vector algebra
@@ -147,6 +152,7 @@ enum { CNT_RAYS = 0, CNT_INST = 1, CNT_AABB = 2, CNT_TRI = 3, CNT_HITS = 4 };
 // {wave-level executions, active lanes summed over them} at counters[8 + 2*region]
 enum { PROF_ROOT = 0, PROF_NODE = 1, PROF_LEAF = 2, PROF_TRI = 3, PROF_INST = 4, PROF_REGIONS = 5 };
 constexpr int kCounterWords = 32;
+constexpr int kCensusWords = 8;  // one census block: CNT_* counters (5 used)
 struct Prof {
     uint32_t wave[PROF_REGIONS], lane[PROF_REGIONS];
     __device__ __forceinline__ void hit(int r) {

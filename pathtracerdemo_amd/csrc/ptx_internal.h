@@ -1,0 +1,126 @@
+// ptx_internal.h -- the handle behind the C ABI (include/ptx.h) and the host helpers shared
+// by ptx_api.cpp (single-handle entry points) and ptx_comm.cpp (RCCL communicator, halo
+// exchange and multi-band frames).  Not installed; not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/ptx.h"
+#include "ptx_launch.h"
+
+namespace ptx {
+constexpr int kPasses = 16;
+constexpr int kEventRing = 256;  // ~15 event pairs per wavefront frame
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+struct TimedLaunch {
+    hipEvent_t start = nullptr, stop = nullptr;
+    int pass = -1;
+    bool pending = false;
+};
+}  // namespace ptx
+
+using namespace ptx;
+
+struct ptx_handle {
+    ptx_config cfg{};
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // reference arrays (host copies: the derived layout is rebuilt when offsets change)
+    std::vector<uint32_t> scene, geometry, accel;
+    DevBuf d_scene, d_geometry;
+    // derived MI355X layout
+    DevBuf d_tris, d_nodes, d_subs, d_insts, d_mats, d_tverts;
+    uint32_t n_tris = 0, n_nodes = 0, n_inst = 0, n_subs = 0, max_depth = 0, stack_depth = 0;
+    uint32_t layout_key[8] = {0};
+    bool layout_valid = false;
+    bool scene_loaded = false;
+    // frame
+    uint32_t uniform[PTX_UNIFORM_WORDS] = {0};
+    bool frame_set = false;
+    // band buffers; the G-buffer and PT_1 reservoirs carry halo_top / halo_bot extra rows
+    // (reuse pipeline on a band: the spatial pass reads neighbours up to reuse_radius away)
+    uint32_t band_h = 0, halo_top = 0, halo_bot = 0;
+    DevBuf d_gbuf, d_res, d_accum, d_counters, d_queue;
+    // reuse pipeline: spatial output / history, shift-job state and results
+    DevBuf d_hist, d_jstate, d_jres, d_nbr;
+    // reservoir size in uint4 (8: the reference's 128-byte Reservoir; 4: the GI reservoir)
+    // and the GI pipeline's per-pixel direct light
+    uint32_t res_u4 = 8;
+    DevBuf d_direct;
+    // the wave state holds the PT_1 pass of the reservoirs in d_res (enqueued, nothing since
+    // rewrote them): the reuse temporal pass may read its path hits instead of re-tracing
+    bool init_state_valid = false;
+    // d_nbr holds the summaries of the band's reservoirs as the temporal pass left them
+    // (set by that pass, dropped by anything else that rewrites G-buffer or reservoirs)
+    bool nbr_valid = false;
+    uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
+    bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
+    uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
+    DevBuf d_qrays, d_qhits;  // staging for ptx_trace (host arrays)
+    // wavefront variant: pixel state, ray queue + ping-pong results / active lists, counters
+    DevBuf d_wstate, d_wrays, d_wres0, d_wres1, d_wact0, d_wact1, d_wctr;
+    size_t wave_ray_cap = 0;
+    // second stream: the two halves of the segments run as independent launch sequences so
+    // one half's latency-bound traces overlap the other's ALU-bound shading
+    static constexpr int kMaxSplit = 4;  // GPU_MAX_HW_QUEUES is 4 on the target boxes
+    hipStream_t sub[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};  // sub[0] unused (= stream)
+    hipEvent_t ev_fork = nullptr, ev_join[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
+    // queue slots wave_buffers allocated (WaveBufs::cnt_stride)
+    uint32_t wave_slots = 0;
+    // row census (PTX_FLAG_ROW_CENSUS): kCensusWords u64 per G-buffer tile row + queue slot
+    DevBuf d_census;
+    uint32_t census_blocks = 0;
+    // multi-GPU (ptx_comm.cpp): the RCCL communicator this handle owns (ncclComm_t), its
+    // rank and world; the halo exchange stream and its fork / done events
+    void *comm = nullptr;
+    int rank = 0, world = 1;
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_front = nullptr, ev_halo = nullptr;
+    // stats
+    TimedLaunch ring[kEventRing];
+    int ring_pos = 0;
+    double ms_total[kPasses] = {};
+    uint64_t launches[kPasses] = {};
+    uint64_t frames = 0;
+};
+
+namespace ptx {
+int fail(ptx_handle *h, int code, const char *fmt, ...);
+#define HIP_CHECK(h, expr)                                                                                   \
+    do {                                                                                                     \
+        hipError_t e_ = (expr);                                                                              \
+        if (e_ != hipSuccess) return fail((h), PTX_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                                          __FILE__, __LINE__);                                               \
+    } while (0)
+void free_buf(DevBuf &b);
+int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes);
+// first band row of the halo-extended G-buffer / reservoir allocations
+uint4 *gbuf_band(ptx_handle *h);
+uint4 *res_band(ptx_handle *h);
+bool has_reuse(const ptx_handle *h);
+int build_layout(ptx_handle *h);
+Scene make_scene(ptx_handle *h);
+void resolve_event(TimedLaunch &t, ptx_handle *h);
+int wave_buffers(ptx_handle *h, WaveBufs &w);
+int reuse_buffers(ptx_handle *h);
+// Passes over the launch's segments as K independent sequences on K streams, joined on
+// h->stream.  summaries: the spatial pass's neighbour-summary prologue (halo rows) runs
+// first; an interior tile set (halo not yet received) runs without it.  then: a second tile
+// set (disjoint queue slots) each stream runs after its share of the first, once
+// `then_wait` has fired -- no join in between.
+hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes, int npasses,
+                             bool summaries = true, const WaveBufs *then = nullptr, hipEvent_t then_wait = nullptr);
+// the neighbour summaries of the halo rows (or of everything when the band's are stale)
+hipError_t spatial_summaries(ptx_handle *h, hipStream_t st);
+void mark_history(ptx_handle *h);
+// ptx_comm.cpp: a frame of a band handle that owns a communicator; its teardown
+int render_band_nccl(ptx_handle *h);
+void comm_destroy(ptx_handle *h);
+}  // namespace ptx

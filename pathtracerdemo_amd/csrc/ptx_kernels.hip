@@ -77,6 +77,7 @@ __global__ __launch_bounds__(BLOCK) void gbuffer_kernel(Scene sc, uint4 *gbuf) {
     if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
     uint32_t x, y;
     if (!pixel_of(sc, x, y)) return;
+    if (COUNT && sc.census) sc.counters = sc.census + (size_t)kCensusWords * ((y - sc.row_begin) / 8u);  // row census
     uint32_t *stack = lds_stack + threadIdx.x;
     Hit h = trace_core_tab<COUNT, false, false>(sc, LDS_TABLES ? l_subs : sc.subs, LDS_TABLES ? l_insts : sc.insts,
                                   camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);

@@ -65,6 +65,15 @@ struct WaveBufs {
     uint32_t act_stride; // list entries per segment (seg_px; seg_px * jobs per pixel for reuse)
     uint32_t *cnt;       // 2 * kWaveMaxRounds * nseg counts
     uint32_t trace_waves;  // trace_queue occupancy target (waves per SIMD; 4 or 5, per pipeline)
+    // Tile set of the launch: virtual tile v (what the segments spread over) is band tile
+    // v < ntile0 ? tile0 + v : tile1 + (v - ntile0), for v < ntile0 + ntile1 (8x8 tiles in
+    // raster order).  Default: the whole band.  A band's spatial pass runs its interior rows
+    // and its halo-dependent edge rows as two tile sets (the exchange overlaps the first).
+    uint32_t tile0, ntile0, tile1, ntile1;
+    // Queue memory: virtual segment j lives in physical slot seg_phys + j (ray / result / list
+    // storage, count words at cnt[(2r or 2r+1) * cnt_stride + slot]).  Two tile sets in flight
+    // at once use disjoint physical slots.
+    uint32_t seg_phys, cnt_stride;
 };
 // occ_only: every query of the round is Q_OCC (any-hit kernel instance)
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t stack_depth,

@@ -53,8 +53,10 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
     const SubRoot *subs = LDS_TABLES ? l_subs : sc.subs;
     const Inst *insts = LDS_TABLES ? l_insts : sc.insts;
-    const uint32_t j = w.seg_base + blockIdx.x;
-    const uint32_t n = w.cnt[(2u * round + 1u) * w.nseg + j];
+    const uint32_t j = w.seg_phys + w.seg_base + blockIdx.x;  // physical queue slot
+    const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
+    if (COUNT && sc.census)  // row census: this slot's queries count into its own block
+        sc.counters = sc.census + (size_t)kCensusWords * ((sc.row_end - sc.row_begin + 7u) / 8u + j);
     const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
     float4 *res = w.res[round & 1u] + 2u * (size_t)j * w.ray_stride;
     // Every lane of the wave calls the traversal every time -- lanes without a query (past
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(WB) void wgbuffer(Scene sc, WaveBufs w, uint4 *gbuf
     // (seg_pixel's layout, cluster 1); walking them in raster order gives each workgroup 4
     // adjacent tiles (a 32x8 strip) -- primary rays of one CU then share BVH nodes in L1.
     const uint32_t L = blockIdx.x * 4u + threadIdx.x / 64u, run = w.cluster * w.seg_count;
-    const uint32_t t = (L / run) * w.cluster * w.nseg + w.cluster * w.seg_base + L % run;
+    const uint32_t t = set_tile(w, (L / run) * w.cluster * w.nseg + w.cluster * w.seg_base + L % run);
     const uint32_t q = t * 64u + (threadIdx.x & 63u);
     uint32_t x, y;
     if (q >= padded_pixels(sc) || !tile_xy(sc, q, x, y)) return;
@@ -927,15 +929,16 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
     }
     static const bool refill = getenv("PTX_TRACE_REFILL") != nullptr;  // A/B switch for profiling
     if (refill) {
-        const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.nseg + w.seg_base;
-        float4 *res = w.res[round & 1] + 2u * (size_t)w.seg_base * w.ray_stride;
+        const uint32_t pb = w.seg_phys + w.seg_base;
+        const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.cnt_stride + pb;
+        float4 *res = w.res[round & 1] + 2u * (size_t)pb * w.ray_stride;
         if (sc.counters)
             hipLaunchKernelGGL(trace_queue_sm<true>, dim3(w.seg_count), dim3(WB), lds, s, sc,
-                               w.rays + 2u * (size_t)w.seg_base * w.ray_stride, res, cnt,
+                               w.rays + 2u * (size_t)pb * w.ray_stride, res, cnt,
                                w.ray_stride, 0u, eps);
         else
             hipLaunchKernelGGL(trace_queue_sm<false>, dim3(w.seg_count), dim3(WB), lds, s, sc,
-                               w.rays + 2u * (size_t)w.seg_base * w.ray_stride, res, cnt,
+                               w.rays + 2u * (size_t)pb * w.ray_stride, res, cnt,
                                w.ray_stride, 0u, eps);
     } else if (sc.counters && getenv("PTX_TRACE_PROF"))  // SIMD-utilisation diagnostics
         hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round,

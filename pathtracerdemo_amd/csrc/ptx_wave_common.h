@@ -39,7 +39,8 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t *lds_ctr, uint32_t n) {
 
 // This workgroup's view of one logic round: its segments of the queues and LDS counters.
 struct Seg {
-    uint32_t j, round;
+    uint32_t j, round;         // virtual segment (pixel layout), round
+    uint32_t pj;               // its physical queue slot
     uint32_t rbase;            // first ray slot of the segment
     float4 *rays, *res_out;    // rays emitted this round + their result/payload slots
     const float4 *res_in;      // results of the previous trace round
@@ -51,14 +52,15 @@ struct Seg {
 __device__ __forceinline__ Seg seg_begin(const WaveBufs &w, uint32_t round, uint32_t *lds) {
     Seg g;
     g.j = w.seg_base + blockIdx.x;
+    g.pj = w.seg_phys + g.j;
     g.round = round;
-    g.rbase = g.j * w.ray_stride;
+    g.rbase = g.pj * w.ray_stride;
     g.rays = w.rays;
     g.res_out = w.res[round & 1u];
     g.res_in = w.res[(round + 1u) & 1u];
-    g.act_out = w.act[round & 1u] + (size_t)g.j * w.act_stride;
-    g.act_in = w.act[(round + 1u) & 1u] + (size_t)g.j * w.act_stride;
-    g.n_in = round ? w.cnt[(2u * (round - 1u)) * w.nseg + g.j] : 0u;
+    g.act_out = w.act[round & 1u] + (size_t)g.pj * w.act_stride;
+    g.act_in = w.act[(round + 1u) & 1u] + (size_t)g.pj * w.act_stride;
+    g.n_in = round ? w.cnt[(2u * (round - 1u)) * w.cnt_stride + g.pj] : 0u;
     g.l_ray = lds;
     g.l_act = lds + 1;
     if (threadIdx.x == 0) { lds[0] = 0u; lds[1] = 0u; }
@@ -68,8 +70,8 @@ __device__ __forceinline__ Seg seg_begin(const WaveBufs &w, uint32_t round, uint
 __device__ __forceinline__ void seg_end(const WaveBufs &w, const Seg &g) {
     __syncthreads();
     if (threadIdx.x == 0) {
-        w.cnt[(2u * g.round) * w.nseg + g.j] = *g.l_act;
-        w.cnt[(2u * g.round + 1u) * w.nseg + g.j] = *g.l_ray;
+        w.cnt[(2u * g.round) * w.cnt_stride + g.pj] = *g.l_act;
+        w.cnt[(2u * g.round + 1u) * w.cnt_stride + g.pj] = *g.l_ray;
     }
 }
 // Padded pixel handled by this thread at offset k of segment j.  A segment is seg_px/64
@@ -79,10 +81,15 @@ __device__ __forceinline__ void seg_end(const WaveBufs &w, const Seg &g) {
 // 1080p: spreading beats clustering adjacent tiles (cluster 4: -5 %, 16: -33 %), and
 // 512-pixel segments beat 1024 (+1-3 %), 256 (-9 %) and 2048 (-11 %); since the split active
 // lists and the cooperative traversal, 768 beats 512 (+1 to +4 % per pipeline).
+// Band tile of virtual tile v of the launch's tile set (WaveBufs::tile0..ntile1); past the
+// set's end a tile index whose pixels fail every `q < padded_pixels` test.
+__device__ __forceinline__ uint32_t set_tile(const WaveBufs &w, uint32_t v) {
+    return v < w.ntile0 ? w.tile0 + v : v - w.ntile0 < w.ntile1 ? w.tile1 + (v - w.ntile0) : 0x3ffffffu;
+}
 __device__ __forceinline__ uint32_t seg_pixel(const WaveBufs &w, uint32_t j, uint32_t k) {
     const uint32_t s = (k + threadIdx.x) >> 6;  // tile slot within the segment (seg_px / 64)
     const uint32_t cl = w.cluster;              // runs of `cl` adjacent tiles
-    const uint32_t t = ((s / cl) * w.nseg + j) * cl + s % cl;
+    const uint32_t t = set_tile(w, ((s / cl) * w.nseg + j) * cl + s % cl);
     return t * 64u + (threadIdx.x & 63u);
 }
 // append the active pixel to this round's list (all lanes)
@@ -110,8 +117,8 @@ __device__ __forceinline__ void job_keep(const Seg &g, const JobLists &L, bool k
 __device__ __forceinline__ void job_seg_end(const WaveBufs &w, const Seg &g, const JobLists &L) {
     __syncthreads();
     if (threadIdx.x == 0) {
-        w.cnt[(2u * g.round) * w.nseg + g.j] = *g.l_act | (*L.l_light << 16);
-        w.cnt[(2u * g.round + 1u) * w.nseg + g.j] = *g.l_ray;
+        w.cnt[(2u * g.round) * w.cnt_stride + g.pj] = *g.l_act | (*L.l_light << 16);
+        w.cnt[(2u * g.round + 1u) * w.cnt_stride + g.pj] = *g.l_ray;
     }
 }
 

@@ -19,14 +19,19 @@
 
 typedef struct {
     ptx_handle *h;
-    int busy;  /* a renderAsync is in flight */
+    int busy;             /* a renderAsync / renderBandsAsync is in flight */
+    uint32_t width, band_h; /* image rows of this handle (ptx_render's output: band_h*W*4 f32) */
 } Handle;
 
+#define MAX_BANDS 64
 typedef struct {
     napi_async_work work;
     napi_deferred deferred;
-    napi_ref out_ref; /* keeps the output Float32Array alive */
-    Handle *H;
+    napi_ref out_ref;             /* keeps the output Float32Array alive */
+    napi_ref h_ref[MAX_BANDS];    /* keeps the handles alive while the job runs */
+    Handle *H[MAX_BANDS];
+    int n;                        /* handles: 1 (renderAsync) or the bands (renderBandsAsync) */
+    int bands;                    /* ptx_render_bands instead of ptx_render */
     float *out;
     int rc;
     char err[512];
@@ -40,6 +45,9 @@ typedef struct {
         }                                                                        \
     } while (0)
 
+static int typed_view(napi_env env, napi_value v, void **data, size_t *count, size_t *elem,
+                      napi_typedarray_type *type_out);
+
 static napi_value throw_ptx(napi_env env, Handle *H, int rc, const char *what) {
     char msg[768];
     const char *detail = H && H->h ? ptx_last_error(H->h) : "";
@@ -52,10 +60,15 @@ static void finalize_handle(napi_env env, void *data, void *hint) {
     (void)env;
     (void)hint;
     Handle *H = (Handle *)data;
-    if (H && H->h && !H->busy) ptx_destroy(H->h);
+    /* an async job holds a reference to its handles, so a busy handle is never collected;
+       at environment teardown with a job still queued, leak rather than free under it */
+    if (!H || H->busy) return;
+    if (H->h) ptx_destroy(H->h);
     free(H);
 }
 
+/* The handle behind a JS external.  Every entry point that touches the ptx handle requires
+ * it idle: a handle is single-threaded (include/ptx.h) and an async render owns it. */
 static Handle *get_handle(napi_env env, napi_value v) {
     void *p = NULL;
     if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
@@ -67,7 +80,35 @@ static Handle *get_handle(napi_env env, napi_value v) {
         napi_throw_error(env, NULL, "ptx handle already destroyed");
         return NULL;
     }
+    if (H->busy) {
+        napi_throw_error(env, NULL, "an async render is in flight on this handle");
+        return NULL;
+    }
     return H;
+}
+
+/* Optional Float32Array output of at least `need` floats (argv[i] absent / null -> NULL). */
+static int get_out(napi_env env, size_t argc, napi_value *argv, size_t i, size_t need, float **out) {
+    *out = NULL;
+    if (argc <= i) return 0;
+    napi_valuetype vt;
+    napi_typeof(env, argv[i], &vt);
+    if (vt == napi_undefined || vt == napi_null) return 0;
+    void *p;
+    size_t n, es;
+    napi_typedarray_type t;
+    if (typed_view(env, argv[i], &p, &n, &es, &t) || t != napi_float32_array) {
+        napi_throw_type_error(env, NULL, "out must be a Float32Array");
+        return -1;
+    }
+    if (n < need) {
+        char msg[160];
+        snprintf(msg, sizeof msg, "out holds %zu floats; the image needs %zu (rows * width * 4)", n, need);
+        napi_throw_range_error(env, NULL, msg);
+        return -1;
+    }
+    *out = (float *)p;
+    return 0;
 }
 
 static int get_u32_prop(napi_env env, napi_value obj, const char *name, uint32_t dflt, uint32_t *out) {
@@ -150,6 +191,8 @@ static napi_value js_create(napi_env env, napi_callback_info info) {
         return NULL;
     }
     H->h = h;
+    H->width = cfg.width;
+    H->band_h = (cfg.row_begin == 0 && cfg.row_end == 0 ? cfg.height : cfg.row_end) - cfg.row_begin;
     napi_value ext;
     CHECK_NAPI(env, napi_create_external(env, H, finalize_handle, NULL, &ext));
     return ext;
@@ -203,25 +246,8 @@ static napi_value js_render(napi_env env, napi_callback_info info) {
     CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
     if (!H) return NULL;
-    if (H->busy) {
-        napi_throw_error(env, NULL, "a renderAsync is in flight on this handle");
-        return NULL;
-    }
     float *out = NULL;
-    if (argc >= 2) {
-        napi_valuetype vt;
-        napi_typeof(env, argv[1], &vt);
-        if (vt != napi_undefined && vt != napi_null) {
-            void *p;
-            size_t n, es;
-            napi_typedarray_type t;
-            if (typed_view(env, argv[1], &p, &n, &es, &t) || t != napi_float32_array) {
-                napi_throw_type_error(env, NULL, "render(h, out): out must be a Float32Array (band_h*W*4)");
-                return NULL;
-            }
-            out = (float *)p;
-        }
-    }
+    if (get_out(env, argc, argv, 1, (size_t)H->band_h * H->width * 4u, &out)) return NULL;
     int rc = ptx_render(H->h, out);
     if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_render");
     return NULL;
@@ -230,14 +256,23 @@ static napi_value js_render(napi_env env, napi_callback_info info) {
 static void render_execute(napi_env env, void *data) {
     (void)env;
     RenderJob *J = (RenderJob *)data;
-    J->rc = ptx_render(J->H->h, J->out);
-    if (J->rc == PTX_OK) J->rc = ptx_synchronize(J->H->h);
-    if (J->rc != PTX_OK) snprintf(J->err, sizeof J->err, "ptx_render failed (%d): %s", J->rc, ptx_last_error(J->H->h));
+    ptx_handle *hs[MAX_BANDS];
+    for (int i = 0; i < J->n; ++i) hs[i] = J->H[i]->h;
+    J->rc = J->bands ? ptx_render_bands(hs, J->n, J->out) : ptx_render(hs[0], J->out);
+    for (int i = 0; i < J->n && J->rc == PTX_OK; ++i) J->rc = ptx_synchronize(hs[i]);
+    if (J->rc != PTX_OK) {
+        const char *m = "";
+        for (int i = 0; i < J->n && !*m; ++i) m = ptx_last_error(hs[i]);
+        snprintf(J->err, sizeof J->err, "render failed (%d): %s", J->rc, m);
+    }
 }
 
 static void render_complete(napi_env env, napi_status status, void *data) {
     RenderJob *J = (RenderJob *)data;
-    J->H->busy = 0;
+    for (int i = 0; i < J->n; ++i) {
+        J->H[i]->busy = 0;
+        if (J->h_ref[i]) napi_delete_reference(env, J->h_ref[i]);
+    }
     napi_value v;
     if (status == napi_ok && J->rc == PTX_OK) {
         napi_get_undefined(env, &v);
@@ -253,46 +288,169 @@ static void render_complete(napi_env env, napi_status status, void *data) {
     free(J);
 }
 
-/* renderAsync(h [, Float32Array out]) -> Promise: ptx_render + synchronize off the event loop */
+/* Queue a render job over handles argv_h[0..n) (already validated idle). */
+static napi_value queue_render(napi_env env, napi_value *argv_h, Handle **H, int n, int bands, napi_value out_v,
+                               float *out) {
+    RenderJob *J = (RenderJob *)calloc(1, sizeof(RenderJob));
+    if (!J) {
+        napi_throw_error(env, NULL, "out of memory");
+        return NULL;
+    }
+    J->n = n;
+    J->bands = bands;
+    J->out = out;
+    if (out) CHECK_NAPI(env, napi_create_reference(env, out_v, 1, &J->out_ref));
+    for (int i = 0; i < n; ++i) {
+        J->H[i] = H[i];
+        CHECK_NAPI(env, napi_create_reference(env, argv_h[i], 1, &J->h_ref[i]));
+    }
+    napi_value promise, name;
+    CHECK_NAPI(env, napi_create_promise(env, &J->deferred, &promise));
+    CHECK_NAPI(env, napi_create_string_utf8(env, bands ? "ptx_render_bands" : "ptx_render", NAPI_AUTO_LENGTH, &name));
+    CHECK_NAPI(env, napi_create_async_work(env, NULL, name, render_execute, render_complete, J, &J->work));
+    for (int i = 0; i < n; ++i) H[i]->busy = 1;
+    CHECK_NAPI(env, napi_queue_async_work(env, J->work));
+    return promise;
+}
+
+/* renderAsync(h [, Float32Array out]) -> Promise: ptx_render + synchronize off the event loop;
+ * the handle stays busy (every other call on it throws) until the promise settles */
 static napi_value js_render_async(napi_env env, napi_callback_info info) {
     size_t argc = 2;
     napi_value argv[2];
     CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
     if (!H) return NULL;
-    if (H->busy) {
-        napi_throw_error(env, NULL, "a renderAsync is already in flight on this handle");
-        return NULL;
+    float *out = NULL;
+    if (get_out(env, argc, argv, 1, (size_t)H->band_h * H->width * 4u, &out)) return NULL;
+    return queue_render(env, argv, &H, 1, 0, argc >= 2 ? argv[1] : NULL, out);
+}
+
+/* The band handles of an array argument (idle, distinct, at most MAX_BANDS). */
+static int band_handles(napi_env env, napi_value arr, napi_value *hv, Handle **H, uint32_t *n, size_t *rows,
+                        uint32_t *width) {
+    bool is_array = false;
+    if (napi_is_array(env, arr, &is_array) != napi_ok || !is_array || napi_get_array_length(env, arr, n) != napi_ok ||
+        *n < 1 || *n > MAX_BANDS) {
+        napi_throw_type_error(env, NULL, "expected an array of 1..64 band handles");
+        return -1;
     }
-    RenderJob *J = (RenderJob *)calloc(1, sizeof(RenderJob));
-    if (!J) {
-        napi_throw_error(env, NULL, "out of memory");
-        return NULL;
-    }
-    J->H = H;
-    if (argc >= 2) {
-        napi_valuetype vt;
-        napi_typeof(env, argv[1], &vt);
-        if (vt != napi_undefined && vt != napi_null) {
-            void *p;
-            size_t n, es;
-            napi_typedarray_type t;
-            if (typed_view(env, argv[1], &p, &n, &es, &t) || t != napi_float32_array) {
-                free(J);
-                napi_throw_type_error(env, NULL, "renderAsync(h, out): out must be a Float32Array");
-                return NULL;
+    *rows = 0;
+    for (uint32_t i = 0; i < *n; ++i) {
+        if (napi_get_element(env, arr, i, &hv[i]) != napi_ok || !(H[i] = get_handle(env, hv[i]))) return -1;
+        for (uint32_t k = 0; k < i; ++k)
+            if (H[k] == H[i]) {
+                napi_throw_error(env, NULL, "a band handle appears twice");
+                return -1;
             }
-            J->out = (float *)p;
-            napi_create_reference(env, argv[1], 1, &J->out_ref);
-        }
+        *rows += H[i]->band_h;
+        *width = H[i]->width;
     }
-    napi_value promise, name;
-    CHECK_NAPI(env, napi_create_promise(env, &J->deferred, &promise));
-    CHECK_NAPI(env, napi_create_string_utf8(env, "ptx_render", NAPI_AUTO_LENGTH, &name));
-    CHECK_NAPI(env, napi_create_async_work(env, NULL, name, render_execute, render_complete, J, &J->work));
-    H->busy = 1;
-    CHECK_NAPI(env, napi_queue_async_work(env, J->work));
-    return promise;
+    return 0;
+}
+
+/* renderBands([h...] [, Float32Array out]) -- one frame over the band handles of this process
+ * (ptx_render_bands: halo over their communicators or peer copies); blocking */
+static napi_value js_render_bands(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], hv[MAX_BANDS];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H[MAX_BANDS];
+    uint32_t n = 0, width = 0;
+    size_t rows = 0;
+    if (argc < 1 || band_handles(env, argv[0], hv, H, &n, &rows, &width)) return NULL;
+    float *out = NULL;
+    if (get_out(env, argc, argv, 1, rows * width * 4u, &out)) return NULL;
+    ptx_handle *hs[MAX_BANDS];
+    for (uint32_t i = 0; i < n; ++i) hs[i] = H[i]->h;
+    int rc = ptx_render_bands(hs, (int)n, out);
+    if (rc != PTX_OK) {
+        for (uint32_t i = 0; i < n; ++i)
+            if (*ptx_last_error(H[i]->h)) return throw_ptx(env, H[i], rc, "ptx_render_bands");
+        return throw_ptx(env, H[0], rc, "ptx_render_bands");
+    }
+    return NULL;
+}
+
+/* renderBandsAsync([h...] [, Float32Array out]) -> Promise */
+static napi_value js_render_bands_async(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], hv[MAX_BANDS];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H[MAX_BANDS];
+    uint32_t n = 0, width = 0;
+    size_t rows = 0;
+    if (argc < 1 || band_handles(env, argv[0], hv, H, &n, &rows, &width)) return NULL;
+    float *out = NULL;
+    if (get_out(env, argc, argv, 1, rows * width * 4u, &out)) return NULL;
+    return queue_render(env, hv, H, (int)n, 1, argc >= 2 ? argv[1] : NULL, out);
+}
+
+/* commUniqueId() -> Uint8Array(128): ncclGetUniqueId, to ship to the other ranks */
+static napi_value js_comm_unique_id(napi_env env, napi_callback_info info) {
+    (void)info;
+    napi_value ab, arr;
+    void *p = NULL;
+    CHECK_NAPI(env, napi_create_arraybuffer(env, PTX_COMM_ID_BYTES, &p, &ab));
+    int rc = ptx_comm_unique_id(p, PTX_COMM_ID_BYTES);
+    if (rc != PTX_OK) return throw_ptx(env, NULL, rc, "ptx_comm_unique_id (is RCCL installed?)");
+    CHECK_NAPI(env, napi_create_typedarray(env, napi_uint8_array, PTX_COMM_ID_BYTES, ab, 0, &arr));
+    return arr;
+}
+
+/* commInit(h, Uint8Array(128) id, rank, world): the handle's own RCCL communicator */
+static napi_value js_comm_init(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    void *p;
+    size_t n, es;
+    int32_t rank = -1, world = 0;
+    if (argc < 4 || typed_view(env, argv[1], &p, &n, &es, NULL) || n * es != PTX_COMM_ID_BYTES ||
+        napi_get_value_int32(env, argv[2], &rank) != napi_ok || napi_get_value_int32(env, argv[3], &world) != napi_ok) {
+        napi_throw_type_error(env, NULL, "commInit(h, id: Uint8Array(128), rank, world)");
+        return NULL;
+    }
+    int rc = ptx_comm_init(H->h, p, PTX_COMM_ID_BYTES, rank, world);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_comm_init");
+    return NULL;
+}
+
+/* commInitAll([h...]): ncclCommInitAll over the band handles of this process (one per GPU) */
+static napi_value js_comm_init_all(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], hv[MAX_BANDS];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H[MAX_BANDS];
+    uint32_t n = 0, width = 0;
+    size_t rows = 0;
+    if (argc < 1 || band_handles(env, argv[0], hv, H, &n, &rows, &width)) return NULL;
+    ptx_handle *hs[MAX_BANDS];
+    for (uint32_t i = 0; i < n; ++i) hs[i] = H[i]->h;
+    int rc = ptx_comm_init_all(hs, (int)n);
+    if (rc != PTX_OK) return throw_ptx(env, H[0], rc, "ptx_comm_init_all");
+    return NULL;
+}
+
+/* rowCensus(h, BigUint64Array(tileRows * 5)) -- PTX_FLAG_ROW_CENSUS handles */
+static napi_value js_row_census(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    void *p;
+    size_t n, es;
+    napi_typedarray_type t;
+    if (argc < 2 || typed_view(env, argv[1], &p, &n, &es, &t) || t != napi_biguint64_array || n % 5) {
+        napi_throw_type_error(env, NULL, "rowCensus(h, out: BigUint64Array(tileRows * 5))");
+        return NULL;
+    }
+    int rc = ptx_row_census(H->h, (uint64_t *)p, n / 5);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_row_census");
+    return NULL;
 }
 
 static napi_value simple_call(napi_env env, napi_callback_info info, int (*fn)(ptx_handle *), const char *what) {
@@ -487,6 +645,9 @@ static napi_value init(napi_env env, napi_value exports) {
         {"resetStats", js_reset_stats},     {"readBuffer", js_read_buffer},
         {"writeBuffer", js_write_buffer},   {"trace", js_trace},
         {"destroy", js_destroy},            {"lastError", js_last_error},
+        {"renderBands", js_render_bands},   {"renderBandsAsync", js_render_bands_async},
+        {"commUniqueId", js_comm_unique_id}, {"commInit", js_comm_init},
+        {"commInitAll", js_comm_init_all},  {"rowCensus", js_row_census},
     };
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
         napi_value f;

@@ -23,7 +23,8 @@ class Renderer:
     def __init__(self, width: int, height: int, device: int = -1, pipeline: str = "restir",
                  row_begin: int = 0, row_end: int = 0, count_work: bool = False, variant: str = "wave",
                  time_launches: bool = False, single_stream: bool = False, reuse_radius: int = 0,
-                 reuse_neighbors: int = 0, temporal_cap: int = 0):
+                 reuse_neighbors: int = 0, temporal_cap: int = 0, row_census: bool = False,
+                 halo_overlap: bool = False):
         self._lib = N.load()
         self.width, self.height = int(width), int(height)
         self.pipeline = pipeline
@@ -33,7 +34,9 @@ class Renderer:
                           reuse_neighbors=reuse_neighbors, temporal_cap=temporal_cap,
                           flags=(N.PTX_FLAG_COUNT_WORK if count_work else 0) | N.VARIANT_FLAGS[variant]
                           | (N.PTX_FLAG_TIME_LAUNCHES if time_launches else 0)
-                          | (N.PTX_FLAG_SINGLE_STREAM if single_stream else 0))
+                          | (N.PTX_FLAG_SINGLE_STREAM if single_stream else 0)
+                          | (N.PTX_FLAG_ROW_CENSUS if row_census else 0)
+                          | (N.PTX_FLAG_HALO_OVERLAP if halo_overlap else 0))
         self._h = ctypes.c_void_p()
         rc = self._lib.ptx_create(ctypes.byref(cfg), ctypes.byref(self._h))
         if rc != N.PTX_OK:
@@ -100,6 +103,53 @@ class Renderer:
 
     def halo_unpack(self, dev_top: int | None, dev_bottom: int | None) -> None:
         self._call("ptx_halo_unpack", self._h, dev_top, dev_bottom)
+
+    # ------------------------------------------------------------------ multi-GPU (include/ptx.h)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """ncclGetUniqueId: made on one rank, shipped to the others by the caller."""
+        lib = N.load()
+        buf = ctypes.create_string_buffer(N.PTX_COMM_ID_BYTES)
+        rc = lib.ptx_comm_unique_id(buf, N.PTX_COMM_ID_BYTES)
+        if rc != N.PTX_OK:
+            raise N.PtxError(f"ptx_comm_unique_id failed ({rc}): is RCCL installed?")
+        return buf.raw
+
+    def comm_init(self, unique_id: bytes, rank: int, world: int) -> None:
+        """The handle's own RCCL communicator: Render() then exchanges the halo itself."""
+        buf = ctypes.create_string_buffer(bytes(unique_id), N.PTX_COMM_ID_BYTES)
+        self._call("ptx_comm_init", self._h, buf, N.PTX_COMM_ID_BYTES, rank, world)
+
+    @staticmethod
+    def comm_init_all(renderers) -> None:
+        """ncclCommInitAll over the band renderers of this process (one per GPU)."""
+        arr = (ctypes.c_void_p * len(renderers))(*[r._h.value for r in renderers])
+        lib = N.load()
+        N.check(lib, renderers[0]._h, lib.ptx_comm_init_all(arr, len(renderers)), "ptx_comm_init_all")
+
+    @staticmethod
+    def render_bands(renderers, out: np.ndarray | None = None) -> None:
+        """One frame over the band renderers of this process, halo exchanged on the device
+        (their communicators, or peer copies); `out` (rows of all bands, W, 4) f32 optional."""
+        arr = (ctypes.c_void_p * len(renderers))(*[r._h.value for r in renderers])
+        lib = N.load()
+        ptr = None
+        if out is not None:
+            rows = sum(r.band_rows for r in renderers)
+            assert out.dtype == np.float32 and out.flags.c_contiguous and out.size == rows * renderers[0].width * 4
+            ptr = out.ctypes.data
+        rc = lib.ptx_render_bands(arr, len(renderers), ptr)
+        if rc != N.PTX_OK:
+            msgs = [lib.ptx_last_error(r._h) for r in renderers]
+            raise N.PtxError(f"ptx_render_bands failed ({rc}): "
+                             + "; ".join(m.decode(errors="replace") for m in msgs if m))
+
+    def row_census(self) -> np.ndarray:
+        """(tile rows, 5) u64 {rays, instance transforms, AABB tests, triangle tests, hits}
+        per 8-row tile row of the band (handle made with row_census=True)."""
+        out = np.zeros(((self.band_rows + 7) // 8, 5), dtype=np.uint64)
+        self._call("ptx_row_census", self._h, out.ctypes.data, out.shape[0])
+        return out
 
     @property
     def reservoir_words(self) -> int:

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), f"libptx.so does not export {name}"
     assert sorted(_native.EXPORTED) == declared
-    assert lib.ptx_abi_version() == _native.PTX_ABI_VERSION == 3
+    assert lib.ptx_abi_version() == _native.PTX_ABI_VERSION == 4
 
 
 def test_create_rejects_bad_config_without_touching_gpu():

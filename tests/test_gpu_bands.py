@@ -1,0 +1,151 @@
+"""Multi-band frames on the GPU (SURVEY.md §8e, configs[3]): the frame split into row bands,
+each band a handle with halo rows, the spatial-reuse halo exchanged on the device
+(ptx_render_bands: peer copies between the handles of one process, or their RCCL
+communicators).  The bar: the bands reproduce the single-handle frame BIT FOR BIT, and the
+single handle is itself pinned to the oracle (test_gpu_reuse.py); small splits are checked
+against the oracle directly.  Plus the work census the cost-balanced split is cut from.
+"""
+import numpy as np
+import pytest
+
+from helpers import uniform_for
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def native():
+    from pathtracerdemo_amd import _native
+    return _native
+
+
+def make(cs, W, H, pipeline="reuse", radius=30, **kw):
+    from pathtracerdemo_amd.renderer import Renderer
+    r = Renderer(W, H, device=0, pipeline=pipeline, reuse_radius=radius, **kw)
+    r.Initialize(cs)
+    return r
+
+
+def assert_same(got, want, what):
+    got, want = np.asarray(got), np.asarray(want)
+    if got.dtype != np.uint32:
+        got, want = got.view(np.uint32), want.view(np.uint32)
+    bad = np.any(got != want, axis=-1)
+    assert bad.sum() == 0, f"{what}: {bad.sum()} pixels differ, first at {np.argwhere(bad)[:4].tolist()}"
+
+
+def render_split(cs, W, H, cuts, frames, pipeline="reuse", radius=30, overlap=False):
+    from pathtracerdemo_amd.renderer import Renderer
+    bounds = [0] + list(cuts) + [H]
+    bands = [make(cs, W, H, pipeline, radius, row_begin=bounds[i], row_end=bounds[i + 1], halo_overlap=overlap)
+             for i in range(len(bounds) - 1)]
+    img = np.zeros((H, W, 4), np.float32)
+    for _ in range(frames):
+        for b in bands:
+            b.Update()
+        Renderer.render_bands(bands, img)
+    hist = np.concatenate([b.read_history() for b in bands])
+    for b in bands:
+        b.close()
+    return hist, img
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_bands_small_split_matches_oracle(scene1, oracle_mod, overlap):
+    """Three unequal bands (peer-copied halos, radius 12) reproduce the whole-frame oracle."""
+    O, W, H, R = oracle_mod, 72, 80, 12
+    fr = O.Frame(uniform_for(scene1, W, H, 1), scene1.scene, scene1.geometry, scene1.accel)
+    fr.reuse = (R, 3, 20)
+    for f in (1, 2, 3):
+        fr.set_frame_index(f)
+        fr.run_reuse_frame(threads=8)
+    hist, img = render_split(scene1, W, H, [17, 50], 3, radius=R, overlap=overlap)
+    assert_same(hist, fr.res_hist, "spatial output")
+    assert_same(img, fr.accum, "radiance")
+
+
+@pytest.mark.parametrize("cuts,overlap", [
+    ([270 * i for i in range(1, 8)], False),                      # 8 equal bands of 270 rows
+    ([270 * i for i in range(1, 8)], True),                       # the same, interior rows overlapped
+    ([301, 563, 820, 1081, 1339, 1600, 1861], True),              # cost-balanced style, ragged
+])
+def test_c4_4k_eight_bands_bit_identical_to_one_handle(scene3, cuts, overlap):
+    """configs[3]: the C3 reuse frame at 3840x2160 as 8 band handles (halo carried through
+    device buffers) equals one 4K handle bit for bit, 3 frames (history included)."""
+    W, H = 3840, 2160
+    one = make(scene3, W, H)
+    for _ in range(3):
+        one.Update()
+        one.Render()
+    want_hist, want_img = one.read_history(), one.read_image()
+    one.close()
+    hist, img = render_split(scene3, W, H, cuts, 3, overlap=overlap)
+    assert_same(hist, want_hist, "spatial output")
+    assert_same(img, want_img, "radiance")
+    assert np.isfinite(img).all()
+
+
+def test_gi_bands_bit_identical(scene3):
+    """ReSTIR GI as 3 bands with peer-copied halos equals the single handle."""
+    W, H = 256, 160
+    one = make(scene3, W, H, "gi")
+    for _ in range(2):
+        one.Update()
+        one.Render()
+    hist, img = render_split(scene3, W, H, [40, 100], 2, pipeline="gi", overlap=True)
+    assert_same(hist, one.read_history(), "GI spatial output")
+    assert_same(img, one.read_image(), "GI radiance")
+
+
+def test_handle_owned_communicator_world_one(scene3):
+    """ptx_comm_init (ncclCommInitRank, world 1): the handle renders through the RCCL band
+    path and matches the plain handle."""
+    from pathtracerdemo_amd.renderer import Renderer
+    W, H = 128, 96
+    a, b = make(scene3, W, H), make(scene3, W, H)
+    b.comm_init(Renderer.comm_unique_id(), 0, 1)
+    for _ in range(2):
+        for r in (a, b):
+            r.Update()
+            r.Render()
+    assert_same(b.read_history(), a.read_history(), "spatial output")
+    assert_same(b.read_image(), a.read_image(), "radiance")
+
+
+def test_render_bands_rejects_gaps(scene3):
+    from pathtracerdemo_amd.renderer import Renderer
+    from pathtracerdemo_amd import _native as N
+    W, H = 64, 120
+    bands = [make(scene3, W, H, row_begin=0, row_end=40), make(scene3, W, H, row_begin=50, row_end=120)]
+    for b in bands:
+        b.Update()
+    with pytest.raises(N.PtxError):
+        Renderer.render_bands(bands)
+
+
+def test_row_census(scene3, oracle_mod, native):
+    """PTX_FLAG_ROW_CENSUS: per tile row, the G-buffer pass's work equals the oracle's for
+    those rows exactly; every pass's census sums to the plain counting build's totals; the
+    census handle renders the same frame."""
+    O, W, H = oracle_mod, 96, 72  # 12 tiles per row: one queue slot per tile row
+    cen = make(scene3, W, H, row_census=True)
+    cnt = make(scene3, W, H, count_work=True)
+    fr = O.Frame(uniform_for(scene3, W, H, 1), scene3.scene, scene3.geometry, scene3.accel)
+    keys = ("rays", "instance_xforms", "aabb_tests", "tri_tests", "hits")
+    for r in (cen, cnt):
+        r.Update()
+        r.reset_stats()
+        r.run_pass(native.PTX_PASS_GBUFFER)
+    g = cen.row_census()
+    for t in range(g.shape[0]):
+        c = fr.run(O.PASS_GBUFFER, 4, (0, 8 * t, W, min(H, 8 * t + 8)))
+        assert [int(v) for v in g[t]] == [c[k] for k in keys], f"tile row {t}"
+    for p in (native.PTX_PASS_INIT, native.PTX_PASS_TEMPORAL, native.PTX_PASS_SPATIAL, native.PTX_PASS_FINAL):
+        for r in (cen, cnt):
+            r.reset_stats()
+            r.run_pass(p)
+        tot = cen.row_census().sum(axis=0)
+        assert [int(v) for v in tot] == [cnt.read_counters()[k] for k in keys], f"pass {p}"
+        if p in (native.PTX_PASS_INIT, native.PTX_PASS_SPATIAL):  # (temporal / final may trace nothing)
+            assert tot[0] > 0
+    assert_same(cen.read_history(), cnt.read_history(), "census handle frame")

@@ -116,6 +116,28 @@ def test_mcpt(scene1, oracle_mod, native, W, H):
     np.testing.assert_array_equal(img.view(np.uint32), fr.accum.view(np.uint32))
 
 
+def test_mcpt_full_hd_window_bit_exact(scene1, oracle_mod):
+    """configs[1] at its own size: TEST_MCPT over the whole 1920x1080 frame on the GPU
+    (Render(), the production launch sequence), FrameIndex 1 and 2 accumulated; the oracle
+    renders 3 row windows (top, middle, bottom) and they must match bit for bit
+    (SH/TEST_MCPT.wgsl:1315-1372 is per pixel)."""
+    W, H = 1920, 1080
+    r = make_renderer(scene1, W, H, pipeline="mcpt")
+    fr = oracle_frame(oracle_mod, scene1, W, H)
+    windows = [(0, 12), (530, 546), (1068, 1080)]
+    for f in (1, 2):
+        r.Update()
+        r.Render()
+        fr.set_frame_index(f)
+        for y0, y1 in windows:
+            fr.run(oracle_mod.PASS_MCPT, 16, (0, y0, W, y1))
+    img = r.read_image()
+    for y0, y1 in windows:
+        np.testing.assert_array_equal(img[y0:y1].view(np.uint32), fr.accum[y0:y1].view(np.uint32))
+        assert rel_l2(img[y0:y1, :, :3], fr.accum[y0:y1, :, :3]) <= 1e-3
+    assert np.isfinite(img).all()
+
+
 @pytest.mark.parametrize("variant", ["tiled", "persistent", "simple"])
 def test_alternate_variants(scene1, oracle_mod, native, variant):
     """The A/B kernel variants obey the same bars as the default wavefront path."""

@@ -223,3 +223,24 @@ def test_full_hd_reuse_window_bit_exact(scene1, oracle_mod):
     assert_same(r.read_image()[y0:y1], fr.accum[y0:y1], "radiance (window)")
     st = r.stats()
     assert st["frames"] == 2 and st["kernel_launches"][7] == 2
+
+
+def test_c3_full_hd_reuse_windows_bit_exact(scene3, oracle_mod):
+    """The headline configuration itself (configs[2]: C3, 32 rect lights, 1920x1080, reuse
+    pipeline, 2 frames with history) on the GPU; the oracle evaluates what 3 row windows
+    (top edge, middle, bottom edge) of frame 2 depend on, and they must match bit for bit."""
+    O, W, H, R = oracle_mod, 1920, 1080, 30
+    windows = [(0, 8), (600, 608), (1072, 1080)]
+    r = reuse_renderer(scene3, W, H)
+    frs = [oracle_frame(O, scene3, W, H) for _ in windows]
+    for f in (1, 2):
+        r.Update()
+        r.Render()
+        for (y0, y1), fr in zip(windows, frs):
+            fr.set_frame_index(f)
+            fr.run_reuse_frame(threads=16, rect=(0, max(0, y0 - 2 * R), W, min(H, y1 + 2 * R)))
+    hist, img = r.read_history(), r.read_image()
+    for (y0, y1), fr in zip(windows, frs):
+        assert_same(hist[y0:y1], fr.res_hist[y0:y1], f"spatial output rows {y0}..{y1}")
+        assert_same(img[y0:y1], fr.accum[y0:y1], f"radiance rows {y0}..{y1}")
+    assert np.isfinite(img).all()
