@@ -308,6 +308,8 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     // measured per pipeline: 4 waves per SIMD (no spill) for the reference
     // pipeline / TEST_MCPT and the reuse pipeline, 5 for ReSTIR GI
     w.trace_waves = h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI ? 5u : 4u;
+    static const uint32_t env_split = getenv("PTX_TRACE_SPLIT") ? (uint32_t)atoi(getenv("PTX_TRACE_SPLIT")) : 0u;
+    w.trace_split = env_split >= 1u && env_split <= 16u ? env_split : 1u;
     w.seg_base = 0;
     w.seg_count = w.nseg;
     static const uint32_t cl = getenv("PTX_SEG_CLUSTER") ? (uint32_t)atoi(getenv("PTX_SEG_CLUSTER")) : 1u;  // A/B

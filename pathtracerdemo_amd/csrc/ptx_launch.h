@@ -65,6 +65,8 @@ struct WaveBufs {
     uint32_t act_stride; // list entries per segment (seg_px; seg_px * jobs per pixel for reuse)
     uint32_t *cnt;       // 2 * kWaveMaxRounds * nseg counts
     uint32_t trace_waves;  // trace_queue occupancy target (waves per SIMD; 4 or 5, per pipeline)
+    uint32_t trace_split;  // workgroups per ray segment in trace_queue (batches of 256 rays dealt
+                           // round-robin over them): a segment's rays are not one serial chain
     // Tile set of the launch: virtual tile v (what the segments spread over) is band tile
     // v < ntile0 ? tile0 + v : tile1 + (v - ntile0), for v < ntile0 + ntile1 (8x8 tiles in
     // raster order).  Default: the whole band.  A band's spatial pass runs its interior rows

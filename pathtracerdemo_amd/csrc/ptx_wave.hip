@@ -50,11 +50,20 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     __shared__ Inst l_insts[LDS_TABLES ? kLdsInsts : 1];
     __shared__ unsigned long long c_key[WB];
     const CoopLds coop{c_key + (threadIdx.x & ~63u)};
+    // workgroup -> (segment, share): the trace_split workgroups of a segment take its
+    // 256-ray batches round-robin; results go to the rays' own slots, so the split is exact.
+    // A segment's shares are consecutive blocks, so they spread over XCDs (blocks b and b+8
+    // share one: MI355X_MICROARCH.md, workgroup dispatch) -- measured faster than keeping
+    // them on one XCD.  For K | 8 the share index rotates with b / 8, else share 0 (the
+    // heaviest) would always land on the same XCDs.
+    const uint32_t K = w.trace_split, b = blockIdx.x;
+    const uint32_t share = (b % K + ((8u % K) == 0u ? (b >> 3) : 0u)) % K, local = b / K;
+    const uint32_t j = w.seg_phys + w.seg_base + local;  // physical queue slot
+    const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
+    if (share * WB >= n) return;  // (workgroup-uniform) nothing for this share
     if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
     const SubRoot *subs = LDS_TABLES ? l_subs : sc.subs;
     const Inst *insts = LDS_TABLES ? l_insts : sc.insts;
-    const uint32_t j = w.seg_phys + w.seg_base + blockIdx.x;  // physical queue slot
-    const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
     if (COUNT && sc.census)  // row census: this slot's queries count into its own block
         sc.counters = sc.census + (size_t)kCensusWords * ((sc.row_end - sc.row_begin + 7u) / 8u + j);
     const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
@@ -62,7 +71,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     // Every lane of the wave calls the traversal every time -- lanes without a query (past
     // the segment's end, or whose Visibility walk is over) with a NaN bound, which no box
     // overlaps -- so the whole wave takes part in the cooperative leaf phases.
-    for (uint32_t i0 = 0; i0 < n; i0 += WB) {  // workgroup-uniform
+    for (uint32_t i0 = share * WB; i0 < n; i0 += K * WB) {  // workgroup-uniform
         const uint32_t i = i0 + threadIdx.x;
         bool active = i < n;
         float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
@@ -914,16 +923,19 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
 }
 
 // =========================================================================== host side
+// trace_queue's grid: trace_split workgroups per segment
+static inline uint32_t trace_grid(const WaveBufs &w) { return w.seg_count * w.trace_split; }
+
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t depth, hipStream_t s,
                       bool occ_only) {
     const PassEps eps = eps_mode == 0 ? PassEps{1e-8f, 1e-6f} : PassEps{1e-4f, 1e-8f};
     const size_t lds = stack_lds_bytes(depth);
     if (occ_only && sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts) {  // occlusion rounds (GI spatial)
         if (sc.counters)
-            hipLaunchKernelGGL((trace_queue<true, 6, false, true, true>), dim3(w.seg_count), dim3(WB), lds, s, sc, w,
+            hipLaunchKernelGGL((trace_queue<true, 6, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
                                (uint32_t)round, eps);
         else
-            hipLaunchKernelGGL((trace_queue<false, 5, false, true, true>), dim3(w.seg_count), dim3(WB), lds, s, sc, w,
+            hipLaunchKernelGGL((trace_queue<false, 5, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
                                (uint32_t)round, eps);
         return hipGetLastError();
     }
@@ -941,10 +953,10 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
                                w.rays + 2u * (size_t)pb * w.ray_stride, res, cnt,
                                w.ray_stride, 0u, eps);
     } else if (sc.counters && getenv("PTX_TRACE_PROF"))  // SIMD-utilisation diagnostics
-        hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round,
+        hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round,
                            eps);
     else if (sc.counters)
-        hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+        hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     else {
         // Occupancy target per pipeline (WaveBufs::trace_waves), LDS-staged tables; A/B
         // switches PTX_TRACE_OCC / PTX_TRACE_NOLDS.  Measured at 1080p with 768-pixel segments:
@@ -957,7 +969,7 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
                  : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
                  : occ == 6  ? trace_queue<false, 6> : occ == 5 ? trace_queue<false, 5> : trace_queue<false, 4>;
-        hipLaunchKernelGGL(k, dim3(w.seg_count), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
+        hipLaunchKernelGGL(k, dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     }
     return hipGetLastError();
 }
