@@ -41,20 +41,28 @@ class Inputs(ctypes.Structure):
                 ("geometry", ctypes.c_void_p), ("accel", ctypes.c_void_p)]
 
 
-def build(force: bool = False) -> str:
+# build variants: "" = the parity oracle; "libm" / "wgsl" = the transcendental-sensitivity
+# builds (PTO_TRANSC=1 / 2 in pt_oracle.c), "asan" = the sanitizer build
+VARIANTS = {"": "liboracle.so", "libm": "liboracle_libm.so", "wgsl": "liboracle_wgsl.so",
+            "wgsl_pow": "liboracle_wgsl_pow.so", "wgsl_sincos": "liboracle_wgsl_sincos.so",
+            "asan": "liboracle_asan.so"}
+
+
+def build(force: bool = False, variant: str = "") -> str:
+    path = os.path.join(HERE, VARIANTS[variant])
     srcs = [os.path.join(HERE, f) for f in ("pt_oracle.c", "pt_oracle_gi.c", "pt_oracle.h")]
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, srcs)):
-        subprocess.run(["make", "-C", HERE, "liboracle.so"], check=True, capture_output=True)
-    return LIB_PATH
+    if force or not os.path.exists(path) or os.path.getmtime(path) < max(map(os.path.getmtime, srcs)):
+        subprocess.run(["make", "-C", HERE, VARIANTS[variant]], check=True, capture_output=True)
+    return path
 
 
-_lib = None
+_libs: dict = {}
 
 
-def lib():
-    global _lib
+def lib(variant: str = ""):
+    _lib = _libs.get(variant)
     if _lib is None:
-        _lib = ctypes.CDLL(build())
+        _lib = _libs[variant] = ctypes.CDLL(build(variant=variant))
         P = ctypes.c_void_p
         _lib.pto_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Inputs), ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, P, P, P, ctypes.POINTER(Counters)]
@@ -96,7 +104,9 @@ def _ptr(a: np.ndarray):
 class Frame:
     """Full-frame oracle buffers for one W x H uniform block."""
 
-    def __init__(self, uniform: np.ndarray, scene: np.ndarray, geometry: np.ndarray, accel: np.ndarray):
+    def __init__(self, uniform: np.ndarray, scene: np.ndarray, geometry: np.ndarray, accel: np.ndarray,
+                 variant: str = ""):
+        self.variant = variant  # oracle build (VARIANTS); "" = the parity oracle
         self.uniform = np.ascontiguousarray(uniform, dtype=np.uint32)
         self.scene = np.ascontiguousarray(scene, dtype=np.uint32)
         self.geometry = np.ascontiguousarray(geometry, dtype=np.uint32)
@@ -124,7 +134,7 @@ class Frame:
         inp = Inputs(self.uniform.ctypes.data, self.scene.ctypes.data, self.geometry.ctypes.data,
                      self.accel.ctypes.data)
         cnt = Counters()
-        lib().pto_trace(ctypes.byref(inp), _ptr(rays), _ptr(hits), len(rays), eps_mode, ctypes.byref(cnt))
+        lib(self.variant).pto_trace(ctypes.byref(inp), _ptr(rays), _ptr(hits), len(rays), eps_mode, ctypes.byref(cnt))
         self.counters["trace"] = cnt.as_dict()
         return (hits, self.counters["trace"]) if return_counters else hits
 
@@ -140,7 +150,7 @@ class Frame:
         if pass_id in (PASS_TEMPORAL, PASS_SPATIAL):
             r, m, cap = self.reuse
             prm = ReuseParams(r, m, cap, 1 if self.hist_valid else 0)
-            rc = lib().pto_run_reuse(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
+            rc = lib(self.variant).pto_run_reuse(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
                                      _ptr(self.reservoir), _ptr(self.res_hist), ctypes.byref(prm),
                                      ctypes.byref(cnt))
             if rc != 0:
@@ -149,7 +159,7 @@ class Frame:
             return self.counters[pass_id]
         res = self.reservoir if reservoir is None else np.ascontiguousarray(reservoir)
         assert res.dtype == np.uint32 and res.shape == self.reservoir.shape
-        rc = lib().pto_run(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
+        rc = lib(self.variant).pto_run(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
                            _ptr(res), _ptr(self.accum), ctypes.byref(cnt))
         if rc != 0:
             raise RuntimeError(f"oracle pass {pass_id} failed ({rc})")
@@ -196,7 +206,7 @@ class Frame:
         prm = ReuseParams(r, m, cap, 1 if self.hist_valid else 0)
         cnt = Counters()
         inp = self._inputs()
-        rc = lib().pto_run_gi(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
+        rc = lib(self.variant).pto_run_gi(pass_id, threads, ctypes.byref(inp), x0, y0, x1, y1, _ptr(self.gbuffer),
                               _ptr(self.gi_res), _ptr(self.gi_hist), _ptr(self.direct), _ptr(self.accum),
                               ctypes.byref(prm), ctypes.byref(cnt))
         if rc != 0:
@@ -217,7 +227,7 @@ class Frame:
         s = np.ascontiguousarray(s, dtype=np.uint32)
         out = np.zeros(5, dtype=np.float32)
         inp = self._inputs()
-        lib().pto_gi_shift(ctypes.byref(inp), _ptr(self.gbuffer), x, y, _ptr(s), _ptr(out))
+        lib(self.variant).pto_gi_shift(ctypes.byref(inp), _ptr(self.gbuffer), x, y, _ptr(s), _ptr(out))
         return bool(out[0]), out[1:4].copy(), float(out[4])
 
 

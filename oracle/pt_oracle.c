@@ -391,14 +391,47 @@ static float geom_shadow(float NdotV, float NdotL, float R) {
  * WebGPU backends; sin/cos carry an absolute error bound of 2^-11).  Both sides of the
  * parity check use the same fixed f32 definitions below instead of libm, so the oracle
  * and the HIP path agree bit for bit (each is within ~2 ulp of the true function).
- * pow(x, 5): two squarings and a product. */
+ * pow(x, 5): two squarings and a product.
+ *
+ * PTO_TRANSC selects other admissible WGSL implementations, for the sensitivity study of
+ * DESIGN.md §2 only (tests/test_transcendental_sensitivity.py; never the parity oracle):
+ *   0  the fixed definitions below (default; what the HIP kernels compute)
+ *   1  libm powf / sinf / cosf (correctly rounded or within 1 ulp)
+ *   2  a WGSL-admissible backend at its error bounds: pow as exp2(5 * log2 x) (the common
+ *      lowering) and sin / cos each off by 2^-11 absolute, the sign hashed from the input
+ *   3  mode 2's pow with libm sin / cos;  4  mode 2's sin / cos with libm pow */
+#ifndef PTO_TRANSC
+#define PTO_TRANSC 0
+#endif
+#if PTO_TRANSC == 0
 static inline float pow5_(float x) {
     float x2 = x * x;
     return (x2 * x2) * x;
 }
+#elif PTO_TRANSC == 1 || PTO_TRANSC == 4
+static inline float pow5_(float x) { return powf(x, 5.0f); }
+#else
+static inline float pow5_(float x) { return exp2f(5.0f * log2f(x)); }
+#endif
 /* sin and cos of x >= 0 (the only use: BSDF sampling angles 2*PI_F*u, u in [0,1]).
  * Cody-Waite reduction by pi/4 in three parts (the first exact for the octant counts
  * used), then the classic single-precision minimax polynomials on [-pi/4, pi/4]. */
+#if PTO_TRANSC == 1 || PTO_TRANSC == 3
+static void sincos_(float x, float *s, float *c) {
+    *s = sinf(x);
+    *c = cosf(x);
+}
+#elif PTO_TRANSC == 2 || PTO_TRANSC == 4
+static float sincos_err = 0x1p-11f;  /* WGSL's bound; pto_set_sincos_error() scans smaller ones */
+void pto_set_sincos_error(float e) { sincos_err = e; }
+static void sincos_(float x, float *s, float *c) {
+    uint32_t b;
+    memcpy(&b, &x, 4);
+    const uint32_t h = pto_pcg(b ^ 0x5EEDu);
+    *s = sinf(x) + ((h & 1u) ? sincos_err : -sincos_err);
+    *c = cosf(x) + ((h & 2u) ? sincos_err : -sincos_err);
+}
+#else
 static void sincos_(float x, float *s, float *c) {
     int j = (int)(x * 1.27323954473516f);
     float y = (float)j;
@@ -417,6 +450,7 @@ static void sincos_(float x, float *s, float *c) {
     else if (j == 4) { *s = -ps; *c = -pc; }
     else { *s = -pc; *c = ps; }
 }
+#endif
 float pto_sin(float x) { float s, c; sincos_(x, &s, &c); return s; }
 float pto_cos(float x) { float s, c; sincos_(x, &s, &c); return c; }
 float pto_pow5(float x) { return pow5_(x); }
