@@ -9,14 +9,17 @@
  * the accumulated RGBA f32 image (ReadImage / RenderAsync(out)); presenting it is the
  * caller's (putImageData), the WebGPU present pass being out of scope (SURVEY.md §8b).
  *
- * `world` is the output of SerializeWorldData plus what Update() reads from the World:
- * { scene, geometry, accel: Uint32Array, offsets: number[7], instanceCount, lightCount }
- * (scene_io.loadCompiledScene builds it from a compiled scene directory).
+ * `world` is the reference's own World (./world.js: World.LoadFromScene over the Scene JSON,
+ * meshes in ResourceManager.MeshPool), serialized here by SerializeWorldData exactly as
+ * Renderer_TEST.CreateGPUResources does (Renderer_TEST.ts:445-460) -- or, equivalently, an
+ * already serialized { scene, geometry, accel: Uint32Array, offsets: number[7],
+ * instanceCount, lightCount } (scene_io.loadCompiledScene reads one from disk).
  * There is no CPU fallback: a missing addon or libptx.so throws at require time.
  */
 const path = require('path');
 const { Camera } = require('./Camera');
 const { mat4 } = require('./wgpu_math');
+const { SerializeWorldData } = require('./world');
 
 const addon = require(path.join(__dirname, '..', 'ptx_node.node'));
 
@@ -86,6 +89,11 @@ class NativeRenderer {
     this.Camera.SetLocationFromXYZ(0, 0, 6);
     this.Camera.SetYaw(0);
     this.Camera.SetPitch(0);
+    // a reference World is serialized here (SerializeWorldData); a serialized one is taken as is
+    if (world && world.InstancesPool instanceof Map) world = SerializeWorldData(world);
+    if (!world || !(world.scene instanceof Uint32Array) || !Array.isArray(world.offsets) || world.offsets.length !== 7) {
+      throw new TypeError('Initialize: expected a World or a serialized world {scene, geometry, accel, offsets[7]}');
+    }
     this.World = world;
     this.ResetFrameCount();
     addon.uploadScene(this.Handle, world.scene, world.geometry, world.accel);

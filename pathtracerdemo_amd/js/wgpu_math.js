@@ -50,6 +50,10 @@ const mat4 = {
       (a31 * b01 - a30 * b03 - a32 * b00) * inv, (a20 * b03 - a21 * b01 + a22 * b00) * inv,
     ]);
   },
+  scaling(v) {
+    return out([v[0], 0, 0, 0, 0, v[1], 0, 0, 0, 0, v[2], 0, 0, 0, 0, 1]);
+  },
+  mul(a, b) { return mat4.multiply(a, b); },
   fromQuat(q) {
     const [x, y, z, w] = Array.from(q);
     const x2 = x + x, y2 = y + y, z2 = z + z;
@@ -81,6 +85,22 @@ const mat4 = {
 };
 
 const quat = {
+  identity() {
+    return out([0, 0, 0, 1]);
+  },
+  fromAxisAngle(axis, angleInRadians) {
+    const halfAngle = angleInRadians * 0.5;
+    const s = Math.sin(halfAngle);
+    return out([s * axis[0], s * axis[1], s * axis[2], Math.cos(halfAngle)]);
+  },
+  multiply(a, b) {
+    const [ax, ay, az, aw] = Array.from(a);
+    const [bx, by, bz, bw] = Array.from(b);
+    return out([ax * bw + aw * bx + ay * bz - az * by,
+      ay * bw + aw * by + az * bx - ax * bz,
+      az * bw + aw * bz + ax * by - ay * bx,
+      aw * bw - ax * bx - ay * by - az * bz]);
+  },
   fromEuler(x, y, z, order) {
     if (order !== 'yxz') throw new Error(`quat.fromEuler: order ${order} not supported`);
     const sx = Math.sin(x * 0.5), cx = Math.cos(x * 0.5);
@@ -95,6 +115,31 @@ const vec3 = {
   fromValues(x, y, z) {
     return out([x, y, z]);
   },
+  create(x = 0, y = 0, z = 0) {
+    return out([x, y, z]);
+  },
+  scale(v, k) {
+    return out([v[0] * k, v[1] * k, v[2] * k]);
+  },
+  dot(a, b) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+  },
+  cross(a, b) {
+    return out([a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]]);
+  },
+  len(v) {
+    return Math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  },
+  normalize(v) {
+    const l = Math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    return l > 0.00001 ? out([v[0] / l, v[1] / l, v[2] / l]) : out([0, 0, 0]);
+  },
 };
 
-module.exports = { mat4, quat, vec3 };
+const vec4 = {
+  create(x = 0, y = 0, z = 0, w = 0) {
+    return out([x, y, z, w]);
+  },
+};
+
+module.exports = { mat4, quat, vec3, vec4 };

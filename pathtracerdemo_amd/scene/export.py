@@ -15,7 +15,7 @@ import sys
 
 import numpy as np
 
-from .world import CompiledScene, compile_scene
+from .world import CompiledScene, compile_scene, load_scene_json, mesh_data
 
 OFFSET_ORDER = ["mesh_descriptor", "material", "light", "lights_cdf", "index", "sub_blas_root", "blas"]
 
@@ -29,6 +29,55 @@ def export_compiled(cs: CompiledScene, out_dir: str, name: str = "") -> str:
             "triangleCount": int(cs.triangle_count), "maxBvhDepth": int(cs.max_bvh_depth)}
     with open(os.path.join(out_dir, "world.json"), "w") as f:
         json.dump(meta, f, indent=1)
+    return out_dir
+
+
+def export_meshes(names, out_dir: str, asset_dir: str | None = None) -> str:
+    """The state of each reference `Mesh` after Mesh.Load (Structs.ts:71-141) -- geometry,
+    BVH-reordered indices, BLAS roots, materials -- for the Node host's restatement of
+    Mesh.Serialize / SerializeWorldData (pathtracerdemo_amd/js/world.js,
+    ResourceManager.LoadCompiledAssets).  GLB parsing and the three-mesh-bvh SAH build stay
+    in the Python scene compiler (three / three-mesh-bvh are not installed here).
+
+    <out_dir>/<mesh>/: positions.f32, normals.f32 (V x 3), uvs.f32 (V x 2, absent if the
+    mesh has none), index.u32, blas_<k>.u32 per sub-mesh root, mesh.json (counts + the
+    three.js MeshStandardMaterial fields Material's constructor reads)."""
+    for name in names:
+        md = mesh_data(name, asset_dir)
+        d = os.path.join(out_dir, name)
+        os.makedirs(d, exist_ok=True)
+        np.ascontiguousarray(md.positions, dtype="<f4").tofile(os.path.join(d, "positions.f32"))
+        np.ascontiguousarray(md.normals, dtype="<f4").tofile(os.path.join(d, "normals.f32"))
+        if md.uvs is not None:
+            np.ascontiguousarray(md.uvs, dtype="<f4").tofile(os.path.join(d, "uvs.f32"))
+        elif os.path.exists(os.path.join(d, "uvs.f32")):
+            os.remove(os.path.join(d, "uvs.f32"))
+        np.ascontiguousarray(md.indices, dtype="<u4").tofile(os.path.join(d, "index.u32"))
+        for k, r in enumerate(md.roots):
+            np.ascontiguousarray(r, dtype="<u4").tofile(os.path.join(d, f"blas_{k}.u32"))
+        mats = [{"color": {"r": float(m.color[0]), "g": float(m.color[1]), "b": float(m.color[2])},
+                 "emissive": {"r": float(m.emissive[0]), "g": float(m.emissive[1]), "b": float(m.emissive[2])},
+                 "emissiveIntensity": float(m.emissive_intensity), "metalness": float(m.metalness),
+                 "roughness": float(m.roughness), "transparent": bool(m.transparent)} for m in md.materials]
+        meta = {"name": name, "vertexCount": int(md.positions.shape[0]), "indexCount": int(len(md.indices)),
+                "rootCount": len(md.roots), "maxBvhDepth": int(md.max_depth), "materials": mats}
+        with open(os.path.join(d, "mesh.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+    return out_dir
+
+
+def export_scene_assets(scene_name: str, out_dir: str) -> str:
+    """The reference Scene JSON (Structs.ts:488-556) plus every mesh it names, for
+    World.LoadFromScene + SerializeWorldData on the Node host."""
+    scene = load_scene_json(scene_name)
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, "scene.json"), "w") as f:
+        json.dump(scene, f, indent=1)
+    names = []
+    for a in scene["assets"]:
+        if a.get("type") == "object" and a.get("meshName") and a["meshName"] not in names:
+            names.append(a["meshName"])
+    export_meshes(names, os.path.join(out_dir, "meshes"))
     return out_dir
 
 

@@ -102,15 +102,32 @@ class SerializedMesh:
     max_depth: int
 
 
+@dataclass
+class MeshData:
+    """What the reference's Mesh constructor keeps (Structs.ts:58-106): the merged geometry
+    after three-mesh-bvh reordered its index buffer, one BLAS root (node array) per group /
+    sub-mesh, and the materials.  `Mesh.Serialize` (Structs.ts:143-215) flattens it; the
+    Node host restates that step from an export of this state (export.export_meshes)."""
+    positions: np.ndarray        # (V, 3) f32
+    normals: np.ndarray          # (V, 3) f32
+    uvs: np.ndarray | None       # (V, 2) f32, or None when a primitive has no UVs
+    indices: np.ndarray          # (3T,) u32, BVH-reordered
+    roots: list                  # per sub-mesh: u32 node array (8 words per node)
+    materials: list              # GltfMaterial per sub-mesh
+    max_depth: int
+
+
 _MESH_CACHE: dict = {}
+_DATA_CACHE: dict = {}
 
 
-def load_mesh(name: str, asset_dir: str | None = None) -> SerializedMesh:
-    """Mesh.Load + constructor + Serialize (Structs.ts:71-215)."""
+def mesh_data(name: str, asset_dir: str | None = None) -> MeshData:
+    """Mesh.Load + constructor (Structs.ts:71-141): GLB primitives merged with one group
+    per primitive (mergeGeometries(geoms, true)), SAH BLAS per group."""
     path = os.path.join(asset_dir or ASSET_DIR, name + ".glb")
     key = (os.path.abspath(path), os.path.getmtime(path))
-    if key in _MESH_CACHE:
-        return _MESH_CACHE[key]
+    if key in _DATA_CACHE:
+        return _DATA_CACHE[key]
     prims = Glb(path).primitives()
     has_uv = all(p.uvs is not None for p in prims)
     pos, nrm, uvs, idx, groups, mats = [], [], [], [], [], []
@@ -125,20 +142,35 @@ def load_mesh(name: str, asset_dir: str | None = None) -> SerializedMesh:
         groups.append((ibase // 3, len(p.indices) // 3))
         vbase += p.positions.shape[0]
         ibase += len(p.indices)
-        mats.append(serialize_material(p.material))
+        mats.append(p.material)
     positions = np.concatenate(pos).astype(np.float32)
     normals = np.concatenate(nrm).astype(np.float32)
     indices = np.concatenate(idx).astype(np.uint32)
     roots, indices, max_depth = build_blas(positions, indices, groups)
-    blas, root_offsets = merge_arrays(roots)
-    vert = np.zeros((positions.shape[0], STRIDE_VERTEX), dtype=np.float32)
-    vert[:, 0:3] = positions
-    vert[:, 3:6] = normals
-    if has_uv:
-        vert[:, 6:8] = np.concatenate(uvs)
+    md = MeshData(positions=positions, normals=normals,
+                  uvs=np.concatenate(uvs).astype(np.float32) if has_uv else None, indices=indices,
+                  roots=[np.asarray(r, dtype=np.uint32) for r in roots], materials=mats, max_depth=max_depth)
+    _DATA_CACHE[key] = md
+    return md
+
+
+def load_mesh(name: str, asset_dir: str | None = None) -> SerializedMesh:
+    """Mesh.Load + constructor + Serialize (Structs.ts:71-215)."""
+    path = os.path.join(asset_dir or ASSET_DIR, name + ".glb")
+    key = (os.path.abspath(path), os.path.getmtime(path))
+    if key in _MESH_CACHE:
+        return _MESH_CACHE[key]
+    md = mesh_data(name, asset_dir)
+    blas, root_offsets = merge_arrays(md.roots)
+    vert = np.zeros((md.positions.shape[0], STRIDE_VERTEX), dtype=np.float32)
+    vert[:, 0:3] = md.positions
+    vert[:, 3:6] = md.normals
+    if md.uvs is not None:
+        vert[:, 6:8] = md.uvs
     sm = SerializedMesh(blas=blas, sub_blas_roots=root_offsets,
-                        vertices=vert.reshape(-1).view(np.uint32), indices=indices,
-                        materials=merge_arrays(mats)[0], max_depth=max_depth)
+                        vertices=vert.reshape(-1).view(np.uint32), indices=md.indices,
+                        materials=merge_arrays([serialize_material(m) for m in md.materials])[0],
+                        max_depth=md.max_depth)
     _MESH_CACHE[key] = sm
     return sm
 
@@ -174,8 +206,11 @@ class Light:
         return Light(position, direction, color, u, v, LIGHT_RECT, intensity, area)
 
     def luminance(self) -> float:
+        """GetLuminance (Structs.ts:385-389): vec3.scale and vec3.fromValues store f32, so
+        both the scaled colour and the Rec. 709 weights are f32; vec3.dot sums in f64."""
         c = (self.color.astype(np.float64) * self.intensity).astype(np.float32).astype(np.float64)
-        return float(c[0] * 0.2126 + c[1] * 0.7152 + c[2] * 0.0722)
+        w = np.array([0.2126, 0.7152, 0.0722], dtype=np.float32).astype(np.float64)
+        return float(c[0] * w[0] + c[1] * w[1] + c[2] * w[2])
 
     def serialize(self) -> np.ndarray:
         f = np.zeros(STRIDE_LIGHT, dtype=np.float32)
@@ -194,7 +229,7 @@ class Light:
 def euler_degrees_to_quat(e) -> np.ndarray:
     """World.ts:14-33: q = qz · (qy · qx)."""
     d2r = math.pi / 180.0
-    x, y, z = (float(np.float32(c)) * d2r for c in e)
+    x, y, z = (float(c) * d2r for c in e)  # the Scene JSON's numbers, not f32-rounded
     qx = wm.quat_from_axis_angle((1, 0, 0), x)
     qy = wm.quat_from_axis_angle((0, 1, 0), y)
     qz = wm.quat_from_axis_angle((0, 0, 1), z)
@@ -326,6 +361,23 @@ def load_scene_json(name: str) -> dict:
         return json.load(fh)
 
 
+def scene_from_backend(record) -> dict:
+    """A Scene from the backend's record: SceneResponse carries `assets` as a JSON string
+    (apps/backend/.../dto/SceneResponse.java:24-25, stored as jsonb by entity/Scene.java:39-41);
+    the frontend's Scene type (GC/Structs.ts:541-556) wants the array.  Accepts the record as a
+    JSON string or dict, with `assets` as a string or already parsed."""
+    rec = json.loads(record) if isinstance(record, (str, bytes)) else dict(record)
+    assets = json.loads(rec["assets"]) if isinstance(rec.get("assets"), (str, bytes)) else rec.get("assets")
+    if not isinstance(assets, list):
+        raise ValueError("scene assets must be an array (or its JSON string)")
+    rec["assets"] = assets
+    return rec
+
+
 def compile_scene(name_or_dict, asset_dir: str | None = None) -> CompiledScene:
-    scene = load_scene_json(name_or_dict) if isinstance(name_or_dict, str) else name_or_dict
+    """A scene name (scenes/<name>.json), a Scene dict, or a backend record (scene_from_backend)."""
+    if isinstance(name_or_dict, str) and not name_or_dict.lstrip().startswith("{"):
+        scene = load_scene_json(name_or_dict)
+    else:
+        scene = scene_from_backend(name_or_dict)
     return serialize_world(World(asset_dir).load_from_scene(scene))

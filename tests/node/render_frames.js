@@ -4,11 +4,23 @@
 const fs = require('fs');
 const { NativeRenderer } = require('../../pathtracerdemo_amd/js/NativeRenderer');
 const { loadCompiledScene } = require('../../pathtracerdemo_amd/js/scene_io');
+const W = require('../../pathtracerdemo_amd/js/world');
+
+// req.assetsDir (export.export_scene_assets): the reference's path -- World.LoadFromScene over
+// the Scene JSON, meshes in ResourceManager.MeshPool, Initialize(World); else a compiled blob
+function loadWorld(req) {
+  if (!req.assetsDir) return loadCompiledScene(req.sceneDir);
+  const scene = W.sceneFromBackend(fs.readFileSync(req.assetsDir + '/scene.json', 'utf8'));
+  W.ResourceManager.LoadCompiledAssets(req.assetsDir + '/meshes', W.sceneMeshNames(scene));
+  const world = new W.World();
+  world.LoadFromScene(scene);
+  return world;
+}
 
 async function main() {
   const req = JSON.parse(process.argv[2]);
   const r = new NativeRenderer(req.width, req.height, { pipeline: req.pipeline, device: 0 });
-  await r.Initialize(loadCompiledScene(req.sceneDir));
+  await r.Initialize(loadWorld(req));
   for (let f = 0; f < req.frames; f++) {
     r.Update();
     await r.RenderAsync();
