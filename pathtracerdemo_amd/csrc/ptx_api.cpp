@@ -247,6 +247,9 @@ Scene make_scene(ptx_handle *h) {
     sc.row_end = h->cfg.row_end;
     sc.counters = (h->cfg.flags & PTX_FLAG_COUNT_WORK) ? (unsigned long long *)h->d_counters.p : nullptr;
     sc.census = (h->cfg.flags & PTX_FLAG_ROW_CENSUS) ? (unsigned long long *)h->d_census.p : nullptr;
+#ifdef PTX_WG_TIMES
+    sc.wgt = (unsigned long long *)h->d_wgt.p;
+#endif
     return sc;
 }
 
@@ -279,7 +282,9 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
         if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
         if (int rc = alloc_buf(h, h->d_wact0, slots * seg_px * jpp * 4u)) return rc;
         if (int rc = alloc_buf(h, h->d_wact1, slots * seg_px * jpp * 4u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wctr, 2u * kWaveMaxRounds * slots * 4u)) return rc;
+        // counts per round and slot, then the dynamic-batch counters of trace_queue: one per
+        // (tile set, launch sequence, round) -- kDynCounters words
+        if (int rc = alloc_buf(h, h->d_wctr, (2u * kWaveMaxRounds * slots + kDynCounters) * 4u)) return rc;
     }
     if (cap > h->wave_ray_cap) {
         free_buf(h->d_wrays);
@@ -322,6 +327,7 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     w.tile1 = w.ntile1 = 0;
     w.seg_phys = 0;
     w.cnt_stride = (uint32_t)slots;
+    w.dyn = nullptr;  // set per launch sequence (launch_wave_parts)
     h->wave_slots = (uint32_t)slots;
     return PTX_OK;
 }
@@ -478,7 +484,12 @@ hipError_t spatial_summaries(ptx_handle *h, hipStream_t st) {
 hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes, int npasses,
                              bool summaries, const WaveBufs *then, hipEvent_t then_wait) {
     static const int env_k = getenv("PTX_WAVE_STREAMS") ? atoi(getenv("PTX_WAVE_STREAMS")) : 0;
-    int k = env_k > 0 ? env_k : 3;
+    // pipelined frames: each of the two contexts in flight runs its passes as ONE launch
+    // sequence (whole-band launches, dynamic trace batches); measured at 1080p C3 reuse: 1
+    // stream per context 338 Msamples/s, 2 streams 308, unpipelined 3 streams 320
+    // (PTX_PIPE_STREAMS: A/B)
+    static const int env_pk = getenv("PTX_PIPE_STREAMS") ? atoi(getenv("PTX_PIPE_STREAMS")) : 0;
+    int k = h->alt_stream && pipelined(h) ? (env_pk > 0 ? env_pk : 1) : env_k > 0 ? env_k : 3;
     if (h->cfg.flags & PTX_FLAG_SINGLE_STREAM) k = 1;
     k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
     if ((uint32_t)k > std::max(w.nseg, then ? then->nseg : 0u)) k = (int)std::max(w.nseg, then ? then->nseg : 0u);
@@ -513,6 +524,11 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
             const WaveBufs &ws = set ? *then : w;
             if (set && then_wait && (e = hipStreamWaitEvent(st, then_wait, 0)) != hipSuccess) return e;
             WaveBufs part = ws;
+            // dynamic trace batches (PTX_TRACE_DYN=0: one slot per trace workgroup, A/B)
+            static const bool dyn_off = getenv("PTX_TRACE_DYN") && atoi(getenv("PTX_TRACE_DYN")) == 0;
+            part.dyn = dyn_off ? nullptr
+                               : (uint32_t *)h->d_wctr.p + 2u * kWaveMaxRounds * ws.cnt_stride +
+                                     (uint32_t)((set * ptx_handle::kMaxSplit + q) * kWaveMaxRounds) * kDynRoundWords;
             part.seg_base = (uint32_t)((uint64_t)ws.nseg * q / k);
             part.seg_count = (uint32_t)((uint64_t)ws.nseg * (q + 1) / k) - part.seg_base;
             if (!part.seg_count) continue;
@@ -552,6 +568,76 @@ void mark_history(ptx_handle *h) {
     h->hist_valid = true;
 }
 
+// ---------------------------------------------------------------- frame pipelining
+bool pipelined(const ptx_handle *h) {
+    static const bool off = getenv("PTX_PIPELINE_FRAMES") && atoi(getenv("PTX_PIPELINE_FRAMES")) == 0;  // A/B
+    const uint32_t fl = h->cfg.flags;
+    return !off && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !h->comm && !h->halo_top && !h->halo_bot &&
+           !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE | PTX_FLAG_COUNT_WORK |
+                   PTX_FLAG_TIME_LAUNCHES | PTX_FLAG_SINGLE_STREAM | PTX_FLAG_ROW_CENSUS)) &&
+           (h->alt_active ? h->stream == h->alt_stream : h->stream == h->own_stream);
+}
+int quiesce(ptx_handle *h) {
+    for (hipStream_t q : {h->stream, h->alt.stream})
+        if (q) HIP_CHECK(h, hipStreamSynchronize(q));
+    for (int k = 1; k < ptx_handle::kMaxSplit; ++k) {
+        if (h->sub[k]) HIP_CHECK(h, hipStreamSynchronize(h->sub[k]));
+        if (h->alt.sub[k]) HIP_CHECK(h, hipStreamSynchronize(h->alt.sub[k]));
+    }
+    return PTX_OK;
+}
+static void swap_frame_ctx(ptx_handle *h) {
+    ptx_handle::FrameCtx &a = h->alt;
+    std::swap(h->d_gbuf, a.gbuf);
+    std::swap(h->d_res, a.res);
+    std::swap(h->d_nbr, a.nbr);
+    std::swap(h->d_wstate, a.wstate);
+    std::swap(h->d_wrays, a.wrays);
+    std::swap(h->d_wres0, a.wres0);
+    std::swap(h->d_wres1, a.wres1);
+    std::swap(h->d_wact0, a.wact0);
+    std::swap(h->d_wact1, a.wact1);
+    std::swap(h->d_wctr, a.wctr);
+    std::swap(h->wave_ray_cap, a.wave_ray_cap);
+    std::swap(h->wave_slots, a.wave_slots);
+    std::swap(h->stream, a.stream);
+    for (int k = 0; k < ptx_handle::kMaxSplit; ++k) {
+        std::swap(h->sub[k], a.sub[k]);
+        std::swap(h->ev_join[k], a.ev_join[k]);
+    }
+    std::swap(h->ev_fork, a.ev_fork);
+    std::swap(h->init_state_valid, a.init_state_valid);
+    std::swap(h->nbr_valid, a.nbr_valid);
+    h->alt_active = !h->alt_active;
+}
+// the second context's G-buffer, reservoirs and stream (its queues, wave state and summaries
+// are allocated by wave_buffers / reuse_buffers on its first frame)
+static int ensure_alt(ptx_handle *h) {
+    ptx_handle::FrameCtx &a = h->alt;
+    if (!h->alt_stream) {
+        HIP_CHECK(h, hipStreamCreateWithFlags(&h->alt_stream, hipStreamNonBlocking));
+        a.stream = h->alt_stream;
+    }
+    if (!h->ev_prev) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_prev, hipEventDisableTiming));
+    DevBuf &g = h->alt_active ? h->d_gbuf : a.gbuf, &r = h->alt_active ? h->d_res : a.res;
+    if (!g.p) {
+        if (int rc = alloc_buf(h, g, h->d_gbuf.bytes ? h->d_gbuf.bytes : a.gbuf.bytes)) return rc;
+        HIP_CHECK(h, hipMemset(g.p, 0, g.bytes));
+    }
+    if (!r.p) {
+        if (int rc = alloc_buf(h, r, h->d_res.bytes ? h->d_res.bytes : a.res.bytes)) return rc;
+        HIP_CHECK(h, hipMemset(r.p, 0, r.bytes));
+    }
+    return PTX_OK;
+}
+// Back to the first context (its stream is own_stream) before the stream is replaced.
+static int leave_alt(ptx_handle *h) {
+    if (!h->alt_active) return PTX_OK;
+    if (int rc = quiesce(h)) return rc;
+    swap_frame_ctx(h);
+    return PTX_OK;
+}
+
 // A whole ReSTIR frame in wavefront form (G-buffer -> init -> final per segment group), timed
 // as one unit in stats slot PTX_STAT_FRAME.  Returns 1 if this path does not apply.
 static int timed_wave_frame(ptx_handle *h) {
@@ -564,6 +650,14 @@ static int timed_wave_frame(ptx_handle *h) {
     }
     Scene sc = make_scene(h);
     if (!tables_fit_lds(sc)) return 1;
+    const bool pipe = pipelined(h);
+    if (pipe) {
+        // frame N goes to the other context; ev_prev marks everything enqueued before it
+        // (frame N-1 and any host operation since) on the current context's stream
+        if (int rc = ensure_alt(h)) return rc;
+        HIP_CHECK(h, hipEventRecord(h->ev_prev, h->stream));
+        swap_frame_ctx(h);
+    }
     WaveBufs w{};
     if (int rc = wave_buffers(h, w)) return rc;
     TimedLaunch &t = h->ring[h->ring_pos];
@@ -571,7 +665,19 @@ static int timed_wave_frame(ptx_handle *h) {
     resolve_event(t, h);
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
     hipError_t e;
-    if (has_reuse(h)) {
+    if (pipe) {
+        // G-buffer + PT_1 of this frame overlap the previous frame's spatial pass + PT_4; the
+        // temporal pass reads that frame's spatial output (d_hist) and shares its job buffers
+        if (int rc = reuse_buffers(h)) return rc;
+        static const int front[2] = {PTX_PASS_GBUFFER, PTX_PASS_INIT};
+        static const int temporal[1] = {PTX_PASS_TEMPORAL};
+        static const int back[2] = {PTX_PASS_SPATIAL, PTX_PASS_FINAL};
+        e = launch_wave_parts(h, sc, w, front, 2);
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
+        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, temporal, 1);
+        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, back, 2);
+        if (e == hipSuccess) mark_history(h);
+    } else if (has_reuse(h)) {
         // per-pixel passes up to the temporal output, then (after every segment is done:
         // the spatial pass reads neighbours) spatial + PT_4
         if (int rc = reuse_buffers(h)) return rc;
@@ -755,6 +861,12 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
         rc = alloc_buf(h, h->d_census, (size_t)h->census_blocks * kCensusWords * 8u);
         if (!rc && hipMemset(h->d_census.p, 0, h->d_census.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
+#ifdef PTX_WG_TIMES
+    if (!rc && getenv("PTX_WGT")) {  // 4 header words + 2^20 records of 4 words
+        rc = alloc_buf(h, h->d_wgt, (4u + 4u * (1u << 20)) * 8u);
+        if (!rc && hipMemset(h->d_wgt.p, 0, 32u) != hipSuccess) rc = PTX_E_HIP;
+    }
+#endif
     if (!rc && hipMemset(h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (!rc && hipMemset(h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (!rc && hipMemset(h->d_gbuf.p, 0, h->d_gbuf.bytes) != hipSuccess) rc = PTX_E_HIP;
@@ -772,6 +884,7 @@ int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const
     if (!h) return PTX_E_INVALID;
     HIP_CHECK(h, hipSetDevice(h->device));  // handles of one process may sit on several GPUs
     if (!scene || !geometry || (!accel && n_accel)) return fail(h, PTX_E_INVALID, "null scene array");
+    if (int rc = quiesce(h)) return rc;  // frames in flight still read the old scene and layout
     h->scene.assign(scene, scene + n_scene);
     h->geometry.assign(geometry, geometry + n_geometry);
     h->accel.assign(accel ? accel : scene, accel ? accel + n_accel : scene);
@@ -985,6 +1098,22 @@ int ptx_reset_stats(ptx_handle *h) {
     return PTX_OK;
 }
 
+#ifdef PTX_WG_TIMES
+// Diagnostic build only: copies up to max_records per-wave records {start, end (100 MHz
+// ticks), kernel id << 32 | block, wave-in-block << 32 | HW_ID} recorded since the last call
+// and restarts the log.  Returns the record count (>= 0) or a PTX_E_* status.
+int ptx_diag_wave_times(ptx_handle *h, uint64_t *out, size_t max_records) {
+    if (!h || !h->d_wgt.p) return PTX_E_INVALID;
+    HIP_CHECK(h, hipDeviceSynchronize());
+    uint64_t n = 0;
+    HIP_CHECK(h, hipMemcpy(&n, h->d_wgt.p, 8, hipMemcpyDeviceToHost));
+    n = std::min<uint64_t>(std::min<uint64_t>(n, 1u << 20), max_records);
+    if (n && out) HIP_CHECK(h, hipMemcpy(out, (uint64_t *)h->d_wgt.p + 4, n * 32u, hipMemcpyDeviceToHost));
+    HIP_CHECK(h, hipMemset(h->d_wgt.p, 0, 8));
+    return (int)n;
+}
+#endif
+
 int ptx_row_census(ptx_handle *h, uint64_t *out, size_t n_tile_rows) {
     if (!h || !out) return PTX_E_INVALID;
     if (!(h->cfg.flags & PTX_FLAG_ROW_CENSUS)) return fail(h, PTX_E_INVALID, "handle has no PTX_FLAG_ROW_CENSUS");
@@ -1086,6 +1215,7 @@ int ptx_trace(ptx_handle *h, const float *rays, float *hits, size_t n, int eps_m
 
 int ptx_set_stream(ptx_handle *h, void *hip_stream) {
     if (!h) return PTX_E_INVALID;
+    if (int rc = leave_alt(h)) return rc;
     h->stream = hip_stream ? (hipStream_t)hip_stream : h->own_stream;
     return PTX_OK;
 }
@@ -1094,6 +1224,8 @@ int ptx_destroy(ptx_handle *h) {
     if (!h) return PTX_E_INVALID;
     (void)hipSetDevice(h->device);
     comm_destroy(h);
+    (void)quiesce(h);
+    if (h->alt_active) swap_frame_ctx(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (hipStream_t q : h->sub)
         if (q) (void)hipStreamSynchronize(q);
@@ -1107,6 +1239,16 @@ int ptx_destroy(ptx_handle *h) {
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
                       &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_direct, &h->d_census})
         free_buf(*b);
+    ptx_handle::FrameCtx &a = h->alt;
+    for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wact0, &a.wact1, &a.wctr})
+        free_buf(*b);
+    if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
+    for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {
+        if (a.ev_join[q]) (void)hipEventDestroy(a.ev_join[q]);
+        if (a.sub[q]) (void)hipStreamDestroy(a.sub[q]);
+    }
+    if (h->alt_stream) (void)hipStreamDestroy(h->alt_stream);
+    if (h->ev_prev) (void)hipEventDestroy(h->ev_prev);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {
         if (h->ev_join[q]) (void)hipEventDestroy(h->ev_join[q]);

@@ -83,7 +83,38 @@ struct Scene {
     // (8 pixel rows); block census_tile_rows() + s: every query of trace-queue slot s
     // (segments of contiguous tiles in census mode, so the host maps them to tile rows)
     unsigned long long *census;
+#ifdef PTX_WG_TIMES
+    unsigned long long *wgt;  // diagnostic build only: per-wave {start, end, kernel | block, hw id} records
+#endif
 };
+
+// Diagnostic build (make wgt -> libptx_wgt.so, tools/wave_timeline.py): every instrumented
+// kernel's waves record their start / end on the 100 MHz real-time clock, so the tool can
+// draw the chip's wave occupancy over a frame and each launch's tail.  No-op otherwise.
+enum : uint32_t { KID_TRACE = 1, KID_GBUF, KID_INIT_START, KID_INIT_STEP, KID_FINAL_START, KID_FINAL_STEP,
+                  KID_TEMP_START, KID_TEMP_COMBINE, KID_SPAT_START, KID_JOB_STEP, KID_SPAT_COMBINE };
+#ifdef PTX_WG_TIMES
+struct WaveTimer {
+    unsigned long long *buf;
+    unsigned long long t0;
+    uint32_t kid;
+    __device__ WaveTimer(unsigned long long *b, uint32_t k) : buf(b), t0(__builtin_amdgcn_s_memrealtime()), kid(k) {}
+    __device__ ~WaveTimer() {
+        if (!buf || __lane_id() != 0u) return;
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long i = atomicAdd(buf, 1ull);
+        if (i >= (1ull << 20)) return;
+        unsigned long long *r = buf + 4u + 4u * i;
+        r[0] = t0;
+        r[1] = t1;
+        r[2] = ((unsigned long long)kid << 32) | blockIdx.x;
+        r[3] = ((unsigned long long)(threadIdx.x >> 6) << 32) | (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
+};
+#define PTX_WAVE_TIMER(sc, k) WaveTimer wave_timer_((sc).wgt, (k))
+#else
+#define PTX_WAVE_TIMER(sc, k) ((void)0)
+#endif
 
 // ------------------------------------------------------------------ f32 vector algebra
 // Operation order is fixed (left-to-right sums, no contraction): DESIGN.md §Numerics.

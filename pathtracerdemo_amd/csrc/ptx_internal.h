@@ -77,6 +77,27 @@ struct ptx_handle {
     // row census (PTX_FLAG_ROW_CENSUS): kCensusWords u64 per G-buffer tile row + queue slot
     DevBuf d_census;
     uint32_t census_blocks = 0;
+    // diagnostic build (PTX_WG_TIMES) with PTX_WGT=1 in the environment: per-wave timing records
+    DevBuf d_wgt;
+    // Frame pipelining (pipelined(): whole-image reuse handles on their own streams): two frames
+    // in flight, each with its own G-buffer, reservoirs, neighbour summaries, wave state,
+    // queues and streams.  Frame N's G-buffer + PT_1 run beside frame N-1's spatial pass + PT_4;
+    // its temporal pass (which reads frame N-1's spatial output, d_hist, and reuses the shared
+    // shift-job buffers) waits for ev_prev, recorded on N-1's stream when N was enqueued.
+    // ptx_render swaps the members above with `alt` per frame, so everything else always sees
+    // the latest frame's buffers; the shared ones (accumulation, history, jobs, scene) never move.
+    struct FrameCtx {
+        DevBuf gbuf, res, nbr, wstate, wrays, wres0, wres1, wact0, wact1, wctr;
+        size_t wave_ray_cap = 0;
+        uint32_t wave_slots = 0;
+        hipStream_t stream = nullptr;
+        hipStream_t sub[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
+        hipEvent_t ev_fork = nullptr, ev_join[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
+        bool init_state_valid = false, nbr_valid = false;
+    } alt;
+    bool alt_active = false;      // the members above hold the second context (stream == alt stream)
+    hipStream_t alt_stream = nullptr;  // the second context's stream (owned)
+    hipEvent_t ev_prev = nullptr;
     // multi-GPU (ptx_comm.cpp): the RCCL communicator this handle owns (ncclComm_t), its
     // rank and world; the halo exchange stream and its fork / done events
     void *comm = nullptr;
@@ -120,6 +141,10 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
 // the neighbour summaries of the halo rows (or of everything when the band's are stale)
 hipError_t spatial_summaries(ptx_handle *h, hipStream_t st);
 void mark_history(ptx_handle *h);
+// frame pipelining: whether ptx_render runs this handle's frames two in flight; wait for both
+// frames' streams (before anything that replaces shared buffers or the stream)
+bool pipelined(const ptx_handle *h);
+int quiesce(ptx_handle *h);
 // ptx_comm.cpp: a frame of a band handle that owns a communicator; its teardown
 int render_band_nccl(ptx_handle *h);
 void comm_destroy(ptx_handle *h);

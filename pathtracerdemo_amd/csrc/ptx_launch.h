@@ -50,6 +50,12 @@ constexpr uint32_t kStateCs2 = 7u, kStateCs3 = 8u, kStateTsel = 9u;
 constexpr uint32_t kWaveSegPixels = 768u;  // padded pixels per segment (12 8x8 tiles); 768 > 512 > 1024 > 256
 constexpr int kWaveRoundsInit = 3, kWaveRoundsFinal = 3, kWaveRoundsMcpt = 4;
 constexpr int kWaveMaxRounds = 5;
+// dynamic trace batches: per (tile set, launch sequence, round) kDynHeads dequeue heads, one
+// per XCD, each on its own 128-byte line (kDynStride words): one device-scope head saturates
+// at ~88 dequeues/us (MI355X_MICROARCH.md, dequeue), far below a trace launch's demand
+constexpr uint32_t kDynHeads = 8u, kDynStride = 32u;
+constexpr uint32_t kDynRoundWords = kDynHeads * kDynStride;
+constexpr uint32_t kDynCounters = 2u * 4u * kWaveMaxRounds * kDynRoundWords;
 struct WaveBufs {
     float4 *state;       // kWaveStateSlots * npix, SoA
     uint32_t npix;       // pixels of the band
@@ -76,6 +82,10 @@ struct WaveBufs {
     // storage, count words at cnt[(2r or 2r+1) * cnt_stride + slot]).  Two tile sets in flight
     // at once use disjoint physical slots.
     uint32_t seg_phys, cnt_stride;
+    // Dynamic trace batches (trace_queue): this launch sequence's kWaveMaxRounds groups of
+    // kDynHeads dequeue heads (round r at dyn + r * kDynRoundWords; the logic round that emits
+    // trace round r zeroes them in seg_begin); nullptr = one slot per trace workgroup.
+    uint32_t *dyn;
 };
 // occ_only: every query of the round is Q_OCC (any-hit kernel instance)
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t stack_depth,

@@ -151,6 +151,7 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
 void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_JOB_STEP);
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
@@ -280,6 +281,7 @@ __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBu
 // (the inlined replay needs more registers than the 4-wave budget: 160 B/lane spilled there)
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(2, 8)))
 void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_TEMP_START);
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
@@ -304,6 +306,7 @@ void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
 // Temporal resampling of the pixel's PT_1 reservoir with the previous frame's output at
 // the same pixel (oracle temporal_pixel): static camera, identity shift.
 __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_TEMP_COMBINE);
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
     for (uint32_t k = 0; k < w.seg_px; k += WB) {
         const uint32_t q = seg_pixel(w, j, k);
@@ -408,6 +411,7 @@ __device__ __forceinline__ bool job_begin_at(const Scene &sc, const ReuseArgs &A
 #endif
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(SPATIAL_START_WAVES, 8)))
 void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_SPAT_START);
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
@@ -585,6 +589,7 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
 }
 
 __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE);
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
     for (uint32_t k = 0; k < w.seg_px; k += WB) {
         const uint32_t q = seg_pixel(w, j, k);

@@ -27,6 +27,7 @@
 // light visibility), MCPT <= 4 (primary + 3 bounces with all lights' shadow rays).
 #include "ptx_wave_common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace ptx {
@@ -41,16 +42,149 @@ namespace ptx {
 #ifndef TRACE_COOP
 #define TRACE_COOP true
 #endif
+// One wave's batch of up to 64 queries (lane i of `rays` / `res`; `active` = lane has one).
+// Every lane of the wave calls the traversal every time -- lanes without a query (past the
+// segment's end, or whose Visibility walk is over) with a NaN bound, which no box overlaps --
+// so the whole wave takes part in the cooperative leaf phases.
+template <bool COUNT, bool PROF, bool OCC>
+__device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
+                                            uint32_t *stack, CoopLds coop, const float4 *rays, float4 *res,
+                                            uint32_t i, bool active) {
+    float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+    if (active) {
+        a = rays[2u * i];
+        b = rays[2u * i + 1u];
+    }
+    Ray r{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)};
+    const uint32_t kind = asu(b.w);
+    const bool vis = kind != Q_CLOSEST;
+    // Visibility (SH/PT_1_InitPass.wgsl:774-802) walks through transmissive hits:
+    // one trace site, looped, so the traversal code is emitted once
+    float T = 1.0f, remain = a.w;
+    for (uint32_t it = 0u;; ++it) {
+        const float t_max = !active ? __builtin_nanf("") : vis ? fminf(remain, 1e10f) : 1e10f;
+        const Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP>(sc, subs, insts, r, eps, stack, WB, t_max,
+                                                                         coop);
+        if (active && !vis) {
+            const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
+            res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
+            res[2u * i + 1u] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
+            active = false;
+        } else if (active) {
+            float out = -1.0f;
+            if (!h.valid || h.t > remain) out = T;
+            else {
+                const float tr = kind == Q_OCC ? 0.0f : get_transmission(sc, h.s.inst, h.s.mat);
+                if (tr == 0.0f) out = 0.0f;
+                else {
+                    T *= tr;
+                    remain -= h.t;
+                    r.o = h.pos;
+                    if (it == 4u) out = 0.0f;  // Visibility gives up after 5 segments
+                }
+            }
+            if (out >= 0.0f) {  // only res.x is written: .yzw and res[2i+1] carry the payload
+                res[2u * i].x = out;
+                active = false;
+            }
+        }
+        if (__ballot(active) == 0ull) break;
+    }
+}
+
+// Dynamic batches (WaveBufs::dyn): the launch's rays -- every slot of the launch's segment
+// range -- are one list of 64-query batches (a slot's batch k = its queries 64k .. 64k+63,
+// consecutive entries of one tile, coherent), and every wave takes the next batch from a
+// per-(part, round) counter until the list is exhausted.  A launch then ends when the
+// last batch ends, not when the heaviest segment does: with a fixed slot per workgroup
+// the spatial pass's largest trace launch ran its median workgroup 1.14 ms and its slowest
+// 1.90 ms (tools/wave_timeline.py).  Each query's result goes to its own slot, so the
+// assignment of batches to waves changes nothing in the output.  The workgroup's first
+// (seg_count + 1) dynamic-LDS words hold the exclusive prefix of the slots' batch counts.
+__device__ __forceinline__ uint32_t dyn_prefix_words(const WaveBufs &w) { return (w.seg_count + 4u) & ~3u; }
+__device__ __forceinline__ void dyn_prefix(const WaveBufs &w, uint32_t round, uint32_t *pref) {
+    __shared__ uint32_t l_wsum[WB / 64];
+    const uint32_t n = w.seg_count, per = (n + WB - 1u) / WB, t0 = threadIdx.x * per;
+    const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.cnt_stride + w.seg_phys + w.seg_base;
+    uint32_t loc = 0u;
+    for (uint32_t k = 0; k < per && t0 + k < n; ++k) loc += (cnt[t0 + k] + 63u) >> 6;
+    uint32_t total;
+    uint32_t ex = wave_scan(loc, total);
+    if (__lane_id() == 63u) l_wsum[threadIdx.x >> 6] = ex + loc;
+    __syncthreads();
+    for (uint32_t q = 0; q < (threadIdx.x >> 6); ++q) ex += l_wsum[q];
+    for (uint32_t k = 0; k < per && t0 + k < n; ++k) {
+        pref[t0 + k] = ex;
+        ex += (cnt[t0 + k] + 63u) >> 6;
+    }
+    if (threadIdx.x == WB - 1u) pref[n] = ex;
+    __syncthreads();
+}
+
 template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true, bool OCC = false>
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
+    PTX_WAVE_TIMER(sc, KID_TRACE);
     extern __shared__ uint32_t wstack[];
-    uint32_t *stack = wstack + threadIdx.x;
+    const bool dyn = !COUNT && w.dyn != nullptr;
+    uint32_t *pref = wstack;                                                // dyn: batch prefix
+    uint32_t *stack = wstack + (dyn ? dyn_prefix_words(w) : 0u) + threadIdx.x;  // then the stacks
     __shared__ SubRoot l_subs[LDS_TABLES ? kLdsSubs : 1];
     __shared__ Inst l_insts[LDS_TABLES ? kLdsInsts : 1];
     __shared__ unsigned long long c_key[WB];
     const CoopLds coop{c_key + (threadIdx.x & ~63u)};
-    // workgroup -> (segment, share): the trace_split workgroups of a segment take its
+    if (dyn) {
+        dyn_prefix(w, round, pref);
+        const uint32_t total = pref[w.seg_count];
+        if (blockIdx.x * (WB / 64u) >= total) return;  // (workgroup-uniform) more waves than batches
+        if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
+        const SubRoot *subs = LDS_TABLES ? l_subs : sc.subs;
+        const Inst *insts = LDS_TABLES ? l_insts : sc.insts;
+        // the batch list in kDynHeads contiguous chunks, chunk x dequeued through head x by the
+        // waves of XCD x (workgroups are dealt to the XCDs round-robin: block b on XCD b % 8);
+        // a wave whose chunk is drained moves on to the next one
+        uint32_t *heads = w.dyn + round * kDynRoundWords;
+        const uint32_t lane = __lane_id();
+        uint32_t x = blockIdx.x % kDynHeads, visited = 0u;
+        uint32_t c0 = (uint32_t)((uint64_t)total * x / kDynHeads), c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
+        // each dequeue takes G consecutive batches (WaveBufs::trace_split in this mode): one
+        // atomic per G * 64 queries, traced back to back by the same wave
+        const uint32_t G = w.trace_split;
+        uint32_t bnext = 0u;
+        if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
+        uint32_t bi = c0 + G * __shfl(bnext, 0);
+        for (;;) {  // wave-uniform
+            if (bi >= c1) {  // this chunk is drained: the next head
+                if (++visited == kDynHeads) break;
+                x = (x + 1u) % kDynHeads;
+                c0 = (uint32_t)((uint64_t)total * x / kDynHeads);
+                c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
+                if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
+                bi = c0 + G * __shfl(bnext, 0);
+                continue;
+            }
+            if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);  // the next dequeue, fetched ahead
+            const uint32_t bend = min(bi + G, c1);
+            uint32_t lo = 0u;
+            for (; bi < bend; ++bi) {
+                uint32_t hi = w.seg_count;  // last slot with pref <= bi (batches ascend: search from lo)
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pref[mid] <= bi) lo = mid;
+                    else hi = mid;
+                }
+                const uint32_t j = w.seg_phys + w.seg_base + lo;
+                const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
+                const uint32_t i = (bi - pref[lo]) * 64u + lane;
+                trace_batch<COUNT, PROF, OCC>(sc, subs, insts, eps, stack, coop,
+                                              w.rays + 2u * (size_t)j * w.ray_stride,
+                                              w.res[round & 1u] + 2u * (size_t)j * w.ray_stride, i, i < n);
+            }
+            bi = c0 + G * __shfl(bnext, 0);
+        }
+        return;
+    }
+    // Static: workgroup -> (segment, share): the trace_split workgroups of a segment take its
     // 256-ray batches round-robin; results go to the rays' own slots, so the split is exact.
     // A segment's shares are consecutive blocks, so they spread over XCDs (blocks b and b+8
     // share one: MI355X_MICROARCH.md, workgroup dispatch) -- measured faster than keeping
@@ -68,52 +202,9 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         sc.counters = sc.census + (size_t)kCensusWords * ((sc.row_end - sc.row_begin + 7u) / 8u + j);
     const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
     float4 *res = w.res[round & 1u] + 2u * (size_t)j * w.ray_stride;
-    // Every lane of the wave calls the traversal every time -- lanes without a query (past
-    // the segment's end, or whose Visibility walk is over) with a NaN bound, which no box
-    // overlaps -- so the whole wave takes part in the cooperative leaf phases.
     for (uint32_t i0 = share * WB; i0 < n; i0 += K * WB) {  // workgroup-uniform
         const uint32_t i = i0 + threadIdx.x;
-        bool active = i < n;
-        float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
-        if (active) {
-            a = rays[2u * i];
-            b = rays[2u * i + 1u];
-        }
-        Ray r{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)};
-        const uint32_t kind = asu(b.w);
-        const bool vis = kind != Q_CLOSEST;
-        // Visibility (SH/PT_1_InitPass.wgsl:774-802) walks through transmissive hits:
-        // one trace site, looped, so the traversal code is emitted once
-        float T = 1.0f, remain = a.w;
-        for (uint32_t it = 0u;; ++it) {
-            const float t_max = !active ? __builtin_nanf("") : vis ? fminf(remain, 1e10f) : 1e10f;
-            const Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP>(sc, subs, insts, r, eps, stack, WB, t_max,
-                                                                             coop);
-            if (active && !vis) {
-                const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
-                res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
-                res[2u * i + 1u] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
-                active = false;
-            } else if (active) {
-                float out = -1.0f;
-                if (!h.valid || h.t > remain) out = T;
-                else {
-                    const float tr = kind == Q_OCC ? 0.0f : get_transmission(sc, h.s.inst, h.s.mat);
-                    if (tr == 0.0f) out = 0.0f;
-                    else {
-                        T *= tr;
-                        remain -= h.t;
-                        r.o = h.pos;
-                        if (it == 4u) out = 0.0f;  // Visibility gives up after 5 segments
-                    }
-                }
-                if (out >= 0.0f) {  // only res.x is written: .yzw and res[2i+1] carry the payload
-                    res[2u * i].x = out;
-                    active = false;
-                }
-            }
-            if (__ballot(active) == 0ull) break;
-        }
+        trace_batch<COUNT, PROF, OCC>(sc, subs, insts, eps, stack, coop, rays, res, i, i < n);
     }
 }
 
@@ -298,6 +389,7 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
 // gbuffer_kernel (SH/PT_01_GBufferPass.wgsl:496-507,643-656).
 template <bool ROOTQ>
 __global__ __launch_bounds__(WB) void wgbuffer(Scene sc, WaveBufs w, uint4 *gbuf) {
+    PTX_WAVE_TIMER(sc, KID_GBUF);
     extern __shared__ uint32_t wstack[];
     uint32_t *stack = wstack + threadIdx.x;
     __shared__ SubRoot l_subs[kLdsSubs];
@@ -472,6 +564,7 @@ __device__ __forceinline__ void winit_finish(const WInit &s, uint4 *reservoir, u
 }
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void winit_start(Scene sc, WaveBufs w, const uint4 *gbuf, uint4 *reservoir) {
+    PTX_WAVE_TIMER(sc, KID_INIT_START);
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
@@ -512,6 +605,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
 }
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void winit_step(Scene sc, WaveBufs w, uint32_t round, uint4 *reservoir) {
+    PTX_WAVE_TIMER(sc, KID_INIT_STEP);
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
@@ -924,12 +1018,24 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
 
 // =========================================================================== host side
 // trace_queue's grid: trace_split workgroups per segment
-static inline uint32_t trace_grid(const WaveBufs &w) { return w.seg_count * w.trace_split; }
+// dynamic batches: one workgroup per slot, at most kDynMaxGroups (the chip holds ~1024 trace
+// workgroups; later ones find the list drained and leave)
+constexpr uint32_t kDynMaxGroups = 1024u, kDynMaxSlots = 4096u;
+static inline bool trace_dyn(const WaveBufs &w) { return w.dyn != nullptr && w.seg_count <= kDynMaxSlots; }
+static inline uint32_t trace_grid(const WaveBufs &w) {
+    return trace_dyn(w) ? std::min(w.seg_count, kDynMaxGroups) : w.seg_count * w.trace_split;
+}
 
-hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t depth, hipStream_t s,
+hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_mode, uint32_t depth, hipStream_t s,
                       bool occ_only) {
     const PassEps eps = eps_mode == 0 ? PassEps{1e-8f, 1e-6f} : PassEps{1e-4f, 1e-8f};
-    const size_t lds = stack_lds_bytes(depth);
+    WaveBufs w = w_in;
+    if (sc.counters || !trace_dyn(w)) w.dyn = nullptr;  // counting builds keep the per-slot census
+    if (w.dyn) {  // batches per dequeue (A/B: PTX_TRACE_DYN_G)
+        static const uint32_t g = getenv("PTX_TRACE_DYN_G") ? (uint32_t)atoi(getenv("PTX_TRACE_DYN_G")) : 0u;
+        w.trace_split = g >= 1u && g <= 16u ? g : 1u;
+    }
+    const size_t lds = stack_lds_bytes(depth) + (w.dyn ? 4u * (size_t)((w.seg_count + 4u) & ~3u) : 0u);
     if (occ_only && sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts) {  // occlusion rounds (GI spatial)
         if (sc.counters)
             hipLaunchKernelGGL((trace_queue<true, 6, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,

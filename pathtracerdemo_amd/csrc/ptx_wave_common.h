@@ -64,6 +64,9 @@ __device__ __forceinline__ Seg seg_begin(const WaveBufs &w, uint32_t round, uint
     g.l_ray = lds;
     g.l_act = lds + 1;
     if (threadIdx.x == 0) { lds[0] = 0u; lds[1] = 0u; }
+    // the batch counter of the trace round this launch feeds (the trace kernel runs after
+    // this launch on the same stream)
+    if (w.dyn && blockIdx.x == 0 && threadIdx.x < kDynHeads) w.dyn[round * kDynRoundWords + threadIdx.x * kDynStride] = 0u;
     __syncthreads();
     return g;
 }

@@ -244,3 +244,36 @@ def test_c3_full_hd_reuse_windows_bit_exact(scene3, oracle_mod):
         assert_same(hist[y0:y1], fr.res_hist[y0:y1], f"spatial output rows {y0}..{y1}")
         assert_same(img[y0:y1], fr.accum[y0:y1], f"radiance rows {y0}..{y1}")
     assert np.isfinite(img).all()
+
+
+@pytest.mark.gpu
+def test_pipelined_frames_interleaved_with_host_ops(scene3, oracle_mod, native):
+    """Frame pipelining (ptx_render runs frame N's G-buffer + PT_1 beside frame N-1's spatial
+    pass, on a second context): host operations between frames -- buffer reads, an
+    accumulation reset (which also drops the history), a camera move -- see and act on the
+    latest frame exactly as with one frame in flight."""
+    O, W, H = oracle_mod, 72, 56
+    fr = oracle_frame(O, scene3, W, H)
+    r = reuse_renderer(scene3, W, H)
+    for f in range(1, 8):
+        if f == 5:  # camera move: the handle drops the history itself
+            r.GetCamera().set_location(0.25, 0.1, 5.5)
+        r.Update()
+        if f == 5:
+            fr = oracle_frame(O, scene3, W, H)
+            fr.uniform[:] = r.uniform
+            fr.accum[:] = np.frombuffer(r.read_image().tobytes(), np.float32).reshape(fr.accum.shape)
+        fr.set_frame_index(r.uniform[23])
+        fr.run_reuse_frame(threads=8)
+        r.Render()
+        if f == 2:
+            assert_same(r.read_history(), fr.res_hist, "spatial output, frame 2")
+            assert_same(r.read_gbuffer(), fr.gbuffer, "G-buffer, frame 2")
+        if f == 3:  # zero the accumulation and drop the history, as ptx_reset_accumulation does
+            r.reset_accumulation()
+            fr.accum[:] = 0.0
+            fr.hist_valid = False
+    assert_same(r.read_reservoir(), fr.reservoir, "temporal output")
+    assert_same(r.read_history(), fr.res_hist, "spatial output")
+    assert_same(r.read_image(), fr.accum, "accumulated radiance")
+    r.close()
