@@ -481,6 +481,7 @@ hipError_t spatial_summaries(ptx_handle *h, hipStream_t st) {
     return e;
 }
 
+static bool whole_band_sequences(const ptx_handle *h);
 hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes, int npasses,
                              bool summaries, const WaveBufs *then, hipEvent_t then_wait) {
     static const int env_k = getenv("PTX_WAVE_STREAMS") ? atoi(getenv("PTX_WAVE_STREAMS")) : 0;
@@ -524,9 +525,14 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
             const WaveBufs &ws = set ? *then : w;
             if (set && then_wait && (e = hipStreamWaitEvent(st, then_wait, 0)) != hipSuccess) return e;
             WaveBufs part = ws;
-            // dynamic trace batches (PTX_TRACE_DYN=0: one slot per trace workgroup, A/B)
-            static const bool dyn_off = getenv("PTX_TRACE_DYN") && atoi(getenv("PTX_TRACE_DYN")) == 0;
-            part.dyn = dyn_off ? nullptr
+            // dynamic trace batches: with the pipelined frames' whole-band launch sequences
+            // (+5.6 % there); with three concurrent sequences per frame the other sequences
+            // already fill a launch's tail and the per-workgroup prefix costs more than it
+            // saves (1080p, static vs dynamic: ReSTIR 1240 vs 1081, GI 675 vs 625, TEST_MCPT
+            // 1264 vs 1229 Msamples/s).  PTX_TRACE_DYN=0 / 1 forces it off / on (A/B).
+            static const int dyn_env = getenv("PTX_TRACE_DYN") ? atoi(getenv("PTX_TRACE_DYN")) : -1;
+            const bool use_dyn = dyn_env == 1 || (dyn_env != 0 && whole_band_sequences(h));
+            part.dyn = !use_dyn ? nullptr
                                : (uint32_t *)h->d_wctr.p + 2u * kWaveMaxRounds * ws.cnt_stride +
                                      (uint32_t)((set * ptx_handle::kMaxSplit + q) * kWaveMaxRounds) * kDynRoundWords;
             part.seg_base = (uint32_t)((uint64_t)ws.nseg * q / k);
@@ -569,10 +575,24 @@ void mark_history(ptx_handle *h) {
 }
 
 // ---------------------------------------------------------------- frame pipelining
+// Frames whose passes run as whole-band launch sequences: pipelined frames, or the same
+// handle timed launch by launch (PTX_FLAG_TIME_LAUNCHES + SINGLE_STREAM, bench.py's roofline
+// region), so both run the same trace kernel mode
+static bool whole_band_sequences(const ptx_handle *h) {
+    const uint32_t fl = h->cfg.flags;
+    const bool timed_alone = (fl & PTX_FLAG_TIME_LAUNCHES) && (fl & PTX_FLAG_SINGLE_STREAM);
+    return (h->alt_stream && pipelined(h)) ||
+           (timed_alone && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !h->comm && !h->halo_top && !h->halo_bot &&
+            (size_t)h->band_h * h->cfg.width <= ((size_t)4u << 20));
+}
 bool pipelined(const ptx_handle *h) {
     static const bool off = getenv("PTX_PIPELINE_FRAMES") && atoi(getenv("PTX_PIPELINE_FRAMES")) == 0;  // A/B
     const uint32_t fl = h->cfg.flags;
+    // at most ~4 Mpx per frame: a 3840x2160 frame's launches are large enough to fill the chip
+    // on their own (configs[3] on one GPU: 384 Msamples/s unpipelined, 355 pipelined)
+    const size_t px = (size_t)h->band_h * h->cfg.width;
     return !off && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !h->comm && !h->halo_top && !h->halo_bot &&
+           px <= (size_t)4u << 20 &&
            !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE | PTX_FLAG_COUNT_WORK |
                    PTX_FLAG_TIME_LAUNCHES | PTX_FLAG_SINGLE_STREAM | PTX_FLAG_ROW_CENSUS)) &&
            (h->alt_active ? h->stream == h->alt_stream : h->stream == h->own_stream);

@@ -557,13 +557,21 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     return best;
 }
 // Sub-root and instance tables staged in LDS when they fit: every ray tests every root of
-// every instance, ~16 table reads per query otherwise paid as scalar-load round trips.
-// Called by all threads of the workgroup (ends with a barrier).
-constexpr uint32_t kLdsSubs = 128, kLdsInsts = 8;
-__host__ __device__ __forceinline__ bool tables_fit_lds(const Scene &sc) {
-    return sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts;
+// every instance, ~16 table reads per query otherwise paid as scalar-load round trips.  The
+// tables sit at the start of the kernel's dynamic LDS, sized to the scene (32 B per sub-mesh
+// root, 144 B per instance) up to kLdsTableMax: ~700 sub-meshes, or 100 furnished instances
+// of a few sub-meshes each.  Larger scenes read the global tables.
+constexpr uint32_t kLdsTableMax = 24576u;
+__host__ __device__ __forceinline__ uint32_t tables_lds_bytes(const Scene &sc) {
+    return ((sc.n_subs * (uint32_t)sizeof(SubRoot) + 15u) & ~15u) + sc.n_inst * (uint32_t)sizeof(Inst);
 }
-__device__ __forceinline__ void stage_tables(const Scene &sc, SubRoot *l_subs, Inst *l_insts) {
+__host__ __device__ __forceinline__ bool tables_fit_lds(const Scene &sc) { return tables_lds_bytes(sc) <= kLdsTableMax; }
+struct LdsTables { const SubRoot *subs; const Inst *insts; };
+// Copies the tables to `lds` (16-byte aligned dynamic LDS); called by every thread of the
+// workgroup (ends with a barrier).  Returns the LDS tables.
+__device__ __forceinline__ LdsTables stage_tables(const Scene &sc, uint32_t *lds) {
+    SubRoot *l_subs = reinterpret_cast<SubRoot *>(lds);
+    Inst *l_insts = reinterpret_cast<Inst *>(lds + ((sc.n_subs * (uint32_t)sizeof(SubRoot) + 15u) & ~15u) / 4u);
     const uint32_t *gs = reinterpret_cast<const uint32_t *>(sc.subs);
     uint32_t *ls = reinterpret_cast<uint32_t *>(l_subs);
     for (uint32_t i = threadIdx.x; i < sc.n_subs * (uint32_t)(sizeof(SubRoot) / 4u); i += blockDim.x) ls[i] = gs[i];
@@ -571,6 +579,7 @@ __device__ __forceinline__ void stage_tables(const Scene &sc, SubRoot *l_subs, I
     uint32_t *li = reinterpret_cast<uint32_t *>(l_insts);
     for (uint32_t i = threadIdx.x; i < sc.n_inst * (uint32_t)(sizeof(Inst) / 4u); i += blockDim.x) li[i] = gi[i];
     __syncthreads();
+    return LdsTables{l_subs, l_insts};
 }
 
 template <bool COUNT, bool PROF = false>

@@ -27,7 +27,7 @@ __device__ __forceinline__ size_t band_index(const Scene &sc, uint32_t x, uint32
     return (size_t)(y - sc.row_begin) * sc.width + x;
 }
 
-extern __shared__ uint32_t lds_stack[];
+extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
 
 // GenerateRayFromThreadID (SH/PT_01_GBufferPass.wgsl:496-507)
 __device__ __forceinline__ Ray camera_ray(const Scene &sc, uint32_t x, uint32_t y) {
@@ -72,15 +72,14 @@ __device__ __forceinline__ void write_color(const Scene &sc, float4 *accum, size
 // =========================================================================== PT_01
 template <bool COUNT, bool LDS_TABLES = false>
 __global__ __launch_bounds__(BLOCK) void gbuffer_kernel(Scene sc, uint4 *gbuf) {
-    __shared__ SubRoot l_subs[LDS_TABLES ? kLdsSubs : 1];
-    __shared__ Inst l_insts[LDS_TABLES ? kLdsInsts : 1];
-    if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
+    // dynamic LDS: [scene tables (LDS_TABLES)] [stacks]
+    const LdsTables T = LDS_TABLES ? stage_tables(sc, lds_stack) : LdsTables{sc.subs, sc.insts};
     uint32_t x, y;
     if (!pixel_of(sc, x, y)) return;
     if (COUNT && sc.census) sc.counters = sc.census + (size_t)kCensusWords * ((y - sc.row_begin) / 8u);  // row census
-    uint32_t *stack = lds_stack + threadIdx.x;
-    Hit h = trace_core_tab<COUNT, false, false>(sc, LDS_TABLES ? l_subs : sc.subs, LDS_TABLES ? l_insts : sc.insts,
-                                  camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f}, stack, BLOCK);
+    uint32_t *stack = lds_stack + (LDS_TABLES ? tables_lds_bytes(sc) / 4u : 0u) + threadIdx.x;
+    Hit h = trace_core_tab<COUNT, false, false>(sc, T.subs, T.insts, camera_ray(sc, x, y), PassEps{1e-8f, 1e-6f},
+                                                stack, BLOCK);
     Compact s = h.s;
     s.valid = h.valid ? 1u : 0u;
     gbuf[band_index(sc, x, y)] = encode(s);
@@ -339,11 +338,12 @@ static dim3 grid_of(const Scene &sc) {
     return dim3((sc.width + TILE - 1) / TILE, (sc.row_end - sc.row_begin + TILE - 1) / TILE, 1);
 }
 hipError_t launch_gbuffer(const Scene &sc, uint4 *gbuf, uint32_t depth, hipStream_t s) {
-    const bool tables_fit = sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts;
+    const bool tables_fit = tables_fit_lds(sc);
     if (sc.counters)
         hipLaunchKernelGGL(gbuffer_kernel<true>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
     else if (tables_fit)
-        hipLaunchKernelGGL((gbuffer_kernel<false, true>), grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
+        hipLaunchKernelGGL((gbuffer_kernel<false, true>), grid_of(sc), dim3(BLOCK),
+                           tables_lds_bytes(sc) + stack_lds_bytes(depth), s, sc, gbuf);
     else
         hipLaunchKernelGGL(gbuffer_kernel<false>, grid_of(sc), dim3(BLOCK), stack_lds_bytes(depth), s, sc, gbuf);
     return hipGetLastError();

@@ -125,21 +125,21 @@ template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true, bool
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     PTX_WAVE_TIMER(sc, KID_TRACE);
-    extern __shared__ uint32_t wstack[];
+    // dynamic LDS: [scene tables (LDS_TABLES)] [batch prefix (dynamic batches)] [stacks]
+    extern __shared__ __attribute__((aligned(16))) uint32_t wstack[];
     const bool dyn = !COUNT && w.dyn != nullptr;
-    uint32_t *pref = wstack;                                                // dyn: batch prefix
-    uint32_t *stack = wstack + (dyn ? dyn_prefix_words(w) : 0u) + threadIdx.x;  // then the stacks
-    __shared__ SubRoot l_subs[LDS_TABLES ? kLdsSubs : 1];
-    __shared__ Inst l_insts[LDS_TABLES ? kLdsInsts : 1];
+    const uint32_t tw = LDS_TABLES ? tables_lds_bytes(sc) / 4u : 0u;
+    uint32_t *pref = wstack + tw;
+    uint32_t *stack = wstack + tw + (dyn ? dyn_prefix_words(w) : 0u) + threadIdx.x;
     __shared__ unsigned long long c_key[WB];
     const CoopLds coop{c_key + (threadIdx.x & ~63u)};
     if (dyn) {
         dyn_prefix(w, round, pref);
         const uint32_t total = pref[w.seg_count];
         if (blockIdx.x * (WB / 64u) >= total) return;  // (workgroup-uniform) more waves than batches
-        if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
-        const SubRoot *subs = LDS_TABLES ? l_subs : sc.subs;
-        const Inst *insts = LDS_TABLES ? l_insts : sc.insts;
+        const LdsTables T = LDS_TABLES ? stage_tables(sc, wstack) : LdsTables{sc.subs, sc.insts};
+        const SubRoot *subs = T.subs;
+        const Inst *insts = T.insts;
         // the batch list in kDynHeads contiguous chunks, chunk x dequeued through head x by the
         // waves of XCD x (workgroups are dealt to the XCDs round-robin: block b on XCD b % 8);
         // a wave whose chunk is drained moves on to the next one
@@ -195,9 +195,9 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     const uint32_t j = w.seg_phys + w.seg_base + local;  // physical queue slot
     const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
     if (share * WB >= n) return;  // (workgroup-uniform) nothing for this share
-    if (LDS_TABLES) stage_tables(sc, l_subs, l_insts);
-    const SubRoot *subs = LDS_TABLES ? l_subs : sc.subs;
-    const Inst *insts = LDS_TABLES ? l_insts : sc.insts;
+    const LdsTables T = LDS_TABLES ? stage_tables(sc, wstack) : LdsTables{sc.subs, sc.insts};
+    const SubRoot *subs = T.subs;
+    const Inst *insts = T.insts;
     if (COUNT && sc.census)  // row census: this slot's queries count into its own block
         sc.counters = sc.census + (size_t)kCensusWords * ((sc.row_end - sc.row_begin + 7u) / 8u + j);
     const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
@@ -222,7 +222,7 @@ template <bool COUNT>
 __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *rays_all, float4 *res_all,
                                                      const uint32_t *cnt, uint32_t stride, uint32_t n_total,
                                                      PassEps eps) {
-    extern __shared__ uint32_t wstack[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t wstack[];
     uint32_t *stack = wstack + threadIdx.x;
     const uint32_t j = blockIdx.x;
     const bool pub = cnt == nullptr;
@@ -390,11 +390,9 @@ __global__ __launch_bounds__(WB) void trace_queue_sm(Scene sc, const float4 *ray
 template <bool ROOTQ>
 __global__ __launch_bounds__(WB) void wgbuffer(Scene sc, WaveBufs w, uint4 *gbuf) {
     PTX_WAVE_TIMER(sc, KID_GBUF);
-    extern __shared__ uint32_t wstack[];
-    uint32_t *stack = wstack + threadIdx.x;
-    __shared__ SubRoot l_subs[kLdsSubs];
-    __shared__ Inst l_insts[kLdsInsts];
-    stage_tables(sc, l_subs, l_insts);
+    extern __shared__ __attribute__((aligned(16))) uint32_t wstack[];  // [scene tables] [stacks]
+    uint32_t *stack = wstack + tables_lds_bytes(sc) / 4u + threadIdx.x;
+    const LdsTables T = stage_tables(sc, wstack);
     // The group's pixels are the tiles t = m * nseg + r, r in [seg_base, seg_base + seg_count)
     // (seg_pixel's layout, cluster 1); walking them in raster order gives each workgroup 4
     // adjacent tiles (a 32x8 strip) -- primary rays of one CU then share BVH nodes in L1.
@@ -408,7 +406,7 @@ __global__ __launch_bounds__(WB) void wgbuffer(Scene sc, WaveBufs w, uint4 *gbuf
     const float v = ((float)y + 0.5f) / (float)sc.U[U_H];
     const f3 st = xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
     const f3 en = xform_point(vpinv, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f + 1.0f));
-    const Hit h = trace_core_tab<false, false, ROOTQ>(sc, l_subs, l_insts, Ray{st, normalize(en - st)},
+    const Hit h = trace_core_tab<false, false, ROOTQ>(sc, T.subs, T.insts, Ray{st, normalize(en - st)},
                                                       PassEps{1e-8f, 1e-6f}, stack, WB);
     Compact c = h.s;
     c.valid = h.valid ? 1u : 0u;
@@ -1035,8 +1033,10 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
         static const uint32_t g = getenv("PTX_TRACE_DYN_G") ? (uint32_t)atoi(getenv("PTX_TRACE_DYN_G")) : 0u;
         w.trace_split = g >= 1u && g <= 16u ? g : 1u;
     }
-    const size_t lds = stack_lds_bytes(depth) + (w.dyn ? 4u * (size_t)((w.seg_count + 4u) & ~3u) : 0u);
-    if (occ_only && sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts) {  // occlusion rounds (GI spatial)
+    // dynamic LDS: scene tables (the LDS-table variants) + batch prefix (dynamic batches) + stacks
+    const size_t lds = (tables_fit_lds(sc) ? tables_lds_bytes(sc) : 0u) +
+                       (w.dyn ? 4u * (size_t)((w.seg_count + 4u) & ~3u) : 0u) + stack_lds_bytes(depth);
+    if (occ_only && tables_fit_lds(sc)) {  // occlusion rounds (GI spatial)
         if (sc.counters)
             hipLaunchKernelGGL((trace_queue<true, 6, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
                                (uint32_t)round, eps);
@@ -1071,7 +1071,7 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
         // (+1.7 % over 4); 6+ spills in the traversal loop.
         static const int env_occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 0;
         const int occ = env_occ ? env_occ : w.trace_waves == 4u ? 4 : 5;
-        const bool tables_fit = sc.n_subs <= kLdsSubs && sc.n_inst <= kLdsInsts && !getenv("PTX_TRACE_NOLDS");
+        const bool tables_fit = tables_fit_lds(sc) && !getenv("PTX_TRACE_NOLDS");
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
                  : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
                  : occ == 6  ? trace_queue<false, 6> : occ == 5 ? trace_queue<false, 5> : trace_queue<false, 4>;
@@ -1100,10 +1100,12 @@ hipError_t wave_gbuffer(const Scene &sc, const WaveBufs &w, uint4 *gbuf, uint32_
     if (!tables_fit_lds(sc)) return hipErrorInvalidValue;  // caller falls back to gbuffer_kernel
     static const bool rootq = getenv("PTX_GBUF_ROOTQ") != nullptr;  // A/B
     if (rootq)
-        hipLaunchKernelGGL(wgbuffer<true>, dim3(w.seg_px / WB * w.seg_count), dim3(WB), stack_lds_bytes(depth), s, sc,
+        hipLaunchKernelGGL(wgbuffer<true>, dim3(w.seg_px / WB * w.seg_count), dim3(WB),
+                           tables_lds_bytes(sc) + stack_lds_bytes(depth), s, sc,
                            w, gbuf);
     else
-        hipLaunchKernelGGL(wgbuffer<false>, dim3(w.seg_px / WB * w.seg_count), dim3(WB), stack_lds_bytes(depth), s,
+        hipLaunchKernelGGL(wgbuffer<false>, dim3(w.seg_px / WB * w.seg_count), dim3(WB),
+                           tables_lds_bytes(sc) + stack_lds_bytes(depth), s,
                            sc, w, gbuf);
     return hipGetLastError();
 }

@@ -182,3 +182,23 @@ def test_gi_bands_with_halo_exchange_gloo(tmp_path, world, scene3, oracle_mod):
     got = np.concatenate([np.load(out % r) for r in range(world)], axis=0)
     assert (got[..., 4 + 11] > 1).any()  # the history took part
     np.testing.assert_array_equal(got, full)
+
+
+def test_c4_cost_balanced_bands_within_ten_percent(scene3, oracle_mod):
+    """configs[3] (C3 at 3840x2160 over 8 GPUs): bands cut from a work census of the frame
+    (bands.row_costs + balanced_bands, what bench.py does with the GPU census) have a
+    predicted max/mean cost <= 1.1, where equal-height bands of the same frame do not.  The
+    census here is the CPU oracle's (run_reuse_frame_census) on the same camera at 960x540,
+    resampled onto the 2160 rows (row_costs); the band predicate is the §8(d) cost model."""
+    from pathtracerdemo_amd import bands as B
+    from helpers import uniform_for
+    O = oracle_mod
+    fr = O.Frame(uniform_for(scene3, 960, 540, 1), scene3.scene, scene3.geometry, scene3.accel)
+    tiles = fr.run_reuse_frame_census(threads=8)
+    costs = B.row_costs(tiles, 3840, 2160)
+    bal = B.balanced_bands(costs, 8, min_rows=30)
+    equal = [B.band(2160, 8, r) for r in range(8)]
+    got, eq = B.band_balance(costs, bal), B.band_balance(costs, equal)
+    assert got <= 1.1, (got, bal)
+    assert eq > got
+    assert all(e - b >= 30 for b, e in bal) and bal[0][0] == 0 and bal[-1][1] == 2160
