@@ -17,6 +17,19 @@ for WL in ${WORKLOADS:-reuse restir mcpt gi}; do
   cp "$src/pmc_WRITE_SIZE/run_counter_collection.csv" "$dst/pmc_WRITE_SIZE/counter_collection.csv"
   cp "$src/bench_trace.log" "$dst/bench_under_rocprof.log"
   tail -n 1 "gpurun_out/bench_${ROUND}_$WL.log" > "$dst/bench_line.json"
-  python3 tools/hbm_traffic.py "$dst" "$WL:${SCENE[$WL]}:trace_queue:1920x1080" "trace_queue<false" > /dev/null
+  # the timed roofline symbol only (GI: the closest-hit instance, not the any-hit one)
+  KN="trace_queue<false, 4, false, true, false>"; [ "$WL" = "gi" ] && KN="trace_queue<false, 5, false, true, false>"
+  python3 tools/hbm_traffic.py "$dst" "$WL:${SCENE[$WL]}:trace_queue:1920x1080" "$KN" > /dev/null
+  # the bench line carries the PMC traffic of THIS build's passes (the bench ran first and
+  # looked up the previous entry)
+  python3 - "$dst" "$WL:${SCENE[$WL]}:trace_queue:1920x1080" <<'PY'
+import json, sys
+d, key = sys.argv[1], sys.argv[2]
+db = json.load(open("profiles/hbm_traffic.json"))
+line = json.load(open(f"{d}/bench_line.json"))
+line["roofline"]["traffic"] = db[key]["bytes_per_launch"]
+line["roofline"]["traffic_source"] = f"{db[key]['source']}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of the same bench command, 2*FETCH_SIZE + WRITE_SIZE per launch of {db[key].get('kernel', 'trace_queue')}"
+json.dump(line, open(f"{d}/bench_line.json", "w"))
+PY
   echo "$WL -> $dst"
 done

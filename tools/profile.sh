@@ -9,6 +9,10 @@ cd /tmp && export TMPDIR=/tmp
 # region (PTX_FLAG_SINGLE_STREAM); the two-stream production overlap is measured by the
 # bench's headline value, not by per-kernel averages
 export PTX_WAVE_STREAMS=${PTX_WAVE_STREAMS:-1}
+# one frame in flight (frame pipelining overlaps consecutive frames' kernels); the reuse
+# pipeline's whole-band sequences use the dynamic trace batches (PTX_TRACE_DYN=1 here makes
+# the production region run the same kernel mode as bench.py's launch-timed region)
+export PTX_PIPELINE_FRAMES=0
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
