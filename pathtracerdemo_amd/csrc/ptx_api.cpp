@@ -225,6 +225,7 @@ int build_layout(ptx_handle *h) {
     if ((size_t)h->stack_depth * kBlock * 4u > 160u * 1024u)
         return fail(h, PTX_E_SCENE, "BLAS depth %u needs more LDS than a CU has", max_depth);
     h->layout_valid = true;
+    h->surf_valid = h->alt.surf_valid = false;  // the surface records name the old layout's materials
     return PTX_OK;
 }
 
@@ -295,6 +296,13 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
         if (int rc = alloc_buf(h, h->d_wres0, cap * 32u)) return rc;
         if (int rc = alloc_buf(h, h->d_wres1, cap * 32u)) return rc;
         h->wave_ray_cap = cap;
+    }
+    w.surf = nullptr;
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE) {
+        const size_t rows = (size_t)h->halo_top + h->band_h + h->halo_bot;
+        if (h->d_surf.bytes != rows * h->cfg.width * 32u) h->surf_valid = false;
+        if (int rc = alloc_buf(h, h->d_surf, rows * h->cfg.width * 32u)) return rc;
+        w.surf = (uint4 *)h->d_surf.p + 2u * (size_t)h->halo_top * h->cfg.width;
     }
     w.state = (float4 *)h->d_wstate.p;
     w.npix = (uint32_t)npix;
@@ -373,6 +381,7 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.use_init = (pass == PTX_PASS_TEMPORAL && h->init_state_valid) ? 1u : 0u;
     A.nbr_out = (uint4 *)h->d_nbr.p + (size_t)h->halo_top * h->cfg.width;
     A.nbr = A.nbr_out;
+    A.surf = h->d_surf.p ? (const uint4 *)h->d_surf.p + 2u * (size_t)h->halo_top * h->cfg.width : nullptr;
     return A;
 }
 
@@ -466,16 +475,18 @@ hipError_t spatial_summaries(ptx_handle *h, hipStream_t st) {
     if (h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) return hipSuccess;  // GI gathers the buffers
     const size_t W = h->cfg.width, top = h->halo_top * W, band = (size_t)h->band_h * W;
     const uint4 *gb = (const uint4 *)h->d_gbuf.p, *rs = (const uint4 *)h->d_res.p;
-    uint4 *nb = (uint4 *)h->d_nbr.p;
+    uint4 *nb = (uint4 *)h->d_nbr.p, *sf = (uint4 *)h->d_surf.p;  // (halo rows: surface records too)
+    const Scene sc = make_scene(h);
     TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
     hipError_t e;
     if (!h->nbr_valid) {
-        e = wave_reuse_summary(gb, rs, nb, px_with_halo(h), st);
+        e = wave_reuse_summary(sc, gb, rs, nb, sf, px_with_halo(h), st);
     } else {
-        e = top ? wave_reuse_summary(gb, rs, nb, top, st) : hipSuccess;
+        e = top ? wave_reuse_summary(sc, gb, rs, nb, sf, top, st) : hipSuccess;
         const size_t b0 = top + band;
         if (e == hipSuccess && px_with_halo(h) > b0)
-            e = wave_reuse_summary(gb + b0, rs + 8u * b0, nb + b0, px_with_halo(h) - b0, st);
+            e = wave_reuse_summary(sc, gb + b0, rs + 8u * b0, nb + b0, sf ? sf + 2u * b0 : nullptr, px_with_halo(h) - b0,
+                                   st);
     }
     event_end(t, st);
     return e;
@@ -505,6 +516,19 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
             h->nbr_valid = false;  // G-buffer / PT_1 / MCPT rewrite what the summaries describe
         }
     }
+    // primary-hit surface records (DI reuse): PT_1 writes the band's; a reuse pass that finds
+    // them stale (G-buffer or scene changed since) computes them first, per launch sequence
+    bool need_surf[8] = {false};
+    bool surf_ok = h->surf_valid;
+    for (int i = 0; i < npasses && i < 8; ++i) {
+        if (passes[i] == PTX_PASS_GBUFFER) surf_ok = false;
+        else if (passes[i] == PTX_PASS_INIT && w.surf) surf_ok = true;
+        else if ((passes[i] == PTX_PASS_TEMPORAL || passes[i] == PTX_PASS_SPATIAL) && w.surf) {
+            need_surf[i] = !surf_ok;
+            surf_ok = true;
+        }
+    }
+    h->surf_valid = surf_ok && w.surf;
     if (k == 0) return hipSuccess;  // empty tile set
     if (k > 1) {
         if (!h->ev_fork && (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return e;
@@ -545,6 +569,12 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
                     h->init_state_valid = false;  // PT_1's state described the previous G-buffer
                     event_end(t, st);
                 } else {
+                    if (i < 8 && need_surf[i]) {
+                        TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
+                        e = wave_surface(sc, part, gbuf_band(h), st);
+                        event_end(t, st);
+                        if (e != hipSuccess) return e;
+                    }
                     e = launch_wave_seq(h, sc, part, passes[i], st);
                 }
                 if (e != hipSuccess) return e;
@@ -611,6 +641,7 @@ static void swap_frame_ctx(ptx_handle *h) {
     std::swap(h->d_gbuf, a.gbuf);
     std::swap(h->d_res, a.res);
     std::swap(h->d_nbr, a.nbr);
+    std::swap(h->d_surf, a.surf);
     std::swap(h->d_wstate, a.wstate);
     std::swap(h->d_wrays, a.wrays);
     std::swap(h->d_wres0, a.wres0);
@@ -628,6 +659,7 @@ static void swap_frame_ctx(ptx_handle *h) {
     std::swap(h->ev_fork, a.ev_fork);
     std::swap(h->init_state_valid, a.init_state_valid);
     std::swap(h->nbr_valid, a.nbr_valid);
+    std::swap(h->surf_valid, a.surf_valid);
     h->alt_active = !h->alt_active;
 }
 // the second context's G-buffer, reservoirs and stream (its queues, wave state and summaries
@@ -768,6 +800,7 @@ static int timed_launch(ptx_handle *h, int pass) {
         e = launch_gbuffer(sc, gbuf_band(h), d, h->stream);
         h->init_state_valid = false;
         h->nbr_valid = false;
+        h->surf_valid = false;
         break;
     case PTX_PASS_INIT:
         e = variant == 0   ? launch_init_tiled(sc, gb, res, d, h->stream)
@@ -915,6 +948,7 @@ int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const
     h->hist_valid = false;
     h->init_state_valid = false;
     h->nbr_valid = false;
+    h->surf_valid = h->alt.surf_valid = false;
     if (h->frame_set) return build_layout(h);
     return PTX_OK;
 }
@@ -1103,7 +1137,7 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
     out->max_bvh_depth = h->max_depth;
     out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
                         h->d_subs.bytes + h->d_insts.bytes + h->d_mats.bytes + h->d_tverts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
-                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_nbr.bytes + h->d_direct.bytes;
+                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_nbr.bytes + h->d_surf.bytes + h->d_direct.bytes;
     return PTX_OK;
 }
 
@@ -1185,6 +1219,7 @@ int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t byte
     HIP_CHECK(h, hipMemcpy(b.p, host_src, bytes, hipMemcpyHostToDevice));
     h->init_state_valid = false;  // the wave state no longer matches the buffers
     h->nbr_valid = false;
+    h->surf_valid = false;  // (a G-buffer write: the surface records describe the old one)
     return PTX_OK;
 }
 
@@ -1257,10 +1292,10 @@ int ptx_destroy(ptx_handle *h) {
     for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
-                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_direct, &h->d_census})
+                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_surf, &h->d_direct, &h->d_census})
         free_buf(*b);
     ptx_handle::FrameCtx &a = h->alt;
-    for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wact0, &a.wact1, &a.wctr})
+    for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wact0, &a.wact1, &a.wctr})
         free_buf(*b);
     if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

@@ -60,6 +60,11 @@ struct ptx_handle {
     // d_nbr holds the summaries of the band's reservoirs as the temporal pass left them
     // (set by that pass, dropped by anything else that rewrites G-buffer or reservoirs)
     bool nbr_valid = false;
+    // DI reuse pipeline: primary-hit surface records of the band (+ halo rows), 32 B per pixel
+    // (WaveBufs::surf); surf_valid: the band rows describe the current G-buffer and scene (PT_1
+    // wrote them; a reuse pass runs wsurface first otherwise; halo rows come with the summaries)
+    DevBuf d_surf;
+    bool surf_valid = false;
     uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
     bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
     uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
@@ -87,13 +92,13 @@ struct ptx_handle {
     // ptx_render swaps the members above with `alt` per frame, so everything else always sees
     // the latest frame's buffers; the shared ones (accumulation, history, jobs, scene) never move.
     struct FrameCtx {
-        DevBuf gbuf, res, nbr, wstate, wrays, wres0, wres1, wact0, wact1, wctr;
+        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wact0, wact1, wctr;
         size_t wave_ray_cap = 0;
         uint32_t wave_slots = 0;
         hipStream_t stream = nullptr;
         hipStream_t sub[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
         hipEvent_t ev_fork = nullptr, ev_join[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
-        bool init_state_valid = false, nbr_valid = false;
+        bool init_state_valid = false, nbr_valid = false, surf_valid = false;
     } alt;
     bool alt_active = false;      // the members above hold the second context (stream == alt stream)
     hipStream_t alt_stream = nullptr;  // the second context's stream (owned)

@@ -86,6 +86,9 @@ struct WaveBufs {
     // kDynHeads dequeue heads (round r at dyn + r * kDynRoundWords; the logic round that emits
     // trace round r zeroes them in seg_begin); nullptr = one slot per trace workgroup.
     uint32_t *dyn;
+    // DI reuse pipeline: primary-hit surface records (2 uint4 per pixel, first band row; halo
+    // rows at negative / >= npix indices), written by winit_start; nullptr otherwise
+    uint4 *surf;
 };
 // occ_only: every query of the round is Q_OCC (any-hit kernel instance)
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t stack_depth,
@@ -112,6 +115,7 @@ struct ReuseArgs {
     uint32_t use_init;  // temporal: this frame's PT_1 wave state (path hits, NEE Visibility) is in w.state
     const uint4 *nbr;   // spatial: per-pixel neighbour summary (wave_reuse_summary), cur's addressing
     uint4 *nbr_out;     // the same buffer: the temporal pass writes its output's summaries
+    const uint4 *surf;  // primary-hit surface records (WaveBufs::surf), cur's addressing
 };
 // rounds of {trace, step} between a reuse pass's start and combine launches
 int reuse_rounds(int pass_temporal, const ReuseArgs &A);
@@ -120,7 +124,12 @@ hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_tempora
 // Spatial pass prologue over every band + halo pixel (npx of them, from the first halo row):
 // the 16-byte neighbour summary {p_hat, q, W, valid | length | C} the spatial kernels gather
 // instead of a G-buffer line and a reservoir line per neighbour.
-hipError_t wave_reuse_summary(const uint4 *gbuf, const uint4 *res, uint4 *nbr, size_t npx, hipStream_t s);
+// With `surf`, the same pixels' primary-hit surface records too (halo rows just received).
+hipError_t wave_reuse_summary(const Scene &sc, const uint4 *gbuf, const uint4 *res, uint4 *nbr, uint4 *surf,
+                              size_t npx, hipStream_t s);
+// The surface records of the launch's segments from the G-buffer (a reuse pass whose band
+// records are stale: no PT_1 since the G-buffer or the scene changed)
+hipError_t wave_surface(const Scene &sc, const WaveBufs &w, const uint4 *gbuf, hipStream_t s);
 
 // ReSTIR GI (ptx_gi.hip; pipeline PTX_PIPELINE_RESTIR_GI): pass 0 init (logic rounds 0..2,
 // traces between), 1 temporal (one launch), 2 spatial (start, trace, combine), 3 final.

@@ -83,19 +83,27 @@ __device__ __forceinline__ bool rr_step(Job &s, const Surface &X, f3 V, f3 L, fl
     return ok;
 }
 
-// Job at domain pixel (x, y) with G-buffer hit x1, sample `ref`: false if eval_sample's
-// preconditions fail (no job; its result is invalid).
+// A fresh job: sample `ref` (length >= 2) replayed from the domain's camera point x0 and
+// primary-hit surface X1 (flat material index matref).
+__device__ __forceinline__ void job_init(Job &s, f3 x0, const Surface &X1, uint32_t matref, int32_t ref,
+                                         uint32_t length, uint32_t seed1) {
+    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = seed1; s.idx = 0u; s.ref = ref;
+    s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
+    s.prev = x0;
+    s.cur = X1;
+    s.matref = matref;
+    s.beta = 1.0f; s.rr_p = 1.0f; s.rr_f = mk(1.0f, 1.0f, 1.0f);
+}
+// Job at domain pixel (x, y) (band index dom, its surface record), sample `ref`: false if
+// eval_sample's preconditions fail (no job; its result is invalid).
 __device__ __forceinline__ bool job_begin(const Scene &sc, const ReuseArgs &A, Job &s, uint32_t x, uint32_t y,
-                                          const Compact &x1, int32_t ref) {
+                                          int32_t dom, int32_t ref) {
     const uint4 *rv = res_at(A.cur, ref);
     const uint32_t C = rv[7].y, length = rv[5].w;
-    if (!x1.valid || C == 0u || length < 2u) return false;
-    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = rv[0].y; s.idx = 0u; s.ref = ref;
-    s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
-    s.prev = x0_of(sc, x, y);
-    s.cur = get_surface(sc, x1);
-    s.matref = mat_index(sc, x1.inst, x1.mat);
-    s.beta = 1.0f; s.rr_p = 1.0f; s.rr_f = mk(1.0f, 1.0f, 1.0f);
+    Surface X1;
+    uint32_t matref;
+    if (C == 0u || length < 2u || !surf_load(sc, A.surf, dom, X1, matref)) return false;
+    job_init(s, x0_of(sc, x, y), X1, matref, ref, length, rv[0].y);
     return true;
 }
 
@@ -293,7 +301,7 @@ void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
         Job s;
         if (q < np && tile_xy(sc, q, x, y)) {
             pix = (y - sc.row_begin) * sc.width + x;
-            active = job_begin(sc, A, s, x, y, gdecode(A.gbuf[pix]), (int32_t)pix);
+            active = job_begin(sc, A, s, x, y, (int32_t)pix, (int32_t)pix);
             if (active && A.use_init) active = temporal_from_init(sc, w, A, s, pix);
         }
         const bool live = job_emit(sc, g, A, active, s, pix);
@@ -375,30 +383,38 @@ __device__ __forceinline__ Nbr nbr_at(const ReuseArgs &A, int32_t idx) {
     const uint4 r5 = rv[5], r6 = rv[6], r7 = rv[7];
     return Nbr{gdecode(A.gbuf[idx]).valid != 0u, r5.w, r7.y, asf(r6.x), asf(r6.y), asf(r7.x)};
 }
-__global__ __launch_bounds__(WB) void wnbr_summary(const uint4 *gbuf, const uint4 *res, uint4 *nbr, size_t npx) {
+__global__ __launch_bounds__(WB) void wnbr_summary(Scene sc, const uint4 *gbuf, const uint4 *res, uint4 *nbr,
+                                                   uint4 *surf, size_t npx) {
     const size_t i = (size_t)blockIdx.x * WB + threadIdx.x;
     if (i >= npx) return;
     const uint4 *rv = res + 8u * i;
-    nbr[i] = nbr_pack((gbuf[i].x >> 31) != 0u, rv[5], rv[6], rv[7]);
+    const uint4 g = gbuf[i];
+    nbr[i] = nbr_pack((g.x >> 31) != 0u, rv[5], rv[6], rv[7]);
+    if (surf) surf_from_gbuf(sc, surf, (ptrdiff_t)i, g);
 }
-hipError_t wave_reuse_summary(const uint4 *gbuf, const uint4 *res, uint4 *nbr, size_t npx, hipStream_t s) {
+hipError_t wave_reuse_summary(const Scene &sc, const uint4 *gbuf, const uint4 *res, uint4 *nbr, uint4 *surf,
+                              size_t npx, hipStream_t s) {
     if (npx == 0) return hipSuccess;
-    hipLaunchKernelGGL(wnbr_summary, dim3((unsigned)((npx + WB - 1) / WB)), dim3(WB), 0, s, gbuf, res, nbr, npx);
+    hipLaunchKernelGGL(wnbr_summary, dim3((unsigned)((npx + WB - 1) / WB)), dim3(WB), 0, s, sc, gbuf, res, nbr, surf,
+                       npx);
     return hipGetLastError();
 }
 
-// job_begin with the domain's camera point and hit surface and the sample's summary at hand
-__device__ __forceinline__ bool job_begin_at(const Scene &sc, const ReuseArgs &A, Job &s, f3 x0, const Surface &X1,
-                                             const Compact &x1, int32_t ref, const Nbr &nb) {
-    const uint32_t C = nb.C, length = nb.length;
-    if (!x1.valid || C == 0u || length < 2u) return false;
-    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = res_at(A.cur, ref)[0].y; s.idx = 0u; s.ref = ref;
-    s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
-    s.prev = x0;
-    s.cur = X1;
-    s.matref = mat_index(sc, x1.inst, x1.mat);
-    s.beta = 1.0f; s.rr_p = 1.0f; s.rr_f = mk(1.0f, 1.0f, 1.0f);
-    return true;
+// The surface records of the launch's segments (WaveBufs::surf) from the G-buffer.
+__global__ __launch_bounds__(WB) void wsurface(Scene sc, WaveBufs w, const uint4 *gbuf) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        surf_from_gbuf(sc, w.surf, (ptrdiff_t)pix, gbuf[pix]);
+    }
+}
+hipError_t wave_surface(const Scene &sc, const WaveBufs &w, const uint4 *gbuf, hipStream_t s) {
+    if (!w.surf || !w.seg_count) return hipSuccess;
+    hipLaunchKernelGGL(wsurface, dim3(w.seg_count), dim3(WB), 0, s, sc, w, gbuf);
+    return hipGetLastError();
 }
 
 // One thread per (pixel, kind): the forward shifts (slots 2m: neighbour m's sample in this
@@ -419,24 +435,27 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
     for (uint32_t base = 0; base < w.seg_px * 2u; base += WB) {  // workgroup-uniform
         const bool backward = base >= w.seg_px;
         const uint32_t q = seg_pixel(w, g.j, base % w.seg_px);
-        uint32_t x = 0u, y = 0u, pix = 0u, seed = 0u;
-        Compact x1{};
+        uint32_t x = 0u, y = 0u, pix = 0u, seed = 0u, mref = 0u;
+        bool valid = false, canon = false;
         Surface X1{};
         f3 x0{};
         if (q < np && tile_xy(sc, q, x, y)) {
             pix = (y - sc.row_begin) * sc.width + x;
-            x1 = gdecode(A.gbuf[pix]);
             seed = reuse_seed(sc, x, y, SALT_SPATIAL);
-            if (x1.valid && !backward) {
-                X1 = get_surface(sc, x1);
-                x0 = x0_of(sc, x, y);
+            if (!backward) {
+                valid = surf_load(sc, A.surf, pix, X1, mref);
+                if (valid) x0 = x0_of(sc, x, y);
+            } else {
+                valid = A.surf[2u * (size_t)pix].w != kNoSurface;
+                const uint4 *rc = A.cur + 8u * (size_t)pix;  // this pixel's sample, shifted to each neighbour
+                canon = valid && rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
             }
         }
         for (uint32_t m = 0; m < A.neighbors; ++m) {  // uniform
             const uint32_t jid = pix * jpp + 2u * m + (backward ? 1u : 0u);
             bool act = false;
             Job s;
-            if (x1.valid) {
+            if (valid) {
                 uint32_t nx = 0u, ny = 0u;
                 bool present = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
                 const int32_t nidx = present ? band_index(sc, nx, ny) : 0;
@@ -444,12 +463,17 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 if (present && !backward) {  // the neighbour's sample in this pixel's domain
                     const Nbr nb = nbr_at(A, nidx);
                     want = nb.valid && nb.length >= 2u && nb.p > 0.0f;
-                    act = want && job_begin_at(sc, A, s, x0, X1, x1, nidx, nb);
-                } else if (present) {  // this pixel's sample in the neighbour's domain
-                    const Compact xn = gdecode(A.gbuf[nidx]);
-                    const uint4 *rc = A.cur + 8u * (size_t)pix;
-                    want = xn.valid && rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
-                    act = want && job_begin(sc, A, s, nx, ny, xn, (int32_t)pix);
+                    act = want && nb.C != 0u;
+                    if (act) job_init(s, x0, X1, mref, nidx, nb.length, res_at(A.cur, nidx)[0].y);
+                } else if (present && canon) {  // this pixel's sample in the neighbour's domain
+                    Surface Xn;
+                    uint32_t nref;
+                    want = surf_load(sc, A.surf, nidx, Xn, nref);
+                    if (want) {
+                        act = true;
+                        job_init(s, x0_of(sc, nx, ny), Xn, nref, (int32_t)pix, A.cur[8u * (size_t)pix + 5u].w,
+                                 A.cur[8u * (size_t)pix].y);
+                    }
                 }
                 if (want && !act) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }

@@ -581,6 +581,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
             if (!x1.valid) {  // reservoir unobservable: PT_4 returns before LoadReservoir (:1404-1408)
                 uint4 *out = reservoir + 8u * (size_t)pix;
                 for (int q8 = 0; q8 < 8; ++q8) out[q8] = make_uint4(0u, 0u, 0u, 0u);
+                if (w.surf) surf_store_none(w.surf, pix);
             } else {
                 active = true;
                 s.seed = pcg(x * 1973u + y * 9277u + sc.U[U_FRAME] * 26699u);
@@ -590,6 +591,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                 s.L = mk(0.0f, 0.0f, 0.0f); s.bseed1 = 0u; s.bseed2 = 0u; s.bsdf_idx = 0u;
                 prev = x0_of(sc, x, y);
                 X = get_surface(sc, x1);
+                if (w.surf) surf_store(w.surf, pix, X, mat_index(sc, x1.inst, x1.mat));  // for the reuse passes
                 if (X.mat.rough >= RECONNECTION_ROUGHNESS) s.flags |= F_R1;
             }
         }

@@ -175,6 +175,39 @@ __device__ __forceinline__ uint32_t padded_pixels(const Scene &sc) {
     return ((sc.width + 7u) / 8u) * ((sc.row_end - sc.row_begin + 7u) / 8u) * 64u;
 }
 
+// Primary-hit surface records (DI reuse pipeline, WaveBufs::surf / ReuseArgs::surf): per band
+// (+ halo) pixel, GetSurface of its G-buffer hit -- {pos, flat material index}, {normal, 0} --
+// written once per frame by PT_1's start kernel (which computes it anyway) or wsurface, and
+// gathered by the temporal / spatial shift jobs instead of recomputing it (an 80-byte vertex
+// record, the instance transform and a normalize) for every job of every domain.  Same bits
+// as get_surface: the record is its output.  kNoSurface: the G-buffer has no hit there.
+constexpr uint32_t kNoSurface = 0xFFFFFFFFu;
+__device__ __forceinline__ void surf_store(uint4 *surf, ptrdiff_t i, const Surface &X, uint32_t matref) {
+    surf[2 * i] = make_uint4(asu(X.pos.x), asu(X.pos.y), asu(X.pos.z), matref);
+    surf[2 * i + 1] = make_uint4(asu(X.nrm.x), asu(X.nrm.y), asu(X.nrm.z), 0u);
+}
+__device__ __forceinline__ void surf_store_none(uint4 *surf, ptrdiff_t i) {
+    surf[2 * i] = make_uint4(0u, 0u, 0u, kNoSurface);
+}
+// the record of band pixel i; false (X untouched) when the pixel has no G-buffer hit
+__device__ __forceinline__ bool surf_load(const Scene &sc, const uint4 *surf, ptrdiff_t i, Surface &X,
+                                          uint32_t &matref) {
+    const uint4 a = surf[2 * i];
+    if (a.w == kNoSurface) return false;
+    const uint4 b = surf[2 * i + 1];
+    X.pos = mk(asf(a.x), asf(a.y), asf(a.z));
+    X.nrm = mk(asf(b.x), asf(b.y), asf(b.z));
+    X.mat = material_at(sc, a.w);
+    matref = a.w;
+    return true;
+}
+// GetSurface of a G-buffer texel into the record (wsurface, halo rows of wnbr_summary)
+__device__ __forceinline__ void surf_from_gbuf(const Scene &sc, uint4 *surf, ptrdiff_t i, uint4 g) {
+    const Compact x1 = gdecode(g);
+    if (!x1.valid) surf_store_none(surf, i);
+    else surf_store(surf, i, get_surface(sc, x1), mat_index(sc, x1.inst, x1.mat));
+}
+
 __device__ __forceinline__ LightSample load_xl(const uint4 *res) {
     const uint4 r1 = res[1], r2 = res[2], r3 = res[3];
     LightSample XL;

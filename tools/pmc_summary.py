@@ -36,3 +36,24 @@ for k, c in agg.items():
         print(f"   L2 hit                  {c['TCC_HIT_sum'] / (c['TCC_HIT_sum'] + c['TCC_MISS_sum']):6.3f}")
     if c.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
         print(f"   L1->L2 req / L1 access  {c['TCP_TCC_READ_REQ_sum'] / c['TCP_TOTAL_CACHE_ACCESSES_sum']:6.3f}")
+
+# Chip-level limiter figures per dispatch (rocprofv3 sums the SQ / GRBM counters over the
+# 8 XCDs; SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles, MI355X_MICROARCH.md):
+#   cycles            = GRBM_GUI_ACTIVE / 8 (per XCD; the kernel's span in shader clocks)
+#   resident waves    = 4 * SQ_WAVE_CYCLES / cycles / 1024 SIMDs  (mean waves per SIMD)
+#   VALU issue share  = 4 * SQ_ACTIVE_INST_VALU / (1024 * cycles)  (SIMD cycles issuing VALU)
+#   VALU instr/query  = SQ_INSTS_VALU / queries (when the query count is given)
+SIMDS = 1024
+print("\n== chip-level, per dispatch of group 1's dispatch count")
+for k, c in agg.items():
+    n = len({d for d in disp[k] if "g1/" in d[0]}) or 1
+    cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8 / n
+    if not cyc or not c.get("SQ_WAVE_CYCLES"):
+        continue
+    res = 4 * c["SQ_WAVE_CYCLES"] / n / cyc / SIMDS
+    valu = 4 * c.get("SQ_ACTIVE_INST_VALU", 0) / n / (SIMDS * cyc)
+    l2 = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]) if c.get("TCC_HIT_sum") else float("nan")
+    l1 = 1 - c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"] if c.get("TCP_TOTAL_CACHE_ACCESSES_sum") else float("nan")
+    print(f"   {k[:48]:48s} cycles {cyc:9.0f}  waves/SIMD {res:5.2f}  VALU issue {valu:5.3f}  "
+          f"VALU insts {c.get('SQ_INSTS_VALU', 0) / n:10.4g}  SALU {c.get('SQ_INSTS_SALU', 0) / n:10.4g}  "
+          f"L1 hit {l1:5.3f}  L2 hit {l2:5.3f}")
