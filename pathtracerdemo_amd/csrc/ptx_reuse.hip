@@ -612,6 +612,104 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
     write_reused(out, res_at(A.cur, src), p_sel, q_sel, f_sel, w_sum, Csum);
 }
 
+// The same combine for M = 3 with four lanes per pixel: lane 0 holds the canonical sample,
+// lane 1 + m neighbour m (its offset draws, summary and two job results gathered by that
+// lane).  The neighbourhood sums (confidences, the canonical MIS weight sum_n Q_n) and the
+// resampling weights' running sum are gathered with __shfl inside the pixel's four lanes and
+// added in the sequential order of combine_pixel (((0 + Q_0) + Q_1) + Q_2, w_c first), so the
+// floats are the same; each lane then evaluates its own UpdateReservoir draw (draw k of the
+// selection stream is seed + 2M + k), the last accepted lane is the selection (ballot), and
+// the 128-byte output reservoir is written 32 bytes per lane.  Bit-identical to combine_pixel.
+constexpr uint32_t kShflLanes = 4u;  // lanes per pixel (M + 1 with M = 3)
+__global__ __launch_bounds__(WB) void wspatial_combine_shfl(Scene sc, WaveBufs w, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE);
+    constexpr uint32_t M = 3u;
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    const uint32_t lane = __lane_id(), r = lane & 3u, base = lane & ~3u;
+    for (uint32_t k = 0; k < w.seg_px; k += WB / kShflLanes) {  // workgroup-uniform
+        // pixel k + threadIdx.x / 4 of the segment (seg_pixel's tile layout)
+        const uint32_t off = k + (threadIdx.x >> 2), sl = off >> 6;
+        const uint32_t q = set_tile(w, ((sl / w.cluster) * w.nseg + j) * w.cluster + sl % w.cluster) * 64u + (off & 63u);
+        uint32_t x = 0u, y = 0u;
+        const bool inside = q < np && tile_xy(sc, q, x, y);
+        const uint32_t pix = inside ? (y - sc.row_begin) * sc.width + x : 0u;
+        const bool hit = inside && gdecode(A.gbuf[pix]).valid;
+        uint4 c5 = make_uint4(0u, 0u, 0u, 0u), c6 = c5, c7 = c5;
+        if (hit) { const uint4 *rc = A.cur + 8u * (size_t)pix; c5 = rc[5]; c6 = rc[6]; c7 = rc[7]; }
+        const CombineCanon c{(float)c7.y, asf(c6.x), asf(c6.y), asf(c7.x), c7.y != 0u && c5.w >= 2u && asf(c6.x) > 0.0f};
+        const float Mf = (float)M;
+        const uint32_t seed0 = hit ? reuse_seed(sc, x, y, SALT_SPATIAL) : 0u;
+        // lane 1 + m: neighbour m
+        bool pres = false;
+        int32_t nid = (int32_t)pix;
+        Nbr nb{false, 0u, 0u, 0.0f, 0.0f, 0.0f};
+        float4 Fr = make_float4(0.0f, 0.0f, 0.0f, 0.0f), B = Fr;
+        if (hit && r > 0u) {
+            const uint32_t m = r - 1u;
+            uint32_t seed = seed0 + 2u * m, nx = 0u, ny = 0u;
+            pres = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+            if (pres) nid = band_index(sc, nx, ny);
+            const uint4 nv = A.nbr[nid];
+            const float4 *jr = A.jres + (size_t)pix * A.jpp;
+            Fr = jr[2u * m];
+            B = jr[2u * m + 1u];
+            nb = nv.w != kNbrEscape ? Nbr{(nv.w >> 31) != 0u, (nv.w >> 24) & 0x7fu, nv.w & 0xffffffu, asf(nv.x),
+                                          asf(nv.y), asf(nv.z)}
+                                    : nbr_at(A, nid);
+            if (!pres) nb.valid = false;
+        }
+        const float Q = nb.valid ? canon_q(c, Mf, nb.C, B) : 1.0f;
+        const uint32_t Cn = nb.valid ? nb.C : 0u;
+        // neighbourhood sums in combine_pixel's order
+        const float Q0 = __shfl(Q, base + 1u), Q1 = __shfl(Q, base + 2u), Q2 = __shfl(Q, base + 3u);
+        const uint32_t Csum = c7.y + __shfl(Cn, base + 1u) + __shfl(Cn, base + 2u) + __shfl(Cn, base + 3u);
+        float sumQ = 0.0f;
+        sumQ += Q0;
+        sumQ += Q1;
+        sumQ += Q2;
+        const float wc = c.ok ? (sumQ / Mf) * c.pc * c.Wc : 0.0f;
+        float pf = 0.0f, qf = 0.0f;
+        SelF fj{false, mk(0.0f, 0.0f, 0.0f)};
+        const float wn = r > 0u ? neighbour_weight(c, Mf, nb, Fr, pf, qf, fj) : wc;
+        // running sum of the resampling weights (canonical first), this lane's draw
+        const float w0 = __shfl(wn, base), w1 = __shfl(wn, base + 1u), w2 = __shfl(wn, base + 2u),
+                    w3 = __shfl(wn, base + 3u);
+        float w_sum = 0.0f, w_upto = 0.0f;
+        w_sum += w0; if (r == 0u) w_upto = w_sum;
+        w_sum += w1; if (r == 1u) w_upto = w_sum;
+        w_sum += w2; if (r == 2u) w_upto = w_sum;
+        w_sum += w3; if (r == 3u) w_upto = w_sum;
+        uint32_t dseed = seed0 + 2u * M + r;
+        const bool accept = hit && rnd(dseed) < wn / w_upto;
+        const uint32_t grp = (uint32_t)(__ballot(accept) >> base) & 0xfu;
+        const uint32_t sel = grp ? 31u - (uint32_t)__builtin_clz(grp) : 0u;  // the last accepted lane
+        // the selected lane's sample: source reservoir, p_hat, q and stored contribution
+        const int32_t src_l = r == 0u ? (int32_t)pix : (pres ? nid : 0);
+        const int32_t src = __shfl(src_l, base + sel);
+        const float p_sel = sel ? __shfl(pf, base + sel) : c.pc, q_sel = sel ? __shfl(qf, base + sel) : c.qc;
+        const float fx = __shfl(fj.f.x, base + sel), fy = __shfl(fj.f.y, base + sel), fz = __shfl(fj.f.z, base + sel);
+        const bool fk = __shfl(fj.known ? 1 : 0, base + sel) != 0;
+        if (!inside) continue;
+        uint4 *out = A.hist + 8u * (size_t)pix;
+        if (!hit) {
+            out[2u * r] = make_uint4(0u, 0u, 0u, 0u);
+            out[2u * r + 1u] = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
+        if (r < 3u) {  // words 8r .. 8r + 7 of the selected sample
+            const uint4 *sv = res_at(A.cur, src);
+            const uint4 a0 = sv[2u * r], a1 = sv[2u * r + 1u];
+            out[2u * r] = a0;
+            out[2u * r + 1u] = a1;
+        } else {
+            const SelF fs = sel ? SelF{fk, mk(fx, fy, fz)} : stored_f(A.cur + 8u * (size_t)pix);
+            out[6] = make_uint4(asu(p_sel), asu(q_sel), fs.known ? asu(fs.f.x) : 0u, fs.known ? asu(fs.f.y) : 0u);
+            out[7] = make_uint4(asu(p_sel > 0.0f ? w_sum / p_sel : 0.0f), Csum, fs.known ? asu(fs.f.z) : 0u,
+                                fs.known ? 1u : 0u);
+        }
+    }
+}
+
 __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, ReuseArgs A) {
     PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE);
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
@@ -646,6 +744,8 @@ hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_tempora
         hipLaunchKernelGGL(wjob_step, grid, blk, 0, s, sc, w, (uint32_t)round, A);
     } else {
         if (pass_temporal) hipLaunchKernelGGL(wtemporal_combine, grid, blk, 0, s, sc, w, A);
+        else if (A.neighbors == 3u && !getenv("PTX_COMBINE_SCALAR"))  // (A/B switch)
+            hipLaunchKernelGGL(wspatial_combine_shfl, dim3(w.seg_count), blk, 0, s, sc, w, A);
         else hipLaunchKernelGGL(wspatial_combine, grid, blk, 0, s, sc, w, A);
     }
     return hipGetLastError();
