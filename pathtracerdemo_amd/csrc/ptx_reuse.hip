@@ -110,8 +110,9 @@ __device__ __forceinline__ bool job_begin(const Scene &sc, const ReuseArgs &A, J
 // The job's next ray: a regenerated BSDF direction (PT_4:1367-1381) or the light
 // segment's Visibility (PT_4:1323-1333).  Called by every lane of the wave; `emit` selects
 // the lanes with a live job.  Returns whether the job continues (else its result is out).
+// seed0: word 0 of the sample's reservoir (its first replayed draw's seed), read when s.i == 1.
 __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const ReuseArgs &A, bool emit, Job &s,
-                                         uint32_t jid) {
+                                         uint32_t jid, uint32_t seed0) {
     bool ray = false, vis = false;
     f3 o = mk(0.0f, 0.0f, 0.0f), d = o, Le = o;
     float remain = -1.0f;
@@ -120,7 +121,7 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
         const f3 V = normalize(s.prev - s.cur.pos);
         bool ok = true;
         if (s.i + 1u < s.length) {
-            uint32_t seed = s.i == 1u ? rv[0].x : s.seed1, lobe;
+            uint32_t seed = s.i == 1u ? seed0 : s.seed1, lobe;
             const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
             const float pdf = pdf_bsdf(s.cur, V, dir);
             s.prod *= pdf;
@@ -197,7 +198,7 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
                 A.jres[jid] = valid ? make_float4(s.f.x, s.f.y, s.f.z, qv) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
         }
-        const bool live = job_emit(sc, g, A, emit, s, jid);
+        const bool live = job_emit(sc, g, A, emit, s, jid, 0u);  // (s.i >= 2 here)
         if (live) job_store(A, jid, s);
         job_keep(g, JL, live, live && s.phase != 0u, jid);
     }
@@ -304,7 +305,7 @@ void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
             active = job_begin(sc, A, s, x, y, (int32_t)pix, (int32_t)pix);
             if (active && A.use_init) active = temporal_from_init(sc, w, A, s, pix);
         }
-        const bool live = job_emit(sc, g, A, active, s, pix);
+        const bool live = job_emit(sc, g, A, active, s, pix, active ? A.cur[8u * (size_t)pix].x : 0u);
         if (live) job_store(A, pix, s);
         job_keep(g, JL, live, live && s.phase != 0u, pix);
     }
@@ -422,6 +423,7 @@ hipError_t wave_surface(const Scene &sc, const WaveBufs &w, const uint4 *gbuf, h
 // this pixel's sample in neighbour m's domain) its reservoir; the neighbour offsets come
 // from one pass over the pixel's salted stream.  A workgroup walks its segment kind by kind
 // and neighbour by neighbour, so a wave emits one 8x8 tile's jobs of one slot at a time.
+constexpr uint32_t kMaxPrefetch = 3u;  // neighbours whose data wspatial_start gathers up front
 #ifndef SPATIAL_START_WAVES
 #define SPATIAL_START_WAVES 3  // the shared surface + one job: 128 VGPRs spill 108 B/lane
 #endif
@@ -431,7 +433,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
-    const uint32_t np = padded_pixels(sc), jpp = A.jpp;
+    const uint32_t np = padded_pixels(sc), jpp = A.jpp, M = A.neighbors;
     for (uint32_t base = 0; base < w.seg_px * 2u; base += WB) {  // workgroup-uniform
         const bool backward = base >= w.seg_px;
         const uint32_t q = seg_pixel(w, g.j, base % w.seg_px);
@@ -439,6 +441,8 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
         bool valid = false, canon = false;
         Surface X1{};
         f3 x0{};
+        uint4 c0 = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t clen = 0u;
         if (q < np && tile_xy(sc, q, x, y)) {
             pix = (y - sc.row_begin) * sc.width + x;
             seed = reuse_seed(sc, x, y, SALT_SPATIAL);
@@ -448,36 +452,78 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
             } else {
                 valid = A.surf[2u * (size_t)pix].w != kNoSurface;
                 const uint4 *rc = A.cur + 8u * (size_t)pix;  // this pixel's sample, shifted to each neighbour
-                canon = valid && rc[7].y != 0u && rc[5].w >= 2u && asf(rc[6].x) > 0.0f;
+                const uint4 r5 = rc[5];
+                canon = valid && rc[7].y != 0u && r5.w >= 2u && asf(rc[6].x) > 0.0f;
+                if (canon) { c0 = rc[0]; clen = r5.w; }
             }
         }
-        for (uint32_t m = 0; m < A.neighbors; ++m) {  // uniform
+        // every neighbour's offset first, then its summary + seeds (forward) or surface record
+        // (backward) for all of them in one round trip, then the jobs one by one
+        uint32_t nxy[kMaxPrefetch];
+        int32_t nidx[kMaxPrefetch];
+        uint4 pa[kMaxPrefetch], pb[kMaxPrefetch];
+        const uint32_t MP = M < kMaxPrefetch ? M : kMaxPrefetch;
+#pragma unroll
+        for (uint32_t m = 0; m < kMaxPrefetch; ++m) {
+            uint32_t nx = 0u, ny = 0u;
+            const bool present = m < MP && valid && spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
+            nxy[m] = present ? (nx | (ny << 16)) : 0xffffffffu;
+            nidx[m] = present ? band_index(sc, nx, ny) : 0;
+        }
+#pragma unroll
+        for (uint32_t m = 0; m < kMaxPrefetch; ++m) {
+            pa[m] = make_uint4(0u, 0u, 0u, kNoSurface);
+            pb[m] = make_uint4(0u, 0u, 0u, 0u);
+            if (nxy[m] != 0xffffffffu) {
+                if (!backward) { pa[m] = A.nbr[nidx[m]]; pb[m] = A.cur[8 * (ptrdiff_t)nidx[m]]; }
+                else if (canon) { pa[m] = A.surf[2 * (ptrdiff_t)nidx[m]]; pb[m] = A.surf[2 * (ptrdiff_t)nidx[m] + 1]; }
+            }
+        }
+        for (uint32_t m = 0; m < M; ++m) {  // uniform
             const uint32_t jid = pix * jpp + 2u * m + (backward ? 1u : 0u);
             bool act = false;
+            uint32_t s0 = 0u;
             Job s;
             if (valid) {
-                uint32_t nx = 0u, ny = 0u;
-                bool present = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
-                const int32_t nidx = present ? band_index(sc, nx, ny) : 0;
+                uint32_t nx = 0u, ny = 0u, pxy = 0xffffffffu;
+                int32_t ni = 0;
+                uint4 a = make_uint4(0u, 0u, 0u, kNoSurface), b = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+                for (uint32_t k = 0; k < kMaxPrefetch; ++k)
+                    if (k == m) { pxy = nxy[k]; ni = nidx[k]; a = pa[k]; b = pb[k]; }
+                if (m >= kMaxPrefetch) {  // (more neighbours than prefetched: this one's draws now)
+                    uint32_t sm = reuse_seed(sc, x, y, SALT_SPATIAL) + 2u * m;  // draws 2m, 2m + 1
+                    if (spatial_neighbor(sm, A.radius, x, y, sc.width, sc.height, nx, ny)) {
+                        pxy = nx | (ny << 16);
+                        ni = band_index(sc, nx, ny);
+                        if (!backward) { a = A.nbr[ni]; b = A.cur[8 * (ptrdiff_t)ni]; }
+                        else if (canon) { a = A.surf[2 * (ptrdiff_t)ni]; b = A.surf[2 * (ptrdiff_t)ni + 1]; }
+                    }
+                }
+                const bool present = pxy != 0xffffffffu;
+                nx = pxy & 0xffffu; ny = pxy >> 16;
                 bool want = false;
                 if (present && !backward) {  // the neighbour's sample in this pixel's domain
-                    const Nbr nb = nbr_at(A, nidx);
+                    const Nbr nb = a.w != kNbrEscape ? Nbr{(a.w >> 31) != 0u, (a.w >> 24) & 0x7fu, a.w & 0xffffffu,
+                                                           asf(a.x), asf(a.y), asf(a.z)}
+                                                     : nbr_at(A, ni);
                     want = nb.valid && nb.length >= 2u && nb.p > 0.0f;
                     act = want && nb.C != 0u;
-                    if (act) job_init(s, x0, X1, mref, nidx, nb.length, res_at(A.cur, nidx)[0].y);
+                    if (act) { job_init(s, x0, X1, mref, ni, nb.length, b.y); s0 = b.x; }
                 } else if (present && canon) {  // this pixel's sample in the neighbour's domain
-                    Surface Xn;
-                    uint32_t nref;
-                    want = surf_load(sc, A.surf, nidx, Xn, nref);
-                    if (want) {
-                        act = true;
-                        job_init(s, x0_of(sc, nx, ny), Xn, nref, (int32_t)pix, A.cur[8u * (size_t)pix + 5u].w,
-                                 A.cur[8u * (size_t)pix].y);
+                    want = act = a.w != kNoSurface;
+                    if (act) {
+                        Surface Xn;
+                        Xn.pos = mk(asf(a.x), asf(a.y), asf(a.z));
+                        Xn.nrm = mk(asf(b.x), asf(b.y), asf(b.z));
+                        Xn.mat = material_at(sc, a.w);
+                        job_init(s, x0_of(sc, nx, ny), Xn, a.w, (int32_t)pix, clen, c0.y);
+                        s0 = c0.x;
                     }
                 }
                 if (want && !act) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
-            const bool live = job_emit(sc, g, A, act, s, jid);
+            const bool live = job_emit(sc, g, A, act, s, jid, s0);
             if (live) job_store(A, jid, s);
             job_keep(g, JL, live, live && s.phase != 0u, jid);
         }
