@@ -215,16 +215,18 @@ __device__ __forceinline__ void box_pair(f3 o, f3 inv, float4 qx, float4 qy, flo
     const v2f t1x = (v2f{qx.x, qx.y} - ox) * ix, t2x = (v2f{qx.z, qx.w} - ox) * ix;
     const v2f t1y = (v2f{qy.x, qy.y} - oy) * iy, t2y = (v2f{qy.z, qy.w} - oy) * iy;
     const v2f t1z = (v2f{qz.x, qz.y} - oz) * iz, t2z = (v2f{qz.z, qz.w} - oz) * iz;
-    float lmin = fmaxf(fminf(t1x.x, t2x.x), fmaxf(fminf(t1y.x, t2y.x), fminf(t1z.x, t2z.x)));
-    float lmax = fminf(fmaxf(t1x.x, t2x.x), fminf(fmaxf(t1y.x, t2y.x), fmaxf(t1z.x, t2z.x)));
-    float rmin = fmaxf(fminf(t1x.y, t2x.y), fmaxf(fminf(t1y.y, t2y.y), fminf(t1z.y, t2z.y)));
-    float rmax = fminf(fmaxf(t1x.y, t2x.y), fminf(fmaxf(t1y.y, t2y.y), fmaxf(t1z.y, t2z.y)));
-    if (lmin > lmax) { lmin = 1.0f; lmax = 0.0f; }
-    if (rmin > rmax) { rmin = 1.0f; rmax = 0.0f; }
+    const float lmin = fmaxf(fminf(t1x.x, t2x.x), fmaxf(fminf(t1y.x, t2y.x), fminf(t1z.x, t2z.x)));
+    const float lmax = fminf(fmaxf(t1x.x, t2x.x), fminf(fmaxf(t1y.x, t2y.x), fmaxf(t1z.x, t2z.x)));
+    const float rmin = fmaxf(fminf(t1x.y, t2x.y), fmaxf(fminf(t1y.y, t2y.y), fminf(t1z.y, t2z.y)));
+    const float rmax = fminf(fmaxf(t1x.y, t2x.y), fminf(fmaxf(t1y.y, t2y.y), fmaxf(t1z.y, t2z.y)));
+    // The reference maps an empty range (min > max) to (1, 0) before the overlap test with
+    // [vx, vy]; with vx = 1e-4 > 0 the mapped range never overlaps, so the test is the
+    // non-empty check plus the overlap -- same result (NaN terms fail both forms).  tl / tr
+    // only order two children that BOTH hit (both non-empty, so never remapped).
     tl = lmin;
     tr = rmin;
-    hl = (vx <= lmax) && (lmin <= vy);
-    hr = (vx <= rmax) && (rmin <= vy);
+    hl = (lmin <= lmax) && (vx <= lmax) && (lmin <= vy);
+    hr = (rmin <= rmax) && (vx <= rmax) && (rmin <= vy);
 }
 
 // The slab test of a sub-mesh root, each axis's {min, max} slab terms as one packed pair
@@ -232,10 +234,9 @@ __device__ __forceinline__ bool box_root(f3 o, f3 inv, const SubRoot &R, float v
     const v2f t_x = (v2f{R.x[0], R.x[1]} - v2f{o.x, o.x}) * v2f{inv.x, inv.x};
     const v2f t_y = (v2f{R.y[0], R.y[1]} - v2f{o.y, o.y}) * v2f{inv.y, inv.y};
     const v2f t_z = (v2f{R.z[0], R.z[1]} - v2f{o.z, o.z}) * v2f{inv.z, inv.z};
-    float tmin = fmaxf(fminf(t_x.x, t_x.y), fmaxf(fminf(t_y.x, t_y.y), fminf(t_z.x, t_z.y)));
-    float tmax = fminf(fmaxf(t_x.x, t_x.y), fminf(fmaxf(t_y.x, t_y.y), fmaxf(t_z.x, t_z.y)));
-    if (tmin > tmax) { tmin = 1.0f; tmax = 0.0f; }
-    return (vx <= tmax) && (tmin <= vy);
+    const float tmin = fmaxf(fminf(t_x.x, t_x.y), fmaxf(fminf(t_y.x, t_y.y), fminf(t_z.x, t_z.y)));
+    const float tmax = fminf(fmaxf(t_x.x, t_x.y), fminf(fmaxf(t_y.x, t_y.y), fmaxf(t_z.x, t_z.y)));
+    return (tmin <= tmax) && (vx <= tmax) && (tmin <= vy);  // (empty -> (1, 0) never overlaps: box_pair)
 }
 
 // GetRayTriangleHitDistance (SH/PT_1_InitPass.wgsl:516-547) on the precomputed edges.
