@@ -204,6 +204,10 @@ int build_layout(ptx_handle *h) {
         I.sub_base = mesh_sub_base[I.mesh];
         I.nsub = mesh_nsub[I.mesh];
         I.tri_base = mesh_tri_base[I.mesh];
+        // exactly the identity (bitwise 1 / +0, M and M^-1): the kernels' transforms of this
+        // instance reduce to x + 0 (inst_point, ptx_device.h) with the same bits
+        static const float kId[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+        if (!std::memcmp(I.m, kId, sizeof kId) && !std::memcmp(I.minv, kId, sizeof kId)) I.mesh |= kInstIdentity;
     }
     if (tris.empty()) tris.resize(12, 0.0f);
     if (tverts.empty()) tverts.resize(20, 0.0f);

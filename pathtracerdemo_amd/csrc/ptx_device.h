@@ -61,8 +61,9 @@ struct alignas(16) SubRoot {    // 32 B: the root box by axis, {min, max} pairs 
 struct alignas(16) Inst {       // 144 B
     float m[16];
     float minv[16];
-    uint32_t mesh, sub_base, nsub, tri_base;
+    uint32_t mesh, sub_base, nsub, tri_base;  // mesh: | kInstIdentity when M and M^-1 are exactly I
 };
+constexpr uint32_t kInstIdentity = 0x80000000u;
 
 // Everything a kernel reads, passed by value (lives in the kernarg segment).
 struct Scene {
@@ -149,6 +150,23 @@ __device__ __forceinline__ f3 wdivide(float x, float y, float z, float w) {
     return f3{x / w, y / w, z / w};
 }
 // column-major mat4 * (p,1) then /w (TransformVec3WithMat4x4, SH/PT_1_InitPass.wgsl:480-484)
+__device__ __forceinline__ f3 xform_point(const float *m, f3 p);
+__device__ __forceinline__ f3 xform_point_t(const float *m, f3 p);
+// The same products for an instance whose matrices are exactly the identity (bitwise 1 / +0):
+// ((1 x + 0 y) + 0 z) + 0 * 1 is x + 0 for finite x, y, z (a -0 becomes +0 -- the last term is
+// +0 -- and w is exactly 1), so the 28-operation transform reduces to three additions with
+// the same bits.  Non-finite points take the full product (0 * inf is NaN there).
+__device__ __forceinline__ bool finite3(f3 p) {
+    return __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
+}
+__device__ __forceinline__ f3 inst_point(const Inst &I, const float *m, f3 p) {
+    if ((I.mesh & kInstIdentity) && finite3(p)) return f3{p.x + 0.0f, p.y + 0.0f, p.z + 0.0f};
+    return xform_point(m, p);
+}
+__device__ __forceinline__ f3 inst_point_t(const Inst &I, const float *m, f3 p) {
+    if ((I.mesh & kInstIdentity) && finite3(p)) return f3{p.x + 0.0f, p.y + 0.0f, p.z + 0.0f};
+    return xform_point_t(m, p);
+}
 __device__ __forceinline__ f3 xform_point(const float *m, f3 p) {
     float x = ((m[0] * p.x + m[4] * p.y) + m[8] * p.z) + m[12] * 1.0f;
     float y = ((m[1] * p.x + m[5] * p.y) + m[9] * p.z) + m[13] * 1.0f;
@@ -373,6 +391,8 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
         const Inst &I = insts[ii];
         if (PROF) pf.hit(PROF_INST);
         // TransformRayWithMat4x4(InRay, M^-1, false), SH/PT_1_InitPass.wgsl:486-496
+        // (the identity shortcut of inst_point is not used here: at the trace kernel's 128-VGPR
+        // budget its extra live values spill, +3.4 % on trace_queue)
         f3 lo = xform_point(I.minv, ray.o);
         f3 le = xform_point(I.minv, ray.o + ray.d);
         f3 ld = le - lo;

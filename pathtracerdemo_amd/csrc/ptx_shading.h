@@ -35,12 +35,12 @@ __device__ __forceinline__ Surface get_surface(const Scene &sc, Compact x) {
     Surface s;
     s.mat = material_at(sc, I.sub_base + x.mat);
     const TriVerts tv = tri_verts(sc, I.tri_base + x.prim);
-    f3 p0 = xform_point(I.m, tv.p[0]);
-    f3 n0 = xform_point_t(I.minv, tv.n[0]);
-    f3 p1 = xform_point(I.m, tv.p[1]);
-    f3 n1 = xform_point_t(I.minv, tv.n[1]);
-    f3 p2 = xform_point(I.m, tv.p[2]);
-    f3 n2 = xform_point_t(I.minv, tv.n[2]);
+    f3 p0 = inst_point(I, I.m, tv.p[0]);
+    f3 n0 = inst_point_t(I, I.minv, tv.n[0]);
+    f3 p1 = inst_point(I, I.m, tv.p[1]);
+    f3 n1 = inst_point_t(I, I.minv, tv.n[1]);
+    f3 p2 = inst_point(I, I.m, tv.p[2]);
+    f3 n2 = inst_point_t(I, I.minv, tv.n[2]);
     float U = x.bu, V = x.bv, W = 1.0f - U - V;
     s.nrm = normalize((n0 * U + n1 * V) + n2 * W);
     s.pos = (p0 * U + p1 * V) + p2 * W;
@@ -53,9 +53,9 @@ __device__ __forceinline__ Surface surface_at(const Scene &sc, const Compact &x,
     Surface s;
     s.mat = material_at(sc, I.sub_base + x.mat);
     const TriVerts tv = tri_verts(sc, I.tri_base + x.prim);
-    f3 n0 = xform_point_t(I.minv, tv.n[0]);
-    f3 n1 = xform_point_t(I.minv, tv.n[1]);
-    f3 n2 = xform_point_t(I.minv, tv.n[2]);
+    f3 n0 = inst_point_t(I, I.minv, tv.n[0]);
+    f3 n1 = inst_point_t(I, I.minv, tv.n[1]);
+    f3 n2 = inst_point_t(I, I.minv, tv.n[2]);
     float U = x.bu, V = x.bv, W = 1.0f - U - V;
     s.nrm = normalize((n0 * U + n1 * V) + n2 * W);
     s.pos = pos;
@@ -65,9 +65,9 @@ __device__ __forceinline__ Surface surface_at(const Scene &sc, const Compact &x,
 __device__ __forceinline__ f3 get_surface_pos(const Scene &sc, Compact x) {
     const Inst &I = sc.insts[x.inst];
     const TriVerts tv = tri_verts(sc, I.tri_base + x.prim);
-    f3 p0 = xform_point(I.m, tv.p[0]);
-    f3 p1 = xform_point(I.m, tv.p[1]);
-    f3 p2 = xform_point(I.m, tv.p[2]);
+    f3 p0 = inst_point(I, I.m, tv.p[0]);
+    f3 p1 = inst_point(I, I.m, tv.p[1]);
+    f3 p2 = inst_point(I, I.m, tv.p[2]);
     float U = x.bu, V = x.bv, W = 1.0f - U - V;
     return (p0 * U + p1 * V) + p2 * W;
 }
