@@ -73,8 +73,9 @@ __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, ui
 }
 
 // PT_1's throughput recursion + Russian roulette at one replayed vertex (oracle rr_step).
-__device__ __forceinline__ bool rr_step(Job &s, const Surface &X, f3 V, f3 L, float pdf) {
-    s.rr_f = s.rr_f * (bsdf(X, V, L) * fabsf(dot(X.nrm, L)));
+// (fv = bsdf(X, V, L), pdf = pdf_bsdf(X, V, L): bsdf_pdf)
+__device__ __forceinline__ bool rr_step(Job &s, const Surface &X, f3 L, f3 fv, float pdf) {
+    s.rr_f = s.rr_f * (fv * fabsf(dot(X.nrm, L)));
     s.rr_p *= pdf;
     const float ps = luminance(s.rr_f) / s.rr_p;
     const bool ok = ps > 0.0f;
@@ -123,15 +124,20 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
         if (s.i + 1u < s.length) {
             uint32_t seed = s.i == 1u ? seed0 : s.seed1, lobe;
             const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
-            const float pdf = pdf_bsdf(s.cur, V, dir);
+            float pdf;
+            const f3 fv = bsdf_pdf(s.cur, V, dir, pdf);
             s.prod *= pdf;
-            ok = rr_step(s, s.cur, V, dir, pdf);
+            ok = rr_step(s, s.cur, dir, fv, pdf);
             s.phase = 0u;
             o = s.cur.pos; d = dir;
         } else {
             const LightSample XL = load_xl(rv);
             const f3 L = direction_to_light(s.cur, XL);
-            if (XL.type == LIGHT_ENV) ok = rr_step(s, s.cur, V, L, pdf_bsdf(s.cur, V, L));
+            if (XL.type == LIGHT_ENV) {
+                float pdf;
+                const f3 fv = bsdf_pdf(s.cur, V, L, pdf);
+                ok = rr_step(s, s.cur, L, fv, pdf);
+            }
             s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
             float gl = 1.0f;
             if (XL.type == LIGHT_RECT) {
@@ -251,9 +257,10 @@ __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBu
         f3 V = normalize(s.prev - s.cur.pos);
         uint32_t seed = s.i == 1u ? rv[0].x : s.seed1, lobe;
         const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
-        const float pdf = pdf_bsdf(s.cur, V, dir);
+        float pdf;
+        const f3 fv = bsdf_pdf(s.cur, V, dir, pdf);
         s.prod *= pdf;
-        if (!rr_step(s, s.cur, V, dir, pdf)) {
+        if (!rr_step(s, s.cur, dir, fv, pdf)) {
             A.jres[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             return false;
         }

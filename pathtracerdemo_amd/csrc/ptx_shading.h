@@ -302,6 +302,33 @@ __device__ __forceinline__ float pdf_bsdf(const Surface &X, f3 V, f3 L) {
     return pdf_btdf(X, V, L);
 }
 
+// bsdf(X, V, L) and pdf_bsdf(X, V, L) together (a sampled direction's throughput factor and its
+// pdf, PT_1:1427-1434): each value computed exactly as the two functions compute it, the
+// reflection branch's half vector, D, F0 and N.L shared instead of evaluated twice.
+__device__ __forceinline__ f3 bsdf_pdf(const Surface &X, f3 V, f3 L, float &pdf) {
+    const f3 N = X.nrm;
+    if (dot(L, N) * dot(V, N) > 0.0f) {
+        const f3 H = normalize(L + V);
+        const float NdotV = fmaxf(dot(N, V), 0.0f), NdotL = fmaxf(dot(N, L), 0.0f);
+        const float LdotN = fmaxf(dot(L, N), 0.0f);
+        const float NdotH = fmaxf(dot(N, H), 0.0f), VdotH = fmaxf(dot(V, H), 0.0f);
+        const f3 base = X.mat.albedo;
+        const float metal = X.mat.metal, R = X.mat.rough;
+        const f3 F0 = mix3(mk(0.04f, 0.04f, 0.04f), base, metal);
+        const float D = ggx_d(NdotH, R);
+        const float G0 = geom_shadow(NdotV, NdotL, R);
+        const f3 F = fresnel(VdotH, F0);
+        const f3 kD = mk(1.0f - F.x, 1.0f - F.y, 1.0f - F.z) * (1.0f - metal);
+        const f3 diffuse = (kD / PI_F) * base;
+        const f3 spec = ((F * D) * G0) * 0.25f;
+        const float p_spec = mixf(luminance(F0), 1.0f, metal);
+        pdf = mixf(LdotN / PI_F, D / fmaxf(4.0f * VdotH, EPS_F), p_spec);
+        return (diffuse + spec) * (1.0f - X.mat.trans);
+    }
+    pdf = pdf_btdf(X, V, L);
+    return btdf(X, V, L) * X.mat.trans;
+}
+
 // DirectionToLight, SH/PT_1_InitPass.wgsl:746-772
 __device__ __forceinline__ f3 direction_to_light(const Surface &X, const LightSample &XL) {
     switch (XL.type) {

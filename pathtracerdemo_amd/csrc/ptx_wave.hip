@@ -513,8 +513,9 @@ __device__ __forceinline__ void winit_vertex(const Scene &sc, const Seg &g, bool
             uint32_t lobe;
             const f3 Lb = sample_bsdf(s.seed, X, V, lobe);
             s.flags |= lobe << (8u + 2u * (s.i - 1u));
-            s.f = s.f * (bsdf(X, V, Lb) * fabsf(dot(X.nrm, Lb)));
-            const float pdfv = pdf_bsdf(X, V, Lb);
+            float pdfv;
+            const f3 bv = bsdf_pdf(X, V, Lb, pdfv);
+            s.f = s.f * (bv * fabsf(dot(X.nrm, Lb)));
             s.p *= pdfv;
             const float ps = luminance(s.f) / s.p;
             if (rnd(s.seed) < ps) {
@@ -914,8 +915,10 @@ __device__ __forceinline__ void wmcpt_vertex(const Scene &sc, const Seg &g, bool
         s.lbase = lbase;
         uint32_t lobe;
         Lb = sample_bsdf(s.seed, X, V, lobe);
-        s.f = s.f * (bsdf(X, V, Lb) * fabsf(dot(X.nrm, Lb)));
-        s.p *= pdf_bsdf(X, V, Lb);
+        float pdfv;
+        const f3 bv = bsdf_pdf(X, V, Lb, pdfv);
+        s.f = s.f * (bv * fabsf(dot(X.nrm, Lb)));
+        s.p *= pdfv;
         s.org = X.pos;
         const float ps = luminance(s.f) / s.p;
         if (rnd(s.seed) < ps) {
