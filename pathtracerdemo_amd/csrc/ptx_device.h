@@ -374,7 +374,7 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t &total) {
 template <bool COUNT, bool PROF = false, bool ROOTQ = true, bool ANY = false, bool COOP = false>
 __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *subs, const Inst *insts, Ray ray,
                                               PassEps eps, uint32_t *stack, uint32_t stride, float t_max = 1e10f,
-                                              CoopLds coop = CoopLds{nullptr}) {
+                                              CoopLds coop = CoopLds{nullptr}, bool want_pos = true) {
     Prof pf{};
     Hit best;
     best.valid = false;
@@ -573,7 +573,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     }
     if (best.valid) {
         best.t = vy;
-        if (!ANY) complete_hit(sc, ray, eps, best, insts);
+        if (!ANY && want_pos) complete_hit(sc, ray, eps, best, insts);
     }
     return best;
 }

@@ -63,8 +63,10 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
     float T = 1.0f, remain = a.w;
     for (uint32_t it = 0u;; ++it) {
         const float t_max = !active ? __builtin_nanf("") : vis ? fminf(remain, 1e10f) : 1e10f;
-        const Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP>(sc, subs, insts, r, eps, stack, WB, t_max,
-                                                                         coop);
+        // a Visibility hit's position is only needed to restart through a transmissive surface:
+        // it is reconstructed below for those lanes only
+        Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP>(sc, subs, insts, r, eps, stack, WB, t_max, coop,
+                                                                   !vis);
         if (active && !vis) {
             const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
             res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
@@ -79,6 +81,7 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
                 else {
                     T *= tr;
                     remain -= h.t;
+                    complete_hit(sc, r, eps, h, insts);
                     r.o = h.pos;
                     if (it == 4u) out = 0.0f;  // Visibility gives up after 5 segments
                 }
