@@ -39,6 +39,9 @@ namespace ptx {
 // several equal-t triangles wins -- unchanged for every hit inside the cap.
 // OCC: every query of the launch is Q_OCC (the GI shift's binary visibility): an any-hit
 // walk (trace_core_tab ANY), exact for "is there a hit with t <= remain".
+#ifndef TRACE_OCC_WAVES
+#define TRACE_OCC_WAVES 5  // occupancy of the occlusion-query instance (GI spatial rounds)
+#endif
 #ifndef TRACE_COOP
 #define TRACE_COOP true
 #endif
@@ -1049,7 +1052,7 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
             hipLaunchKernelGGL((trace_queue<true, 6, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
                                (uint32_t)round, eps);
         else
-            hipLaunchKernelGGL((trace_queue<false, 5, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
+            hipLaunchKernelGGL((trace_queue<false, TRACE_OCC_WAVES, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
                                (uint32_t)round, eps);
         return hipGetLastError();
     }
