@@ -90,8 +90,8 @@ def parse():
     ap.add_argument("--scene", default=None, help="default: c3_interior_32 (reuse), dummy_scene_1 (others)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--variant", choices=["wave", "tiled", "persistent", "simple"], default="wave",
-                    help="kernel variant (A/B): wavefront queues, tile + LDS ray exchange, persistent lanes, 1 thread/pixel")
+    ap.add_argument("--variant", choices=["wave", "simple"], default="wave",
+                    help="kernel variant (A/B): wavefront queues, or 1 thread/pixel")
     return ap.parse_args()
 
 

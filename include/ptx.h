@@ -87,8 +87,9 @@ extern "C" {
 
 #define PTX_FLAG_COUNT_WORK 1u     /* count rays / AABB / triangle tests on device (slower)   */
 #define PTX_FLAG_SIMPLE_KERNELS 2u   /* A/B: one thread per pixel, no ray exchange            */
-#define PTX_FLAG_PERSISTENT_LANES 4u /* A/B: persistent lanes with pixel regeneration         */
-#define PTX_FLAG_TILED_EXCHANGE 8u   /* A/B: 16x16 tiles with an LDS ray exchange             */
+#define PTX_FLAGS_RETIRED 12u      /* bits 4, 8: the persistent-lane / tiled-exchange A/B variants
+                                      (round 1; both lost to the wavefront kernels, removed):
+                                      ptx_create rejects them with PTX_E_INVALID               */
 #define PTX_FLAG_TIME_LAUNCHES 16u   /* HIP events around every wavefront launch (stats slots
                                         PTX_STAT_WAVE_*); costs ~5% of frame time            */
 #define PTX_FLAG_SINGLE_STREAM 32u   /* run the wavefront passes as one launch sequence (no

@@ -25,15 +25,13 @@ PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS, PTX_BUF_RES
 PTX_BUF_DIRECT = 5
 PTX_FLAG_COUNT_WORK = 1
 PTX_FLAG_SIMPLE_KERNELS = 2
-PTX_FLAG_PERSISTENT_LANES = 4
-PTX_FLAG_TILED_EXCHANGE = 8
+PTX_FLAGS_RETIRED = 12  # the removed persistent-lane / tiled A/B variants: ptx_create rejects them
 PTX_FLAG_TIME_LAUNCHES = 16
 PTX_FLAG_SINGLE_STREAM = 32
 PTX_FLAG_ROW_CENSUS = 64
 PTX_FLAG_HALO_OVERLAP = 128
 PTX_COMM_ID_BYTES = 128
-VARIANT_FLAGS = {"wave": 0, "tiled": PTX_FLAG_TILED_EXCHANGE, "persistent": PTX_FLAG_PERSISTENT_LANES,
-                 "simple": PTX_FLAG_SIMPLE_KERNELS}
+VARIANT_FLAGS = {"wave": 0, "simple": PTX_FLAG_SIMPLE_KERNELS}
 
 # every symbol include/ptx.h declares (checked by tests/test_abi.py)
 EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame", "ptx_render", "ptx_run_pass",

@@ -629,7 +629,7 @@ bool pipelined(const ptx_handle *h) {
     const size_t px = (size_t)h->band_h * h->cfg.width;
     return !off && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !h->comm && !h->halo_top && !h->halo_bot &&
            px <= (size_t)4u << 20 &&
-           !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE | PTX_FLAG_COUNT_WORK |
+           !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK |
                    PTX_FLAG_TIME_LAUNCHES | PTX_FLAG_SINGLE_STREAM | PTX_FLAG_ROW_CENSUS)) &&
            (h->alt_active ? h->stream == h->alt_stream : h->stream == h->own_stream);
 }
@@ -700,7 +700,7 @@ static int leave_alt(ptx_handle *h) {
 // as one unit in stats slot PTX_STAT_FRAME.  Returns 1 if this path does not apply.
 static int timed_wave_frame(ptx_handle *h) {
     const uint32_t fl = h->cfg.flags;
-    if (fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE | PTX_FLAG_COUNT_WORK))
+    if (fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK))
         return 1;
     if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before rendering");
     if (!h->layout_valid) {
@@ -765,16 +765,10 @@ static int timed_launch(ptx_handle *h, int pass) {
     h->ring_pos = (h->ring_pos + 1) % kEventRing;
     resolve_event(t, h);
     Scene sc = make_scene(h);
-    // kernel variant: wavefront (default), tile + LDS ray exchange, persistent lanes, or one
-    // thread per pixel
+    // kernel variant: wavefront (default) or one thread per pixel (PTX_FLAG_SIMPLE_KERNELS: the
+    // independent per-pixel form the parity tests check the wavefront queues against)
     const uint32_t fl = h->cfg.flags;
-    const int variant = (fl & PTX_FLAG_SIMPLE_KERNELS)      ? 2
-                        : (fl & PTX_FLAG_PERSISTENT_LANES)  ? 1
-                        : (fl & PTX_FLAG_TILED_EXCHANGE)    ? 0
-                                                            : 3;
-    unsigned int *ctr = (unsigned int *)h->d_queue.p + pass;
-    if (variant == 1 && pass != PTX_PASS_GBUFFER)
-        HIP_CHECK(h, hipMemsetAsync(ctr, 0, sizeof(unsigned int), h->stream));
+    const int variant = (fl & PTX_FLAG_SIMPLE_KERNELS) ? 2 : 3;
     WaveBufs w{};
     const bool reuse_pass = pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL;
     if (reuse_pass && (variant != 3 || !has_reuse(h)))
@@ -809,19 +803,13 @@ static int timed_launch(ptx_handle *h, int pass) {
         h->surf_valid = false;
         break;
     case PTX_PASS_INIT:
-        e = variant == 0   ? launch_init_tiled(sc, gb, res, d, h->stream)
-            : variant == 1 ? launch_init_persistent(sc, gb, res, ctr, d, h->stream)
-                           : launch_init(sc, gb, res, d, h->stream);
+        e = launch_init(sc, gb, res, d, h->stream);
         break;
     case PTX_PASS_FINAL:
-        e = variant == 0   ? launch_final_tiled(sc, gb, res, acc, d, h->stream)
-            : variant == 1 ? launch_final_persistent(sc, gb, res, acc, ctr, d, h->stream)
-                           : launch_final(sc, gb, res, acc, d, h->stream);
+        e = launch_final(sc, gb, res, acc, d, h->stream);
         break;
     case PTX_PASS_MCPT:
-        e = variant == 0   ? launch_mcpt_tiled(sc, acc, d, h->stream)
-            : variant == 1 ? launch_mcpt_persistent(sc, acc, ctr, d, h->stream)
-                           : launch_mcpt(sc, acc, d, h->stream);
+        e = launch_mcpt(sc, acc, d, h->stream);
         break;
     default: return fail(h, PTX_E_INVALID, "unknown pass %d", pass);
     }
@@ -857,12 +845,13 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!cfg || !out) return PTX_E_INVALID;
     *out = nullptr;
     if (cfg->width == 0 || cfg->height == 0 || cfg->pipeline > PTX_PIPELINE_RESTIR_GI) return PTX_E_INVALID;
+    if (cfg->flags & PTX_FLAGS_RETIRED) return PTX_E_INVALID;  // the removed A/B kernel variants
     if ((cfg->pipeline == PTX_PIPELINE_RESTIR_REUSE || cfg->pipeline == PTX_PIPELINE_RESTIR_GI) &&
-        (cfg->flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE)))
+        (cfg->flags & (PTX_FLAG_SIMPLE_KERNELS)))
         return PTX_E_INVALID;  // the reuse passes exist in wavefront form only
     if (cfg->reuse_neighbors > 16u) return PTX_E_INVALID;
     if ((cfg->flags & PTX_FLAG_ROW_CENSUS) &&
-        (cfg->flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE)))
+        (cfg->flags & (PTX_FLAG_SIMPLE_KERNELS)))
         return PTX_E_INVALID;  // the census maps wavefront queue slots to tile rows
     ptx_handle *h = new (std::nothrow) ptx_handle();
     if (!h) return PTX_E_NOMEM;
@@ -1000,7 +989,7 @@ int ptx_run_passes(ptx_handle *h, const int *passes, int n) {
             return fail(h, PTX_E_INVALID, "the GI pipeline has no MCPT pass");
     }
     const uint32_t fl = h->cfg.flags;
-    if (fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE | PTX_FLAG_COUNT_WORK)) {
+    if (fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK)) {
         for (int i = 0; i < n; ++i)
             if (int rc = timed_launch(h, passes[i])) return rc;
         return PTX_OK;

@@ -142,8 +142,7 @@ BandSets band_sets(const ptx_handle *h, const WaveBufs &w) {
 // Layout, queue and reuse buffers of a band frame; 1 = not a wavefront band frame.
 int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w) {
     if (!has_reuse(h)) return fail(h, PTX_E_INVALID, "band frames need the reuse or GI pipeline");
-    if (h->cfg.flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_PERSISTENT_LANES | PTX_FLAG_TILED_EXCHANGE |
-                        PTX_FLAG_COUNT_WORK))
+    if (h->cfg.flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK))
         return fail(h, PTX_E_INVALID, "band frames run the wavefront kernels (no counting / A-B variants)");
     if (!h->scene_loaded || !h->frame_set) return fail(h, PTX_E_INVALID, "scene and frame must be set before rendering");
     if (!h->layout_valid)

@@ -19,24 +19,9 @@ hipError_t launch_final(const Scene &sc, const uint4 *gbuf, const uint4 *reservo
                         uint32_t stack_depth, hipStream_t s);
 hipError_t launch_mcpt(const Scene &sc, float4 *accum, uint32_t stack_depth, hipStream_t s);
 
-// persistent-lane variants (ptx_persist.hip); ctr = a zeroed u32 pixel-queue counter
-hipError_t launch_init_persistent(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, unsigned int *ctr,
-                                  uint32_t stack_depth, hipStream_t s);
-hipError_t launch_final_persistent(const Scene &sc, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
-                                   unsigned int *ctr, uint32_t stack_depth, hipStream_t s);
-hipError_t launch_mcpt_persistent(const Scene &sc, float4 *accum, unsigned int *ctr, uint32_t stack_depth,
-                                  hipStream_t s);
-
 // closest-hit queries for a ray array (ptx_kernels.hip)
 hipError_t launch_trace_rays(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
                              uint32_t stack_depth, hipStream_t s);
-
-// tile + LDS ray-exchange variants (ptx_persist.hip): A/B
-hipError_t launch_init_tiled(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, uint32_t stack_depth,
-                             hipStream_t s);
-hipError_t launch_final_tiled(const Scene &sc, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
-                              uint32_t stack_depth, hipStream_t s);
-hipError_t launch_mcpt_tiled(const Scene &sc, float4 *accum, uint32_t stack_depth, hipStream_t s);
 
 // wavefront variant (ptx_wave.hip): the default.  A pass is a fixed sequence of rounds:
 // logic round 0 (start), then {trace r, logic r+1} for r < kWaveRounds[pass].  Every

@@ -27,7 +27,7 @@ const PIPELINE = { restir: 0, mcpt: 1, reuse: 2, gi: 3 };
 const PASS = { GBUFFER: 0, INIT: 1, FINAL: 2, MCPT: 3, TRACE: 4, WAVE_TRACE: 5, WAVE_LOGIC: 6, FRAME: 7,
   TEMPORAL: 8, SPATIAL: 9, PASS_GROUP: 10 };
 const BUF = { GBUFFER: 0, RESERVOIR: 1, ACCUM: 2, COUNTERS: 3, RESERVOIR_HIST: 4 };
-const FLAGS = { COUNT_WORK: 1, SIMPLE_KERNELS: 2, PERSISTENT_LANES: 4, TILED_EXCHANGE: 8, TIME_LAUNCHES: 16 };
+const FLAGS = { COUNT_WORK: 1, SIMPLE_KERNELS: 2, TIME_LAUNCHES: 16 };
 const UNIFORM_WORDS = 33;
 
 /** The 33-word uniform block of Renderer_TEST.Update (Renderer_TEST.ts:165-206). */

@@ -38,6 +38,9 @@ def test_create_rejects_bad_config_without_touching_gpu():
     assert lib.ptx_create(ctypes.byref(bad), ctypes.byref(h)) == -1
     assert lib.ptx_last_error(None) == b"null handle"
     assert lib.ptx_render(None, None) == -1
+    for retired in (4, 8):  # the removed persistent-lane / tiled A/B variants
+        bad = N.PtxConfig(width=16, height=16, flags=retired, device=0)
+        assert lib.ptx_create(ctypes.byref(bad), ctypes.byref(h)) == -1 and not h.value
 
 
 def test_band_partition():
