@@ -433,29 +433,31 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
             // IS the reference's test of that root (same function, same arguments)
             const float vy_pf = vy;
             for (;;) {
-                while (leaf == 0u && (sp >= 0 || mask != 0u)) {
-                    if (PROF) pf.hit(PROF_NODE);
-                    if (sp < 0) {
+                // One wave-uniform loop; per iteration a lane with an empty stack takes its next
+                // root and a lane with a stack pops -- and a root that passes its test IS the
+                // lane's next node (its push + pop folded), tested in the same iteration.  Per
+                // lane the root tests, pops, tests and pushes are the reference's sequence.
+                for (;;) {
+                    if (__ballot(leaf == 0u && (sp >= 0 || mask != 0u)) == 0ull) break;
+                    if (PROF && leaf == 0u && (sp >= 0 || mask != 0u)) pf.hit(PROF_NODE);
+                    uint32_t ref = 0u;
+                    bool node = false;
+                    if (leaf == 0u && sp < 0 && mask != 0u) {
                         const uint32_t k = (uint32_t)__builtin_ctz(mask);
                         mask &= mask - 1u;
                         const SubRoot &R = roots[s0 + k];
                         if ((ROOTQ && vy == vy_pf) || box_root(lo, inv, R, vx, vy)) {
                             grp = s0 + k;
-                            if (R.ref & LEAF_BIT) {  // a one-leaf root: its push + pop, folded
-                                leaf = R.ref;
-                                break;
-                            }
-                            stack[0] = R.ref;
-                            sp = 0;
+                            if (R.ref & LEAF_BIT) leaf = R.ref;  // a one-leaf root
+                            else { ref = R.ref; node = true; }
                         }
-                        continue;
+                    } else if (leaf == 0u && sp >= 0) {
+                        ref = stack[(uint32_t)sp * stride];
+                        --sp;
+                        if (ref & LEAF_BIT) leaf = ref;
+                        else node = true;
                     }
-                    const uint32_t ref = stack[(uint32_t)sp * stride];
-                    --sp;
-                    if (ref & LEAF_BIT) {
-                        leaf = ref;
-                        break;
-                    }
+                    if (!node) continue;
                     const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + ref);
                     float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
                     uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
