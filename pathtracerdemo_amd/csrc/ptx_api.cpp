@@ -322,11 +322,10 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     // streams (e.g. one half's spatial pass beside the other half's PT_4)
     w.act_stride = (uint32_t)(seg_px * jpp);
     w.cnt = (uint32_t *)h->d_wctr.p;
-    // measured per pipeline: 4 waves per SIMD (no spill) for the reference
-    // pipeline / TEST_MCPT and the reuse pipeline, 5 for ReSTIR GI -- and for bands of more than
-    // 4 Mpx (a 3840x2160 frame on one GPU: 394.2 vs 391.8 Msamples/s, trace roofline 0.553 vs
-    // 0.532; its launches are large enough that a fifth wave beats the spill)
-    w.trace_waves = (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI || npix > ((size_t)4u << 20)) ? 5u : 4u;
+    // measured (with the flat node loop): 4 waves per SIMD (no spill) for every
+    // pipeline at 1080p (GI 720 vs 714 Msamples/s at 5), 5 for bands of more than 4 Mpx (a
+    // 3840x2160 frame on one GPU: 414.6 vs 413.9 Msamples/s, trace roofline 0.611 vs 0.597)
+    w.trace_waves = npix > ((size_t)4u << 20) ? 5u : 4u;
     static const uint32_t env_split = getenv("PTX_TRACE_SPLIT") ? (uint32_t)atoi(getenv("PTX_TRACE_SPLIT")) : 0u;
     w.trace_split = env_split >= 1u && env_split <= 16u ? env_split : 1u;
     w.seg_base = 0;

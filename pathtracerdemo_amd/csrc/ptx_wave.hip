@@ -1077,9 +1077,9 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
     else {
         // Occupancy target per pipeline (WaveBufs::trace_waves), LDS-staged tables; A/B
         // switches PTX_TRACE_OCC / PTX_TRACE_NOLDS.  Measured at 1080p with 768-pixel segments:
-        // 4 waves/SIMD (no spill) is fastest for the reference pipeline, TEST_MCPT and reuse
-        // (+2 %, +0-2.6 %, +1.7 % over 5), 5 (96 VGPRs, 48-64 B/lane spill) for ReSTIR GI
-        // (+1.7 % over 4); 6+ spills in the traversal loop.
+        // 4 waves/SIMD (no spill) is fastest for every pipeline (with the flat node loop: reuse
+        // 369-373 vs 339-340, ReSTIR 1301 vs 1235, TEST_MCPT 1359 vs 1261, GI 720 vs 714 at 5,
+        // which spills 48-64 B/lane); 5 only for bands above 4 Mpx; 6+ spills in the node loop.
         static const int env_occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 0;
         const int occ = env_occ ? env_occ : w.trace_waves == 4u ? 4 : 5;
         const bool tables_fit = tables_fit_lds(sc) && !getenv("PTX_TRACE_NOLDS");
