@@ -361,14 +361,23 @@ __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, Pa
 // (atomic loads / stores for the keys: plain accesses would let the compiler assume no
 // other lane writes them).
 struct CoopLds { unsigned long long *key; };  // 64 entries per wave
+// Inclusive prefix sum over the 64 lanes of the wave (every lane active) in six DPP adds: a
+// Hillis-Steele scan inside each row of 16 lanes (row_shr 1, 2, 4, 8; lanes shifted in from
+// outside the row add 0), then row 15's sum broadcast into rows 1 and 3 and row 31's into
+// rows 2 and 3 (row_bcast).  No LDS round trips (__shfl_up is a ds_bpermute each step).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    uint32_t t = v;
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x111, 0xf, 0xf, false);  // row_shr:1
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x112, 0xf, 0xf, false);  // row_shr:2
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x114, 0xf, 0xf, false);  // row_shr:4
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x118, 0xf, 0xf, false);  // row_shr:8
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return t;
+}
 __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t &total) {
-    const uint32_t lane = __lane_id();
-    uint32_t incl = v;
-    for (uint32_t o = 1u; o < 64u; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
-    total = __shfl(incl, 63);
+    const uint32_t incl = wave_incl_scan(v);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     return incl - v;
 }
 template <bool COUNT, bool PROF = false, bool ROOTQ = true, bool ANY = false, bool COOP = false>

@@ -16,16 +16,7 @@ enum : uint32_t { Q_CLOSEST = 0u, Q_VIS = 1u, Q_OCC = 2u };
 
 // ---------------------------------------------------------------- wave helpers
 // Exclusive prefix sum of `v` over the wave and the wave total.
-__device__ __forceinline__ uint32_t wave_scan(uint32_t v, uint32_t &total) {
-    const uint32_t lane = __lane_id();
-    uint32_t incl = v;
-    for (uint32_t o = 1u; o < 64u; o <<= 1) {
-        uint32_t t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
-    total = __shfl(incl, 63);
-    return incl - v;
-}
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v, uint32_t &total) { return wave_excl_sum(v, total); }
 // Reserve `n` consecutive slots of this workgroup's segment (one LDS atomic per wave).
 // Must be reached by every lane of the wave.
 __device__ __forceinline__ uint32_t wave_alloc(uint32_t *lds_ctr, uint32_t n) {
@@ -33,7 +24,7 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t *lds_ctr, uint32_t n) {
     const uint32_t excl = wave_scan(n, total);
     uint32_t base = 0u;
     if (__lane_id() == 0u && total) base = atomicAdd(lds_ctr, total);
-    base = __shfl(base, 0);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);  // (lane 0 is active: every lane is)
     return base + excl;
 }
 
