@@ -37,6 +37,15 @@ void free_buf(DevBuf &b) {
     b.p = nullptr;
     b.bytes = 0;
 }
+// Fill device memory and wait for it: every stream of a handle is non-blocking, so a plain
+// hipMemset (null stream) is NOT ordered before their kernels -- a fill still in flight when a
+// frame starts overwrites what the frame wrote (seen as a reuse mismatch when another handle
+// kept the null stream busy).  Used for the one-time clears.
+static hipError_t memset_sync(void *p, int value, size_t bytes) {
+    hipError_t e = hipMemsetAsync(p, value, bytes, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    return e;
+}
 int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
     if (b.bytes == bytes && b.p) return PTX_OK;
     free_buf(b);
@@ -44,12 +53,17 @@ int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
     hipError_t e = hipMalloc(&b.p, bytes);
     if (e != hipSuccess) return fail(h, PTX_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
     b.bytes = bytes;
+    // diagnostics: PTX_DEBUG_FILL=<byte> fills every new buffer with that byte (an
+    // uninitialised read then shows up as a parity failure)
+    static const int fill = getenv("PTX_DEBUG_FILL") ? atoi(getenv("PTX_DEBUG_FILL")) : -1;
+    if (fill >= 0) HIP_CHECK(h, memset_sync(b.p, fill & 0xff, bytes));
     return PTX_OK;
 }
 static int upload(ptx_handle *h, DevBuf &b, const void *src, size_t bytes) {
     int rc = alloc_buf(h, b, std::max<size_t>(bytes, 16));
     if (rc) return rc;
     if (bytes) HIP_CHECK(h, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    if (bytes) HIP_CHECK(h, hipStreamSynchronize(nullptr));  // (null-stream copy done before any handle stream reads it)
     return PTX_OK;
 }
 
@@ -679,11 +693,11 @@ static int ensure_alt(ptx_handle *h) {
     DevBuf &g = h->alt_active ? h->d_gbuf : a.gbuf, &r = h->alt_active ? h->d_res : a.res;
     if (!g.p) {
         if (int rc = alloc_buf(h, g, h->d_gbuf.bytes ? h->d_gbuf.bytes : a.gbuf.bytes)) return rc;
-        HIP_CHECK(h, hipMemset(g.p, 0, g.bytes));
+        HIP_CHECK(h, memset_sync(g.p, 0, g.bytes));
     }
     if (!r.p) {
         if (int rc = alloc_buf(h, r, h->d_res.bytes ? h->d_res.bytes : a.res.bytes)) return rc;
-        HIP_CHECK(h, hipMemset(r.p, 0, r.bytes));
+        HIP_CHECK(h, memset_sync(r.p, 0, r.bytes));
     }
     return PTX_OK;
 }
@@ -892,11 +906,11 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!rc) rc = alloc_buf(h, h->d_res, px_halo * 16u * h->res_u4);
     if (!rc && has_reuse(h)) {
         rc = alloc_buf(h, h->d_hist, px * 16u * h->res_u4);
-        if (!rc && hipMemset(h->d_hist.p, 0, h->d_hist.bytes) != hipSuccess) rc = PTX_E_HIP;
+        if (!rc && memset_sync(h->d_hist.p, 0, h->d_hist.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
     if (!rc && h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {
         rc = alloc_buf(h, h->d_direct, px * 16u);
-        if (!rc && hipMemset(h->d_direct.p, 0, h->d_direct.bytes) != hipSuccess) rc = PTX_E_HIP;
+        if (!rc && memset_sync(h->d_direct.p, 0, h->d_direct.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
     if (!rc) rc = alloc_buf(h, h->d_accum, px * 16u);
     if (!rc) rc = alloc_buf(h, h->d_counters, kCounterWords * 8u);
@@ -906,18 +920,18 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
         const size_t tile_rows = (h->band_h + 7u) / 8u, tiles = tile_rows * ((h->cfg.width + 7u) / 8u);
         h->census_blocks = (uint32_t)(tile_rows + tiles * 64u / 256u + 2u);
         rc = alloc_buf(h, h->d_census, (size_t)h->census_blocks * kCensusWords * 8u);
-        if (!rc && hipMemset(h->d_census.p, 0, h->d_census.bytes) != hipSuccess) rc = PTX_E_HIP;
+        if (!rc && memset_sync(h->d_census.p, 0, h->d_census.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
 #ifdef PTX_WG_TIMES
     if (!rc && getenv("PTX_WGT")) {  // 4 header words + 2^20 records of 4 words
         rc = alloc_buf(h, h->d_wgt, (4u + 4u * (1u << 20)) * 8u);
-        if (!rc && hipMemset(h->d_wgt.p, 0, 32u) != hipSuccess) rc = PTX_E_HIP;
+        if (!rc && memset_sync(h->d_wgt.p, 0, 32u) != hipSuccess) rc = PTX_E_HIP;
     }
 #endif
-    if (!rc && hipMemset(h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
-    if (!rc && hipMemset(h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;
-    if (!rc && hipMemset(h->d_gbuf.p, 0, h->d_gbuf.bytes) != hipSuccess) rc = PTX_E_HIP;
-    if (!rc && hipMemset(h->d_res.p, 0, h->d_res.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && memset_sync(h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && memset_sync(h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && memset_sync(h->d_gbuf.p, 0, h->d_gbuf.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && memset_sync(h->d_res.p, 0, h->d_res.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (rc) {
         ptx_destroy(h);
         return rc;
@@ -1141,8 +1155,8 @@ int ptx_reset_stats(ptx_handle *h) {
     HIP_CHECK(h, hipStreamSynchronize(h->stream));
     for (int p = 0; p < kPasses; ++p) { h->ms_total[p] = 0.0; h->launches[p] = 0; }
     h->frames = 0;
-    HIP_CHECK(h, hipMemset(h->d_counters.p, 0, h->d_counters.bytes));
-    if (h->d_census.p) HIP_CHECK(h, hipMemset(h->d_census.p, 0, h->d_census.bytes));
+    HIP_CHECK(h, memset_sync(h->d_counters.p, 0, h->d_counters.bytes));
+    if (h->d_census.p) HIP_CHECK(h, memset_sync(h->d_census.p, 0, h->d_census.bytes));
     return PTX_OK;
 }
 
@@ -1157,7 +1171,7 @@ int ptx_diag_wave_times(ptx_handle *h, uint64_t *out, size_t max_records) {
     HIP_CHECK(h, hipMemcpy(&n, h->d_wgt.p, 8, hipMemcpyDeviceToHost));
     n = std::min<uint64_t>(std::min<uint64_t>(n, 1u << 20), max_records);
     if (n && out) HIP_CHECK(h, hipMemcpy(out, (uint64_t *)h->d_wgt.p + 4, n * 32u, hipMemcpyDeviceToHost));
-    HIP_CHECK(h, hipMemset(h->d_wgt.p, 0, 8));
+    HIP_CHECK(h, memset_sync(h->d_wgt.p, 0, 8));
     return (int)n;
 }
 #endif

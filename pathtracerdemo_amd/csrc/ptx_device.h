@@ -354,13 +354,13 @@ __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, Pa
 // out 64 at a time, each lane testing one (lane, triangle) pair with the owning lane's ray
 // and bound.  A leaf's sequential loop (`if (best < t) continue`: ties replace) ends with the
 // minimum accepted t and the LAST triangle reaching it, which is exactly a min over the key
-// (t bits, ~k) -- t > 0, so its bits order like the floats -- taken with an LDS atomic per
+// (t bits, ~triangle index) -- t > 0, so its bits order like the floats -- taken with an LDS atomic per
 // owner.  Every lane's own walk (pops, pushes, bound, counts) is unchanged; a NaN t (which
 // the sequential loop accepts and then poisons the bound with) sends the phase through the
 // sequential loop instead.  Cross-lane data moves only through shuffles and LDS atomics
 // (atomic loads / stores for the keys: plain accesses would let the compiler assume no
 // other lane writes them).
-struct CoopLds { unsigned long long *key; };  // 64 entries per wave
+struct CoopLds { unsigned long long *key; uint32_t *mark; };  // 64 entries of each per wave
 // Inclusive prefix sum over the 64 lanes of the wave (every lane active) in six DPP adds: a
 // Hillis-Steele scan inside each row of 16 lanes (row_shr 1, 2, 4, 8; lanes shifted in from
 // outside the row add 0), then row 15's sum broadcast into rows 1 and 3 and row 31's into
@@ -373,6 +373,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x118, 0xf, 0xf, false);  // row_shr:8
     t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x142, 0xa, 0xf, false);  // row_bcast:15
     t += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return t;
+}
+// Inclusive prefix maximum over the wave, the same six DPP steps (lanes shifted in add 0).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    uint32_t t = v;
+    t = max(t, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x111, 0xf, 0xf, false));
+    t = max(t, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x112, 0xf, 0xf, false));
+    t = max(t, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x114, 0xf, 0xf, false));
+    t = max(t, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x118, 0xf, 0xf, false));
+    t = max(t, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x142, 0xa, 0xf, false));
+    t = max(t, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x143, 0xc, 0xf, false));
     return t;
 }
 __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t &total) {
@@ -496,26 +507,35 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                     bool nan_seen = false;
                     for (uint32_t c0 = 0; c0 < total; c0 += 64u) {
                         const uint32_t u = c0 + lane;
-                        // owner of triangle u = the last lane whose exclusive count is <= u
-                        // (it holds a nonempty leaf: the next lane's count start is > u)
-                        int owner = 0;
-                        for (int step = 32; step >= 1; step >>= 1) {
-                            const uint32_t e = __shfl(excl, owner + step);
-                            if (e <= u) owner += step;
-                        }
-                        const uint32_t o_excl = __shfl(excl, owner), o_first = __shfl(lfirst, owner);
+                        // owner of triangle u = the last lane with a nonempty leaf whose
+                        // exclusive count is <= u: each such lane whose leaf starts inside this
+                        // chunk marks its start position (lane + 1; starts are distinct and
+                        // ascend with the lane), position 0 also takes the last owner that
+                        // started before the chunk, and a prefix maximum over the positions
+                        // carries every mark forward
+                        __hip_atomic_store(&coop.mark[lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                        if (cnt != 0u && excl >= c0 && excl - c0 < 64u)
+                            __hip_atomic_store(&coop.mark[excl - c0], lane + 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                        uint32_t m = __hip_atomic_load(&coop.mark[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        const unsigned long long before = __ballot(cnt != 0u && excl < c0);
+                        if (lane == 0u && before != 0ull) m = max(m, 64u - (uint32_t)__builtin_clzll(before));
+                        const int owner = (int)wave_incl_max(m) - 1;
+                        // triangle u of the deal is the owner's leaf triangle lfirst + (u - excl)
+                        const uint32_t tri = u + __shfl(lfirst - excl, owner);
                         const f3 olo = mk(__shfl(lo.x, owner), __shfl(lo.y, owner), __shfl(lo.z, owner));
                         const f3 old = mk(__shfl(ld.x, owner), __shfl(ld.y, owner), __shfl(ld.z, owner));
                         const float ovy = __shfl(vy, owner);
                         if (u < total) {
                             if (PROF) pf.hit(PROF_TRI);
-                            const uint32_t k = u - o_excl;
-                            const float4 *tp = tris + 3u * (o_first + k);
+                            const float4 *tp = tris + 3u * tri;
                             const float t = ray_tri(olo, old, tp[0], tp[1], tp[2], eps.det_eps);
                             if (t != t) nan_seen = true;
                             else if (!(ovy < t))
                                 atomicMin(&coop.key[owner], ((unsigned long long)__float_as_uint(t) << 32) |
-                                                                (unsigned long long)(0xffffffffu - k));
+                                                                (unsigned long long)(0xffffffffu - tri));
                         }
                     }
                     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -529,7 +549,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                                 best.valid = true;
                                 best.s.inst = ii;
                                 best.s.mat = grp;
-                                best.s.prim = lfirst + (0xffffffffu - (uint32_t)key);
+                                best.s.prim = 0xffffffffu - (uint32_t)key;
                                 if (ANY) {  // occluded: no more work for this lane
                                     stop = true;
                                     sp = -1;

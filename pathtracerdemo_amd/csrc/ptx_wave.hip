@@ -138,7 +138,8 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     uint32_t *pref = wstack + tw;
     uint32_t *stack = wstack + tw + (dyn ? dyn_prefix_words(w) : 0u) + threadIdx.x;
     __shared__ unsigned long long c_key[WB];
-    const CoopLds coop{c_key + (threadIdx.x & ~63u)};
+    __shared__ uint32_t c_mark[WB];
+    const CoopLds coop{c_key + (threadIdx.x & ~63u), c_mark + (threadIdx.x & ~63u)};
     if (dyn) {
         dyn_prefix(w, round, pref);
         const uint32_t total = pref[w.seg_count];

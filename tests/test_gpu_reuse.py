@@ -277,3 +277,29 @@ def test_pipelined_frames_interleaved_with_host_ops(scene3, oracle_mod, native):
     assert_same(r.read_history(), fr.res_hist, "spatial output")
     assert_same(r.read_image(), fr.accum, "accumulated radiance")
     r.close()
+
+
+def test_pipelined_frames_beside_another_handle(scene1, scene3, oracle_mod):
+    """A reuse handle created while another handle is alive (smoke()'s order): its one-time
+    clears must be done before its non-blocking streams start (a null-stream hipMemset still
+    in flight once zeroed part of the first pipelined frame's reservoirs)."""
+    from pathtracerdemo_amd.renderer import Renderer
+    O = oracle_mod
+    other = Renderer(64, 64, device=0)
+    other.Initialize(scene1)
+    other.Update()
+    other.Render()
+    other.read_image()
+    W, H = 48, 32
+    fr = oracle_frame(O, scene3, W, H)
+    r = reuse_renderer(scene3, W, H)
+    for f in (1, 2, 3):
+        fr.set_frame_index(f)
+        fr.run_reuse_frame(threads=8)
+        r.Update()
+        r.Render()
+    assert_same(r.read_reservoir(), fr.reservoir, "temporal output")
+    assert_same(r.read_history(), fr.res_hist, "spatial output")
+    assert_same(r.read_image(), fr.accum, "accumulated radiance")
+    r.close()
+    other.close()
