@@ -159,7 +159,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         const uint32_t G = w.trace_split;
         uint32_t bnext = 0u;
         if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
-        uint32_t bi = c0 + G * __shfl(bnext, 0);
+        uint32_t bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
         for (;;) {  // wave-uniform
             if (bi >= c1) {  // this chunk is drained: the next head
                 if (++visited == kDynHeads) break;
@@ -167,7 +167,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                 c0 = (uint32_t)((uint64_t)total * x / kDynHeads);
                 c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
                 if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
-                bi = c0 + G * __shfl(bnext, 0);
+                bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
                 continue;
             }
             if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);  // the next dequeue, fetched ahead
@@ -187,7 +187,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                                               w.rays + 2u * (size_t)j * w.ray_stride,
                                               w.res[round & 1u] + 2u * (size_t)j * w.ray_stride, i, i < n);
             }
-            bi = c0 + G * __shfl(bnext, 0);
+            bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
         }
         return;
     }
