@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--halo", choices=["rccl", "torch"], default="rccl",
                     help="halo exchange: the handle's own RCCL communicator, or torch.distributed "
                          "(host-driven, the CPU tests' path)")
+    ap.add_argument("--no-calibrate", dest="calibrate", action="store_false",
+                    help="strong scaling: keep the census bands (default: re-cut them from each band's "
+                         "measured frame time, untimed, before the run)")
     ap.add_argument("--halo-overlap", action="store_true",
                     help="spatial pass of the interior rows while the halo is in flight")
     ap.add_argument("--scene", default=None, help="default: c3_interior_32 (reuse), dummy_scene_1 (others)")
@@ -132,6 +135,34 @@ def census(cs, W, H, pipeline, device, passes):
         out[p] = rc.row_census().astype(np.float64)
     rc.close()
     return out
+
+
+def calibrate_band(cs, W, H, pipeline, device, row_begin, row_end, passes, frames=4):
+    """ms per frame of rows [row_begin, row_end) rendered alone on this rank's GPU (no halo
+    exchange; the pass groups of a band frame), after two untimed frames -- the measured
+    band cost the strong split is re-cut from (bands.recalibrated_costs)."""
+    from pathtracerdemo_amd import _native as N
+    from pathtracerdemo_amd.renderer import Renderer
+    pid = {"gbuffer": N.PTX_PASS_GBUFFER, "init": N.PTX_PASS_INIT, "final": N.PTX_PASS_FINAL,
+           "mcpt": N.PTX_PASS_MCPT, "temporal": N.PTX_PASS_TEMPORAL, "spatial": N.PTX_PASS_SPATIAL}
+    ids = [pid[p] for p in passes]
+    cut = ids.index(N.PTX_PASS_SPATIAL) if N.PTX_PASS_SPATIAL in ids else len(ids)
+    front, back = ids[:cut], ids[cut:]
+    r = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end)
+    r.Initialize(cs)
+    t0 = 0.0
+    for it in range(2 + frames):
+        if it == 2:
+            r.synchronize()
+            t0 = time.perf_counter()
+        r.Update()
+        r.run_passes(front)
+        if back:
+            r.run_passes(back)
+    r.synchronize()
+    ms = (time.perf_counter() - t0) / frames * 1e3
+    r.close()
+    return ms
 
 
 def band_work(tile_census: np.ndarray, row_begin: int, row_end: int) -> dict:
@@ -183,6 +214,7 @@ def main():
     # cost-balanced bands of a strong-scaled frame
     cen = census(cs, W, H, pipeline, device, passes)
     radius = 30
+    calib = None
     if strong and world > 1:
         if args.bands == "balanced":
             total = sum(cen.values())
@@ -192,6 +224,21 @@ def main():
             all_bands = [B.band(H, world, r) for r in range(world)]
             costs = B.row_costs(sum(cen.values()), W, H)
         balance = B.band_balance(costs, all_bands)
+        if args.bands == "balanced" and args.calibrate and dist is not None:
+            # time every rank's band alone (no exchange), gather, rescale the row costs by
+            # measured / predicted band cost and cut again (bands.recalibrated_costs); twice
+            calib = {"rounds": []}
+            for _ in range(2):
+                b0, b1 = all_bands[rank]
+                cal = calibrate_band(cs, W, H, pipeline, device, b0, b1, passes)
+                gathered = [None] * world
+                dist.all_gather_object(gathered, cal)
+                calib["rounds"].append({"bands": [list(b) for b in all_bands],
+                                        "band_ms": [round(v, 4) for v in gathered],
+                                        "measured_max_over_mean": round(max(gathered) / (sum(gathered) / world), 4)})
+                costs = B.recalibrated_costs(costs, all_bands, gathered)
+                all_bands = B.balanced_bands(costs, world, min_rows=radius)
+                balance = B.band_balance(costs, all_bands)
     else:
         all_bands = [B.weak_band(H // world, r) for r in range(world)]
         balance = 1.0
@@ -384,6 +431,8 @@ def main():
     if world > 1:
         line["bands"] = {"rows": [list(b) for b in all_bands], "split": args.bands if strong else "weak",
                          "predicted_max_over_mean": round(balance, 4), "ms_per_frame_by_rank": band_ms}
+        if calib is not None:
+            line["bands"]["calibration"] = calib
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

@@ -205,3 +205,25 @@ def test_c4_cost_balanced_bands_within_ten_percent(scene3, oracle_mod):
     assert got <= 1.1, (got, bal)
     assert eq > got
     assert all(e - b >= 30 for b, e in bal) and bal[0][0] == 0 and bal[-1][1] == 2160
+
+
+def test_recalibrated_costs_rebalance_measured_bands():
+    """Bands re-cut from measured band times: each band's rescaled cost is its measured time,
+    rows keep their census shape inside it, and the re-cut bands even out the rescaled cost."""
+    import numpy as np
+    from pathtracerdemo_amd.bands import balanced_bands, band_balance, recalibrated_costs
+    H, world = 2160, 8
+    rng = np.random.default_rng(3)
+    census = rng.uniform(0.5, 1.5, H)
+    truth = census * np.where((np.arange(H) > 800) & (np.arange(H) < 1300), 3.0, 1.0)  # a slow middle
+    bands = balanced_bands(census, world, min_rows=30)
+    ms = [float(truth[b0:b1].sum()) for b0, b1 in bands]
+    assert max(ms) / np.mean(ms) > 1.5  # the census cut is badly off on the truth
+    c = recalibrated_costs(census, bands, ms)
+    for (b0, b1), t in zip(bands, ms):
+        assert abs(c[b0:b1].sum() - t) < 1e-6 * t
+    re = balanced_bands(c, world, min_rows=30)
+    assert band_balance(truth, re) < 1.15  # one round gets close ...
+    ms2 = [float(truth[b0:b1].sum()) for b0, b1 in re]
+    re2 = balanced_bands(recalibrated_costs(c, re, ms2), world, min_rows=30)
+    assert band_balance(truth, re2) < 1.05  # ... and a second round closer
