@@ -226,9 +226,10 @@ def main():
         balance = B.band_balance(costs, all_bands)
         if args.bands == "balanced" and args.calibrate and dist is not None:
             # time every rank's band alone (no exchange), gather, rescale the row costs by
-            # measured / predicted band cost and cut again (bands.recalibrated_costs); twice
+            # measured / predicted band cost and cut again (bands.recalibrated_costs); a band's
+            # time is not additive in its rows (per-band launch tails), so three rounds
             calib = {"rounds": []}
-            for _ in range(2):
+            for _ in range(3):
                 b0, b1 = all_bands[rank]
                 cal = calibrate_band(cs, W, H, pipeline, device, b0, b1, passes)
                 gathered = [None] * world
