@@ -67,8 +67,9 @@ def ray_bytes(c: dict) -> int:
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1,
-                    help="ranks (one GPU each); spawned by bench.py itself unless run under torchrun")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each; default 1, or WORLD_SIZE under torchrun); spawned by bench.py "
+                         "itself unless run under torchrun")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["reuse", "restir", "mcpt", "gi"], default="reuse")
@@ -91,7 +92,9 @@ def parse():
     ap.add_argument("--halo-overlap", action="store_true",
                     help="spatial pass of the interior rows while the halo is in flight")
     ap.add_argument("--scene", default=None, help="default: c3_interior_32 (reuse), dummy_scene_1 (others)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="C-oracle CPU baseline threads (default: every logical CPU of the host, os.cpu_count(); "
+                         "a 16-thread figure is reported beside it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", choices=["wave", "simple"], default="wave",
                     help="kernel variant (A/B): wavefront queues, or 1 thread/pixel")
@@ -178,6 +181,8 @@ def band_work(tile_census: np.ndarray, row_begin: int, row_end: int) -> dict:
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is None:  # under torchrun the launcher's world size is the GPU count
+        args.gpus = world
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     if world != args.gpus:
@@ -304,6 +309,15 @@ def main():
     st = r.stats()
     img = r.read_image()
     nonfinite = int((~np.isfinite(img[..., :3])).sum())
+    frames_rendered = args.warmup + args.steps
+    # multi-rank self-check: each rank's band (radiance + spatial output after every frame it
+    # rendered) is hashed here and compared on rank 0 with the same rows of ONE handle of the
+    # whole frame rendered the same number of frames (bands are bit-identical by design)
+    band_digest = None
+    if reuse and world > 1 and strong:
+        import hashlib
+        band_digest = hashlib.sha256(img.tobytes() + r.read_history().tobytes()).hexdigest()
+    comm = r.comm_info() if use_comm else None
     r.close()
 
     # Second timed region, same K steps, with HIP events around every wavefront launch
@@ -327,18 +341,25 @@ def main():
         st_k = rk.stats()
         rk.close()
 
-    # per-rank band times (rank 0 reports them all)
+    # per-rank band times, communicators and band digests (rank 0 reports them all)
     band_ms = [own_elapsed / args.steps * 1e3]
+    ranks_info = None
     if dist is not None:
         import torch
         t = torch.zeros(world, dtype=torch.float64, device=f"cuda:{device}" if backend == "nccl" else "cpu")
         t[rank] = own_elapsed / args.steps * 1e3
         dist.all_reduce(t)
         band_ms = [round(float(v), 4) for v in t.tolist()]
+        ranks_info = [None] * world
+        dist.all_gather_object(ranks_info, {"rank": rank, "device": device, "rows": [row_begin, row_end],
+                                            "comm": comm, "digest": band_digest})
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
+    parity = None
+    if band_digest is not None:
+        parity = one_handle_check(cs, W, H, pipeline, device, frames_rendered, ranks_info)
     samples = W * H * args.steps  # all ranks, 1 spp
     value = samples / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
@@ -391,8 +412,13 @@ def main():
             traffic = None
     cpu = ts_cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads)
-        ts_cpu = ts_cpu_baseline(cs, args.scene, W, Hb, args.cpu_threads)
+        cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads or (os.cpu_count() or 1))
+        ts_cpu = ts_cpu_baseline(cs, args.scene, W, Hb, 16, rows=Hb)
+    # configs[3]'s 3840x2160 frame on this one GPU: the single-GPU reference of the strong
+    # split the N > 1 lines run (their per-GPU efficiency is value_N / (N x this value))
+    one_gpu_4k = None
+    if world == 1 and pipeline == "reuse" and (W, H) == (1920, 1080) and args.variant == "wave":
+        one_gpu_4k = one_gpu_rate(cs, 3840, 2160, pipeline, device, max(5, args.steps // 2), args.warmup)
     if world > 1:
         workload = (f"{args.scene} {pipeline} {W}x{H} split over {world} GPUs, 1 spp/frame (configs[3])"
                     if strong else f"{args.scene} {pipeline} {W}x{Hb} per GPU, 1 spp/frame")
@@ -403,7 +429,7 @@ def main():
         "metric": "Msamples/sec at 1920x1080, 1 spp ReSTIR DI; per-pixel L2 vs WebGPU ref",
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "scaling": "strong" if strong or world == 1 else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": workload,
                    "pipeline": {"restir": "PT_01 gbuffer -> PT_1 init -> PT_4 final",
                                 "reuse": "PT_01 gbuffer -> PT_1 init -> temporal -> spatial (3 neighbours, "
@@ -429,14 +455,66 @@ def main():
         "cpu_baseline": cpu,
         "ts_cpu_baseline": ts_cpu,
     }
+    if world == 1:
+        line["scaling_note"] = ("one GPU: configs[2]'s frame; `--gpus N` splits configs[3]'s 3840x2160 frame into N "
+                                "row bands (strong); configs3_one_gpu is that frame on this one GPU")
+    if one_gpu_4k is not None:
+        line["configs3_one_gpu"] = one_gpu_4k
     if world > 1:
         line["bands"] = {"rows": [list(b) for b in all_bands], "split": args.bands if strong else "weak",
                          "predicted_max_over_mean": round(balance, 4), "ms_per_frame_by_rank": band_ms}
         if calib is not None:
             line["bands"]["calibration"] = calib
+        line["ranks"] = [{k: v for k, v in ri.items() if k != "digest"} for ri in ranks_info]
+        if parity is not None:
+            line["parity_check"] = parity
+    # any PTX_* switch in the environment (PTX_AB selects A/B kernel variants: unset = product)
+    line["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("PTX_")}
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def one_handle_check(cs, W, H, pipeline, device, frames, ranks_info):
+    """Rank 0, after the timed regions: ONE handle of the whole W x H frame renders `frames`
+    frames and the rows of every rank's band must hash to that rank's digest (radiance +
+    spatial output, bit for bit)."""
+    import hashlib
+    from pathtracerdemo_amd.renderer import Renderer
+    one = Renderer(W, H, device=device, pipeline=pipeline)
+    one.Initialize(cs)
+    for _ in range(frames):
+        one.Update()
+        one.Render()
+    img, hist = one.read_image(), one.read_history()
+    one.close()
+    bad = [ri["rank"] for ri in ranks_info
+           if hashlib.sha256(img[ri["rows"][0]:ri["rows"][1]].tobytes() +
+                             hist[ri["rows"][0]:ri["rows"][1]].tobytes()).hexdigest() != ri["digest"]]
+    return {"bands_bit_identical_to_one_handle": not bad, "ranks_differing": bad, "frames": frames,
+            "compared": "radiance + spatial-output reservoirs of every band vs the same rows of one "
+                        f"{W}x{H} handle on rank 0's GPU"}
+
+
+def one_gpu_rate(cs, W, H, pipeline, device, steps, warmup):
+    """Msamples/s of one whole W x H frame per step on this GPU (one handle, untimed census-free)."""
+    from pathtracerdemo_amd.renderer import Renderer
+    r = Renderer(W, H, device=device, pipeline=pipeline)
+    r.Initialize(cs)
+    for _ in range(warmup):
+        r.Update()
+        r.Render()
+    r.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r.Update()
+        r.Render()
+    r.synchronize()
+    dt = time.perf_counter() - t0
+    r.close()
+    return {"frame": f"{W}x{H}", "value": round(W * H * steps / dt / 1e6, 3), "unit": "Msamples/s",
+            "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps,
+            "note": "configs[3]'s frame on ONE GPU: the reference for the N-GPU strong split"}
 
 
 def cpu_baseline(cs, W, H, pipeline, threads):
@@ -444,22 +522,27 @@ def cpu_baseline(cs, W, H, pipeline, threads):
     whole frames: one frame (restir / mcpt), two for reuse (the second with its history)."""
     from oracle import oracle as O
     from pathtracerdemo_amd.scene.camera import Camera
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = max(1, threads)
     cam = Camera(W, H)
     cam.set_location(0, 0, 6)
     u = cs.uniform(W, H, cam.view_projection_inverse(), cam.location, 1)
-    fr = O.Frame(u, cs.scene, cs.geometry, cs.accel)
     nf = 2 if pipeline in ("reuse", "gi") else 1
-    t0 = time.perf_counter()
-    for f in range(1, nf + 1):
-        fr.set_frame_index(f)
-        if pipeline == "reuse":
-            fr.run_reuse_frame(threads=threads)
-        elif pipeline == "gi":
-            fr.run_gi_frame(threads=threads)
-        else:
-            fr.run(O.PASS_RESTIR if pipeline == "restir" else O.PASS_MCPT, threads=threads)
-    dt = time.perf_counter() - t0
+
+    def full_frames(nthreads):
+        fr = O.Frame(u, cs.scene, cs.geometry, cs.accel)
+        t0 = time.perf_counter()
+        for f in range(1, nf + 1):
+            fr.set_frame_index(f)
+            if pipeline == "reuse":
+                fr.run_reuse_frame(threads=nthreads)
+            elif pipeline == "gi":
+                fr.run_gi_frame(threads=nthreads)
+            else:
+                fr.run(O.PASS_RESTIR if pipeline == "restir" else O.PASS_MCPT, threads=nthreads)
+        return time.perf_counter() - t0
+
+    dt = full_frames(threads)
+    dt16 = full_frames(min(16, threads)) if threads != 16 else dt
     # one thread on a 64-row band of the same frames (the single-core rate)
     fr1 = O.Frame(u, cs.scene, cs.geometry, cs.accel)
     rows = min(H, 64)
@@ -477,10 +560,29 @@ def cpu_baseline(cs, W, H, pipeline, threads):
     dt1 = time.perf_counter() - t1
     return {"value": round(nf * W * H / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{nf} full {W}x{H} frame(s) ({pipeline}, FrameIndex 1..{nf}), C oracle, {threads} pthreads",
-            "seconds": round(dt, 2), "cpu_model": cpu_model(),
+            "seconds": round(dt, 2), "cpu_model": cpu_model(), "host_cpus": host_cpus(),
+            "at_16_threads": {"value": round(nf * W * H / dt16 / 1e6, 4), "unit": "Msamples/s", "cores": min(16, threads),
+                              "seconds": round(dt16, 2)},
             "single_thread": {"value": round(nf * W * rows / dt1 / 1e6, 4), "unit": "Msamples/s",
                               "sample": f"rows {y0}..{y0 + rows} of the same {nf} frame(s), 1 thread",
                               "seconds": round(dt1, 2)}}
+
+
+def host_cpus() -> dict:
+    """Logical CPUs of the host, those this process may run on, and its cgroup CPU quota (the
+    share a container actually gets), so the baseline's thread count can be read against them."""
+    out = {"logical": os.cpu_count()}
+    try:
+        out["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            out["cgroup_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return out
 
 
 def cpu_model() -> str:
@@ -495,7 +597,7 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def ts_cpu_baseline(cs, scene, W, H, threads, rows=256):
+def ts_cpu_baseline(cs, scene, W, H, threads, rows=None):
     """SURVEY.md §8(d)'s JS CPU tracer (pathtracerdemo_amd/js/cpu: the reference's live
     pipeline PT_01 -> PT_1 -> PT_4 restated in JavaScript, bit-identical to the oracle) on
     Node worker_threads: a band of `rows` rows in the middle of the frame, wall clock."""
@@ -508,6 +610,7 @@ def ts_cpu_baseline(cs, scene, W, H, threads, rows=256):
     from pathtracerdemo_amd.scene.camera import Camera
     from pathtracerdemo_amd.scene.export import export_compiled
     threads = max(1, min(threads, os.cpu_count() or 1))
+    rows = rows or H
     cam = Camera(W, H)
     cam.set_location(0, 0, 6)
     u = cs.uniform(W, H, cam.view_projection_inverse(), cam.location, 1)

@@ -173,6 +173,12 @@ int ptx_comm_unique_id(void *id_out, size_t bytes);
 int ptx_comm_init(ptx_handle *h, const void *unique_id, size_t bytes, int rank, int world);
 int ptx_comm_init_all(ptx_handle *const *handles, int n);
 int ptx_render_bands(ptx_handle *const *handles, int n, float *rgba_out);
+/* The communicator a band handle owns: its rank and world size (0 / 1 without one) and the
+ * halo bytes it has sent so far -- what a benchmark reports to prove N ranks exchanged.
+ * ptx_comm_init also swaps the band geometry with the neighbouring ranks once and fails on
+ * rows that do not continue or halos that do not match; ptx_render checks the communicator's
+ * asynchronous error state (ncclCommGetAsyncError) every frame. */
+int ptx_comm_info(ptx_handle *h, int *rank, int *world, uint64_t *halo_bytes_sent);
 /* Work census of a PTX_FLAG_ROW_CENSUS handle since the last ptx_reset_stats: per 8-row tile
  * row of the band, 5 u64 {rays, instance transforms, AABB tests, triangle tests, hits} of every
  * query traced for that row's pixels (the §8(d) algorithmic-bytes counters).  Cost-balanced
@@ -184,6 +190,11 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out);
 int ptx_reset_stats(ptx_handle *h);
 int ptx_read_buffer(ptx_handle *h, int which, void *host_dst, size_t bytes);
 int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t bytes);
+/* A buffer's device address.  On a handle whose frames are pipelined (whole-image reuse
+ * pipeline on its own stream: two frames in flight) the G-buffer and
+ * reservoir buffers alternate between two allocations frame by frame: the pointer returned
+ * for PTX_BUF_GBUFFER / PTX_BUF_RESERVOIR is valid until the next ptx_render.  Accumulation,
+ * history and counters never move. */
 int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes);
 /* Closest-hit queries (TraceRay, SH/PT_1_InitPass.wgsl:605-715) for arbitrary rays.
  * rays: n x {o.x,o.y,o.z,d.x, d.y,d.z,-,-} f32 (32 B); hits: n x {t, flags|inst|mat (u32 bits),

@@ -39,7 +39,7 @@ EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame"
             "ptx_write_buffer", "ptx_device_pointer", "ptx_set_stream", "ptx_destroy", "ptx_last_error",
             "ptx_trace", "ptx_trace_device", "ptx_run_passes", "ptx_halo_rows", "ptx_halo_pack",
             "ptx_halo_unpack", "ptx_comm_unique_id", "ptx_comm_init", "ptx_comm_init_all", "ptx_render_bands",
-            "ptx_row_census"]
+            "ptx_row_census", "ptx_comm_info"]
 
 
 class PtxConfig(ctypes.Structure):
@@ -115,6 +115,8 @@ def load(path: str = LIB_PATH):
     lib.ptx_comm_unique_id.argtypes = [P, ctypes.c_size_t]
     lib.ptx_comm_init.argtypes = [H, P, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
     lib.ptx_comm_init_all.argtypes = [ctypes.POINTER(H), ctypes.c_int]
+    lib.ptx_comm_info.argtypes = [H, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                  ctypes.POINTER(ctypes.c_uint64)]
     lib.ptx_render_bands.argtypes = [ctypes.POINTER(H), ctypes.c_int, P]
     lib.ptx_row_census.argtypes = [H, P, ctypes.c_size_t]
     lib.ptx_destroy.argtypes = [H]

@@ -21,6 +21,19 @@
 namespace ptx {
 
 
+int ab_knob(const char *key, int dflt) {
+    static const std::string ab = getenv("PTX_AB") ? getenv("PTX_AB") : "";
+    const size_t n = std::strlen(key);
+    for (size_t pos = 0; pos < ab.size();) {
+        size_t end = ab.find(',', pos);
+        if (end == std::string::npos) end = ab.size();
+        if (end - pos >= n && ab.compare(pos, n, key) == 0 && (end - pos == n || ab[pos + n] == '='))
+            return end - pos == n ? 1 : std::atoi(ab.c_str() + pos + n + 1);
+        pos = end + 1;
+    }
+    return dflt;
+}
+
 int fail(ptx_handle *h, int code, const char *fmt, ...) {
     if (h) {
         char buf[512];
@@ -37,13 +50,21 @@ void free_buf(DevBuf &b) {
     b.p = nullptr;
     b.bytes = 0;
 }
-// Fill device memory and wait for it: every stream of a handle is non-blocking, so a plain
-// hipMemset (null stream) is NOT ordered before their kernels -- a fill still in flight when a
-// frame starts overwrites what the frame wrote (seen as a reuse mismatch when another handle
-// kept the null stream busy).  Used for the one-time clears.
-static hipError_t memset_sync(void *p, int value, size_t bytes) {
-    hipError_t e = hipMemsetAsync(p, value, bytes, nullptr);
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+// Every copy and fill between the host and a handle's buffers runs on the handle's current
+// stream and is waited for there.  The handle's streams are non-blocking, so nothing on the
+// null stream is ordered before their kernels: a null-stream fill still in flight when a frame
+// started once overwrote what the frame wrote (a reuse mismatch seen when another handle kept
+// the null stream busy), and a pageable host-to-device hipMemcpy may return before its DMA has
+// landed.  On the handle's stream the transfer is ordered after everything enqueued before it,
+// and the sync orders it before everything enqueued after.
+static hipError_t memset_sync(ptx_handle *h, void *p, int value, size_t bytes) {
+    hipError_t e = hipMemsetAsync(p, value, bytes, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return e;
+}
+static hipError_t copy_sync(ptx_handle *h, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return e;
 }
 int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
@@ -53,17 +74,16 @@ int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
     hipError_t e = hipMalloc(&b.p, bytes);
     if (e != hipSuccess) return fail(h, PTX_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
     b.bytes = bytes;
-    // diagnostics: PTX_DEBUG_FILL=<byte> fills every new buffer with that byte (an
+    // diagnostics: PTX_AB=DEBUG_FILL=<byte> fills every new buffer with that byte (an
     // uninitialised read then shows up as a parity failure)
-    static const int fill = getenv("PTX_DEBUG_FILL") ? atoi(getenv("PTX_DEBUG_FILL")) : -1;
-    if (fill >= 0) HIP_CHECK(h, memset_sync(b.p, fill & 0xff, bytes));
+    static const int fill = ab_knob("DEBUG_FILL", -1);
+    if (fill >= 0) HIP_CHECK(h, memset_sync(h, b.p, fill & 0xff, bytes));
     return PTX_OK;
 }
 static int upload(ptx_handle *h, DevBuf &b, const void *src, size_t bytes) {
     int rc = alloc_buf(h, b, std::max<size_t>(bytes, 16));
     if (rc) return rc;
-    if (bytes) HIP_CHECK(h, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
-    if (bytes) HIP_CHECK(h, hipStreamSynchronize(nullptr));  // (null-stream copy done before any handle stream reads it)
+    if (bytes) HIP_CHECK(h, copy_sync(h, b.p, src, bytes, hipMemcpyHostToDevice));
     return PTX_OK;
 }
 
@@ -86,6 +106,8 @@ static inline float as_f32(uint32_t u) {
 // read by GetBlasNode, SH/PT_01_GBufferPass.wgsl:310-322) and emits the child-pair node
 // records, the edge-form triangle table and the instance table of ptx_device.h.
 int build_layout(ptx_handle *h) {
+    // frames in flight (either pipelined context) still read the layout being replaced
+    if (int rc = quiesce(h)) return rc;
     const uint32_t *U = h->uniform;
     const auto &S = h->scene, &G = h->geometry, &A = h->accel;
     const uint32_t off_desc = U[U_OFF_DESC], off_mat = U[U_OFF_MAT], off_index = U[U_OFF_INDEX];
@@ -290,7 +312,7 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t jpp = has_reuse(h) ? 2u * h->reuse_neighbors : 1u;
     const size_t per_px = std::max<size_t>(std::max<size_t>(2u, (size_t)nl + 1u), jpp);
     const size_t padded = (size_t)((h->cfg.width + 7u) / 8u) * ((h->band_h + 7u) / 8u) * 64u;
-    static const uint32_t env_px = getenv("PTX_SEG_PX") ? (uint32_t)atoi(getenv("PTX_SEG_PX")) : 0u;  // A/B
+    static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);  // A/B
     const uint32_t seg_px = (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) ? env_px : kWaveSegPixels;
     const size_t nseg = (padded + seg_px - 1u) / seg_px;
     // queue slots: the whole band, or two tile sets in flight at once (interior + edge rows of
@@ -340,11 +362,11 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     // pipeline at 1080p (GI 720 vs 714 Msamples/s at 5), 5 for bands of more than 4 Mpx (a
     // 3840x2160 frame on one GPU: 414.6 vs 413.9 Msamples/s, trace roofline 0.611 vs 0.597)
     w.trace_waves = npix > ((size_t)4u << 20) ? 5u : 4u;
-    static const uint32_t env_split = getenv("PTX_TRACE_SPLIT") ? (uint32_t)atoi(getenv("PTX_TRACE_SPLIT")) : 0u;
+    static const uint32_t env_split = (uint32_t)ab_knob("TRACE_SPLIT", 0);
     w.trace_split = env_split >= 1u && env_split <= 16u ? env_split : 1u;
     w.seg_base = 0;
     w.seg_count = w.nseg;
-    static const uint32_t cl = getenv("PTX_SEG_CLUSTER") ? (uint32_t)atoi(getenv("PTX_SEG_CLUSTER")) : 1u;  // A/B
+    static const uint32_t cl = (uint32_t)ab_knob("SEG_CLUSTER", 1);  // A/B
     w.cluster = (cl == 2u || cl == 4u || cl == 8u || cl == 16u) ? cl : 1u;
     // row census: a segment is seg_px / 64 tiles adjacent in raster order, so its queue
     // slot's work belongs to one tile row (two where a tile row's width is not a multiple)
@@ -488,7 +510,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
 // (fork/join through events on the handle's stream), so one part's latency-bound traces
 // overlap another's ALU-bound shading and trace tails.  Each part runs `passes` in order
 // over its own segments (a frame: G-buffer -> init -> final per part, nothing shared).
-// PTX_WAVE_STREAMS=1..4 overrides K (A/B: 3 measured best since the cooperative traversal,
+// PTX_AB=WAVE_STREAMS=1..4 overrides K (A/B: 3 measured best since the cooperative traversal,
 // +2.5 % over 2 on reuse / ReSTIR; 4 oversubscribes the 4 hardware queues).
 hipError_t spatial_summaries(ptx_handle *h, hipStream_t st) {
     if (h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) return hipSuccess;  // GI gathers the buffers
@@ -514,12 +536,12 @@ hipError_t spatial_summaries(ptx_handle *h, hipStream_t st) {
 static bool whole_band_sequences(const ptx_handle *h);
 hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes, int npasses,
                              bool summaries, const WaveBufs *then, hipEvent_t then_wait) {
-    static const int env_k = getenv("PTX_WAVE_STREAMS") ? atoi(getenv("PTX_WAVE_STREAMS")) : 0;
+    static const int env_k = ab_knob("WAVE_STREAMS", 0);
     // pipelined frames: each of the two contexts in flight runs its passes as ONE launch
     // sequence (whole-band launches, dynamic trace batches); measured at 1080p C3 reuse: 1
     // stream per context 338 Msamples/s, 2 streams 308, unpipelined 3 streams 320
-    // (PTX_PIPE_STREAMS: A/B)
-    static const int env_pk = getenv("PTX_PIPE_STREAMS") ? atoi(getenv("PTX_PIPE_STREAMS")) : 0;
+    // (PTX_AB=PIPE_STREAMS=k: A/B)
+    static const int env_pk = ab_knob("PIPE_STREAMS", 0);
     int k = h->alt_stream && pipelined(h) ? (env_pk > 0 ? env_pk : 1) : env_k > 0 ? env_k : 3;
     if (h->cfg.flags & PTX_FLAG_SINGLE_STREAM) k = 1;
     k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
@@ -572,8 +594,8 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
             // (+5.6 % there); with three concurrent sequences per frame the other sequences
             // already fill a launch's tail and the per-workgroup prefix costs more than it
             // saves (1080p, static vs dynamic: ReSTIR 1240 vs 1081, GI 675 vs 625, TEST_MCPT
-            // 1264 vs 1229 Msamples/s).  PTX_TRACE_DYN=0 / 1 forces it off / on (A/B).
-            static const int dyn_env = getenv("PTX_TRACE_DYN") ? atoi(getenv("PTX_TRACE_DYN")) : -1;
+            // 1264 vs 1229 Msamples/s).  PTX_AB=TRACE_DYN=0 / 1 forces it off / on.
+            static const int dyn_env = ab_knob("TRACE_DYN", -1);
             const bool use_dyn = dyn_env == 1 || (dyn_env != 0 && whole_band_sequences(h));
             part.dyn = !use_dyn ? nullptr
                                : (uint32_t *)h->d_wctr.p + 2u * kWaveMaxRounds * ws.cnt_stride +
@@ -635,7 +657,7 @@ static bool whole_band_sequences(const ptx_handle *h) {
             (size_t)h->band_h * h->cfg.width <= ((size_t)4u << 20));
 }
 bool pipelined(const ptx_handle *h) {
-    static const bool off = getenv("PTX_PIPELINE_FRAMES") && atoi(getenv("PTX_PIPELINE_FRAMES")) == 0;  // A/B
+    static const bool off = ab_knob("PIPELINE_FRAMES", 1) == 0;  // A/B
     const uint32_t fl = h->cfg.flags;
     // at most ~4 Mpx per frame: a 3840x2160 frame's launches are large enough to fill the chip
     // on their own (configs[3] on one GPU: 384 Msamples/s unpipelined, 355 pipelined)
@@ -693,16 +715,16 @@ static int ensure_alt(ptx_handle *h) {
     DevBuf &g = h->alt_active ? h->d_gbuf : a.gbuf, &r = h->alt_active ? h->d_res : a.res;
     if (!g.p) {
         if (int rc = alloc_buf(h, g, h->d_gbuf.bytes ? h->d_gbuf.bytes : a.gbuf.bytes)) return rc;
-        HIP_CHECK(h, memset_sync(g.p, 0, g.bytes));
+        HIP_CHECK(h, memset_sync(h, g.p, 0, g.bytes));
     }
     if (!r.p) {
         if (int rc = alloc_buf(h, r, h->d_res.bytes ? h->d_res.bytes : a.res.bytes)) return rc;
-        HIP_CHECK(h, memset_sync(r.p, 0, r.bytes));
+        HIP_CHECK(h, memset_sync(h, r.p, 0, r.bytes));
     }
     return PTX_OK;
 }
 // Back to the first context (its stream is own_stream) before the stream is replaced.
-static int leave_alt(ptx_handle *h) {
+int leave_alt(ptx_handle *h) {
     if (!h->alt_active) return PTX_OK;
     if (int rc = quiesce(h)) return rc;
     swap_frame_ctx(h);
@@ -906,11 +928,11 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!rc) rc = alloc_buf(h, h->d_res, px_halo * 16u * h->res_u4);
     if (!rc && has_reuse(h)) {
         rc = alloc_buf(h, h->d_hist, px * 16u * h->res_u4);
-        if (!rc && memset_sync(h->d_hist.p, 0, h->d_hist.bytes) != hipSuccess) rc = PTX_E_HIP;
+        if (!rc && memset_sync(h, h->d_hist.p, 0, h->d_hist.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
     if (!rc && h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {
         rc = alloc_buf(h, h->d_direct, px * 16u);
-        if (!rc && memset_sync(h->d_direct.p, 0, h->d_direct.bytes) != hipSuccess) rc = PTX_E_HIP;
+        if (!rc && memset_sync(h, h->d_direct.p, 0, h->d_direct.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
     if (!rc) rc = alloc_buf(h, h->d_accum, px * 16u);
     if (!rc) rc = alloc_buf(h, h->d_counters, kCounterWords * 8u);
@@ -920,18 +942,18 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
         const size_t tile_rows = (h->band_h + 7u) / 8u, tiles = tile_rows * ((h->cfg.width + 7u) / 8u);
         h->census_blocks = (uint32_t)(tile_rows + tiles * 64u / 256u + 2u);
         rc = alloc_buf(h, h->d_census, (size_t)h->census_blocks * kCensusWords * 8u);
-        if (!rc && memset_sync(h->d_census.p, 0, h->d_census.bytes) != hipSuccess) rc = PTX_E_HIP;
+        if (!rc && memset_sync(h, h->d_census.p, 0, h->d_census.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
 #ifdef PTX_WG_TIMES
-    if (!rc && getenv("PTX_WGT")) {  // 4 header words + 2^20 records of 4 words
+    if (!rc && ab_knob("WGT", 0)) {  // 4 header words + 2^20 records of 4 words
         rc = alloc_buf(h, h->d_wgt, (4u + 4u * (1u << 20)) * 8u);
-        if (!rc && memset_sync(h->d_wgt.p, 0, 32u) != hipSuccess) rc = PTX_E_HIP;
+        if (!rc && memset_sync(h, h->d_wgt.p, 0, 32u) != hipSuccess) rc = PTX_E_HIP;
     }
 #endif
-    if (!rc && memset_sync(h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
-    if (!rc && memset_sync(h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;
-    if (!rc && memset_sync(h->d_gbuf.p, 0, h->d_gbuf.bytes) != hipSuccess) rc = PTX_E_HIP;
-    if (!rc && memset_sync(h->d_res.p, 0, h->d_res.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && memset_sync(h, h->d_accum.p, 0, h->d_accum.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && memset_sync(h, h->d_counters.p, 0, h->d_counters.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && memset_sync(h, h->d_gbuf.p, 0, h->d_gbuf.bytes) != hipSuccess) rc = PTX_E_HIP;
+    if (!rc && memset_sync(h, h->d_res.p, 0, h->d_res.bytes) != hipSuccess) rc = PTX_E_HIP;
     if (rc) {
         ptx_destroy(h);
         return rc;
@@ -1155,8 +1177,8 @@ int ptx_reset_stats(ptx_handle *h) {
     HIP_CHECK(h, hipStreamSynchronize(h->stream));
     for (int p = 0; p < kPasses; ++p) { h->ms_total[p] = 0.0; h->launches[p] = 0; }
     h->frames = 0;
-    HIP_CHECK(h, memset_sync(h->d_counters.p, 0, h->d_counters.bytes));
-    if (h->d_census.p) HIP_CHECK(h, memset_sync(h->d_census.p, 0, h->d_census.bytes));
+    HIP_CHECK(h, memset_sync(h, h->d_counters.p, 0, h->d_counters.bytes));
+    if (h->d_census.p) HIP_CHECK(h, memset_sync(h, h->d_census.p, 0, h->d_census.bytes));
     return PTX_OK;
 }
 
@@ -1168,10 +1190,10 @@ int ptx_diag_wave_times(ptx_handle *h, uint64_t *out, size_t max_records) {
     if (!h || !h->d_wgt.p) return PTX_E_INVALID;
     HIP_CHECK(h, hipDeviceSynchronize());
     uint64_t n = 0;
-    HIP_CHECK(h, hipMemcpy(&n, h->d_wgt.p, 8, hipMemcpyDeviceToHost));
+    HIP_CHECK(h, copy_sync(h, &n, h->d_wgt.p, 8, hipMemcpyDeviceToHost));
     n = std::min<uint64_t>(std::min<uint64_t>(n, 1u << 20), max_records);
-    if (n && out) HIP_CHECK(h, hipMemcpy(out, (uint64_t *)h->d_wgt.p + 4, n * 32u, hipMemcpyDeviceToHost));
-    HIP_CHECK(h, memset_sync(h->d_wgt.p, 0, 8));
+    if (n && out) HIP_CHECK(h, copy_sync(h, out, (uint64_t *)h->d_wgt.p + 4, n * 32u, hipMemcpyDeviceToHost));
+    HIP_CHECK(h, memset_sync(h, h->d_wgt.p, 0, 8));
     return (int)n;
 }
 #endif
@@ -1182,14 +1204,13 @@ int ptx_row_census(ptx_handle *h, uint64_t *out, size_t n_tile_rows) {
     const uint32_t tile_rows = (h->band_h + 7u) / 8u, tiles_x = (h->cfg.width + 7u) / 8u;
     if (n_tile_rows != tile_rows) return fail(h, PTX_E_INVALID, "census: %zu tile rows, band has %u", n_tile_rows, tile_rows);
     std::vector<unsigned long long> c((size_t)h->census_blocks * kCensusWords);
-    HIP_CHECK(h, hipStreamSynchronize(h->stream));
-    HIP_CHECK(h, hipMemcpy(c.data(), h->d_census.p, c.size() * 8u, hipMemcpyDeviceToHost));
+    HIP_CHECK(h, copy_sync(h, c.data(), h->d_census.p, c.size() * 8u, hipMemcpyDeviceToHost));
     std::memset(out, 0, (size_t)tile_rows * 5u * sizeof(uint64_t));
     for (uint32_t r = 0; r < tile_rows; ++r)
         for (int k = 0; k < 5; ++k) out[5u * r + k] += c[(size_t)kCensusWords * r + k];
     // queue slot s traced the rays of segment s: tiles [s*m, s*m + m) in raster order
     // (m = seg_px / 64); a slot spanning two tile rows is split by its tiles in each
-    static const uint32_t env_px = getenv("PTX_SEG_PX") ? (uint32_t)atoi(getenv("PTX_SEG_PX")) : 0u;
+    static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);
     const uint32_t seg_px = (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) ? env_px : kWaveSegPixels;
     const uint32_t m = seg_px / 64u, ntiles = tile_rows * tiles_x;
     for (uint32_t s = 0; tile_rows + s < h->census_blocks && (size_t)s * m < ntiles; ++s) {
@@ -1213,8 +1234,7 @@ int ptx_read_buffer(ptx_handle *h, int which, void *host_dst, size_t bytes) {
     DevBuf b;
     if (!buffer_view(h, which, b) || bytes > b.bytes)
         return fail(h, PTX_E_INVALID, "read of %zu bytes from buffer %d", bytes, which);
-    HIP_CHECK(h, hipStreamSynchronize(h->stream));
-    HIP_CHECK(h, hipMemcpy(host_dst, b.p, bytes, hipMemcpyDeviceToHost));
+    HIP_CHECK(h, copy_sync(h, host_dst, b.p, bytes, hipMemcpyDeviceToHost));
     return PTX_OK;
 }
 
@@ -1223,8 +1243,7 @@ int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t byte
     DevBuf b;
     if (!buffer_view(h, which, b) || bytes > b.bytes)
         return fail(h, PTX_E_INVALID, "write of %zu bytes to buffer %d", bytes, which);
-    HIP_CHECK(h, hipStreamSynchronize(h->stream));
-    HIP_CHECK(h, hipMemcpy(b.p, host_src, bytes, hipMemcpyHostToDevice));
+    HIP_CHECK(h, copy_sync(h, b.p, host_src, bytes, hipMemcpyHostToDevice));
     h->init_state_valid = false;  // the wave state no longer matches the buffers
     h->nbr_valid = false;
     h->surf_valid = false;  // (a G-buffer write: the surface records describe the old one)
@@ -1286,8 +1305,11 @@ int ptx_set_stream(ptx_handle *h, void *hip_stream) {
 int ptx_destroy(ptx_handle *h) {
     if (!h) return PTX_E_INVALID;
     (void)hipSetDevice(h->device);
-    comm_destroy(h);
+    // everything enqueued (a band frame's sends / receives on the exchange stream included)
+    // finishes before the communicator and the exchange stream go
     (void)quiesce(h);
+    if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+    comm_destroy(h);
     if (h->alt_active) swap_frame_ctx(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (hipStream_t q : h->sub)

@@ -43,6 +43,7 @@ struct Rccl {
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
     ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*async_error)(ncclComm_t, ncclResult_t *) = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
     bool ok = false;
     std::string why;
@@ -75,6 +76,7 @@ const Rccl &rccl() {
         sym(r.group_start, "ncclGroupStart");
         sym(r.group_end, "ncclGroupEnd");
         sym(r.destroy, "ncclCommDestroy");
+        sym(r.async_error, "ncclCommGetAsyncError");
         sym(r.error_string, "ncclGetErrorString");
         r.ok = all;
     });
@@ -239,10 +241,67 @@ int band_back(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *fr
     return PTX_OK;
 }
 
+// An error a previous frame's sends / receives raised asynchronously (a peer that died, a
+// broken link): checked once per frame, so a failed exchange surfaces as a status instead of
+// a hang or a silently stale halo (failure handling).
+int comm_health(ptx_handle *h) {
+    ncclResult_t st = ncclSuccess;
+    NCCL_CHECK(h, rccl().async_error((ncclComm_t)h->comm, &st));
+    if (st != ncclSuccess && st != ncclInProgress)
+        return fail(h, PTX_E_HIP, "RCCL communicator (rank %d of %d) reports: %s", h->rank, h->world,
+                    rccl().error_string(st));
+    return PTX_OK;
+}
+
+// Once, at ptx_comm_init: every rank swaps its band geometry {width, height, row_begin, row_end,
+// halo_top, halo_bot} with the ranks above and below, and refuses a neighbour whose rows do
+// not continue its own or whose halo would not match what this band sends -- such a mismatch
+// would otherwise hang in ncclGroupEnd or carry rows from past the band.
+int check_neighbours(ptx_handle *h) {
+    if (h->world < 2) return PTX_OK;
+    const Rccl &R = rccl();
+    ncclComm_t c = (ncclComm_t)h->comm;
+    uint32_t mine[6] = {h->cfg.width, h->cfg.height, h->cfg.row_begin, h->cfg.row_end, h->halo_top, h->halo_bot};
+    uint32_t got[2][6] = {};
+    uint32_t *d = nullptr;
+    HIP_CHECK(h, hipMalloc(&d, 18 * sizeof(uint32_t)));
+    auto done = [&](int rc) { (void)hipFree(d); return rc; };
+    hipError_t e = hipMemcpyAsync(d, mine, sizeof mine, hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) return done(fail(h, PTX_E_HIP, "neighbour check: %s", hipGetErrorString(e)));
+    ncclResult_t r = R.group_start();
+    if (r == ncclSuccess && h->rank > 0) {
+        r = R.send(d, 6, ncclUint32, h->rank - 1, c, h->stream);
+        if (r == ncclSuccess) r = R.recv(d + 6, 6, ncclUint32, h->rank - 1, c, h->stream);
+    }
+    if (r == ncclSuccess && h->rank + 1 < h->world) {
+        r = R.send(d, 6, ncclUint32, h->rank + 1, c, h->stream);
+        if (r == ncclSuccess) r = R.recv(d + 12, 6, ncclUint32, h->rank + 1, c, h->stream);
+    }
+    const ncclResult_t r2 = R.group_end();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess) return done(fail(h, PTX_E_HIP, "neighbour check: %s", R.error_string(r)));
+    e = hipMemcpyAsync(got, d + 6, sizeof got, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return done(fail(h, PTX_E_HIP, "neighbour check: %s", hipGetErrorString(e)));
+    const uint32_t *up = got[0], *dn = got[1];
+    if (h->rank > 0 && (up[0] != mine[0] || up[1] != mine[1] || up[3] != mine[2] || up[5] != mine[4]))
+        return done(fail(h, PTX_E_INVALID,
+                         "ptx_comm_init: rank %d has rows [%u,%u) with a %u-row halo below in a %ux%u frame; this band "
+                         "(rank %d) starts at row %u with a %u-row halo above in a %ux%u frame",
+                         h->rank - 1, up[2], up[3], up[5], up[0], up[1], h->rank, mine[2], mine[4], mine[0], mine[1]));
+    if (h->rank + 1 < h->world && (dn[0] != mine[0] || dn[1] != mine[1] || dn[2] != mine[3] || dn[4] != mine[5]))
+        return done(fail(h, PTX_E_INVALID,
+                         "ptx_comm_init: rank %d has rows [%u,%u) with a %u-row halo above in a %ux%u frame; this band "
+                         "(rank %d) ends at row %u with a %u-row halo below in a %ux%u frame",
+                         h->rank + 1, dn[2], dn[3], dn[4], dn[0], dn[1], h->rank, mine[3], mine[5], mine[0], mine[1]));
+    return done(PTX_OK);
+}
+
 }  // namespace
 
 // ptx_render of a band handle that owns a communicator: one whole frame, exchange included.
 int render_band_nccl(ptx_handle *h) {
+    if (int rc = comm_health(h)) return rc;
     Scene sc{};
     WaveBufs w{};
     if (int rc = band_prepare(h, sc, w)) return rc;
@@ -254,6 +313,8 @@ int render_band_nccl(ptx_handle *h) {
     const int rc = nccl_halo(h, xs);
     NCCL_CHECK(h, rccl().group_end());
     if (rc) return rc;
+    if (h->halo_top) h->halo_bytes_sent += send_up(h).gb + send_up(h).rb;
+    if (h->halo_bot) h->halo_bytes_sent += send_down(h).gb + send_down(h).rb;
     if (int r2 = halo_landed(h, xs)) return r2;
     return band_back(h, sc, w, ft);
 }
@@ -280,9 +341,13 @@ int ptx_comm_init(ptx_handle *h, const void *unique_id, size_t bytes, int rank, 
     if ((h->halo_top && rank == 0) || (h->halo_bot && rank == world - 1))
         return fail(h, PTX_E_INVALID, "ptx_comm_init: band rows [%u,%u) need neighbours rank %d of %d cannot have",
                     h->cfg.row_begin, h->cfg.row_end, rank, world);
+    if ((h->halo_top || h->halo_bot) && h->band_h < std::max(h->halo_top, h->halo_bot))
+        return fail(h, PTX_E_INVALID, "ptx_comm_init: band of %u rows cannot feed a %u / %u-row halo", h->band_h,
+                    h->halo_top, h->halo_bot);
     const Rccl &R = rccl();
     if (!R.ok) return fail(h, PTX_E_HIP, "RCCL unavailable: %s", R.why.c_str());
     HIP_CHECK(h, hipSetDevice(h->device));
+    if (int rc = leave_alt(h)) return rc;  // band frames run on the first context's stream
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof id);
     ncclComm_t c = nullptr;
@@ -290,6 +355,18 @@ int ptx_comm_init(ptx_handle *h, const void *unique_id, size_t bytes, int rank, 
     h->comm = c;
     h->rank = rank;
     h->world = world;
+    if (int rc = check_neighbours(h)) {
+        comm_destroy(h);
+        return rc;
+    }
+    return PTX_OK;
+}
+
+int ptx_comm_info(ptx_handle *h, int *rank, int *world, uint64_t *halo_bytes_sent) {
+    if (!h) return PTX_E_INVALID;
+    if (rank) *rank = h->comm ? h->rank : 0;
+    if (world) *world = h->comm ? h->world : 1;
+    if (halo_bytes_sent) *halo_bytes_sent = h->halo_bytes_sent;
     return PTX_OK;
 }
 
@@ -307,6 +384,10 @@ int ptx_comm_init_all(ptx_handle *const *hs, int n) {
     }
     const Rccl &R = rccl();
     if (!R.ok) return fail(hs[0], PTX_E_HIP, "RCCL unavailable: %s", R.why.c_str());
+    for (int i = 0; i < n; ++i) {
+        HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
+        if (int rc = leave_alt(hs[i])) return rc;
+    }
     std::vector<ncclComm_t> comms(n);
     NCCL_CHECK(hs[0], R.init_all(comms.data(), n, devs.data()));
     for (int i = 0; i < n; ++i) {

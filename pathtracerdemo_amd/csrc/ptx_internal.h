@@ -109,6 +109,7 @@ struct ptx_handle {
     int rank = 0, world = 1;
     hipStream_t xstream = nullptr;
     hipEvent_t ev_front = nullptr, ev_halo = nullptr;
+    uint64_t halo_bytes_sent = 0;  // halo bytes this handle's communicator has sent (ptx_comm_info)
     // stats
     TimedLaunch ring[kEventRing];
     int ring_pos = 0;
@@ -150,6 +151,8 @@ void mark_history(ptx_handle *h);
 // frames' streams (before anything that replaces shared buffers or the stream)
 bool pipelined(const ptx_handle *h);
 int quiesce(ptx_handle *h);
+// back to the first frame context (quiesce + swap) before the handle's stream or mode changes
+int leave_alt(ptx_handle *h);
 // ptx_comm.cpp: a frame of a band handle that owns a communicator; its teardown
 int render_band_nccl(ptx_handle *h);
 void comm_destroy(ptx_handle *h);

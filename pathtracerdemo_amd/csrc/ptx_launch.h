@@ -10,6 +10,12 @@ namespace ptx {
 constexpr int kTile = 16;
 constexpr int kBlock = 256;
 
+// A/B and diagnostic switches: every one is read from ONE environment variable, PTX_AB, a
+// comma-separated list of KEY or KEY=int (e.g. PTX_AB=TRACE_DYN=0,SEG_PX=512); a key that is
+// absent gives `dflt`.  Without PTX_AB every launch runs the product configuration, and
+// bench.py echoes PTX_AB (and any other PTX_* variable) in its line.  Defined in ptx_api.cpp.
+int ab_knob(const char *key, int dflt);
+
 // dynamic LDS bytes for a traversal stack of `depth` entries per thread
 inline size_t stack_lds_bytes(uint32_t depth) { return (size_t)depth * kBlock * sizeof(uint32_t); }
 

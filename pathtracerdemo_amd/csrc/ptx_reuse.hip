@@ -797,7 +797,7 @@ hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_tempora
         hipLaunchKernelGGL(wjob_step, grid, blk, 0, s, sc, w, (uint32_t)round, A);
     } else {
         if (pass_temporal) hipLaunchKernelGGL(wtemporal_combine, grid, blk, 0, s, sc, w, A);
-        else if (A.neighbors == 3u && !getenv("PTX_COMBINE_SCALAR"))  // (A/B switch)
+        else if (A.neighbors == 3u && !ab_knob("COMBINE_SCALAR", 0))  // (A/B switch)
             hipLaunchKernelGGL(wspatial_combine_shfl, dim3(w.seg_count), blk, 0, s, sc, w, A);
         else hipLaunchKernelGGL(wspatial_combine, grid, blk, 0, s, sc, w, A);
     }

@@ -1041,8 +1041,8 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
     const PassEps eps = eps_mode == 0 ? PassEps{1e-8f, 1e-6f} : PassEps{1e-4f, 1e-8f};
     WaveBufs w = w_in;
     if (sc.counters || !trace_dyn(w)) w.dyn = nullptr;  // counting builds keep the per-slot census
-    if (w.dyn) {  // batches per dequeue (A/B: PTX_TRACE_DYN_G)
-        static const uint32_t g = getenv("PTX_TRACE_DYN_G") ? (uint32_t)atoi(getenv("PTX_TRACE_DYN_G")) : 0u;
+    if (w.dyn) {  // batches per dequeue (A/B: PTX_AB=TRACE_DYN_G=g)
+        static const uint32_t g = (uint32_t)ab_knob("TRACE_DYN_G", 0);
         w.trace_split = g >= 1u && g <= 16u ? g : 1u;
     }
     // dynamic LDS: scene tables (the LDS-table variants) + batch prefix (dynamic batches) + stacks
@@ -1057,7 +1057,7 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
                                (uint32_t)round, eps);
         return hipGetLastError();
     }
-    static const bool refill = getenv("PTX_TRACE_REFILL") != nullptr;  // A/B switch for profiling
+    static const bool refill = ab_knob("TRACE_REFILL", 0) != 0;  // A/B switch for profiling
     if (refill) {
         const uint32_t pb = w.seg_phys + w.seg_base;
         const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.cnt_stride + pb;
@@ -1070,20 +1070,21 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
             hipLaunchKernelGGL(trace_queue_sm<false>, dim3(w.seg_count), dim3(WB), lds, s, sc,
                                w.rays + 2u * (size_t)pb * w.ray_stride, res, cnt,
                                w.ray_stride, 0u, eps);
-    } else if (sc.counters && getenv("PTX_TRACE_PROF"))  // SIMD-utilisation diagnostics
+    } else if (sc.counters && ab_knob("TRACE_PROF", 0))  // SIMD-utilisation diagnostics
         hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round,
                            eps);
     else if (sc.counters)
         hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     else {
         // Occupancy target per pipeline (WaveBufs::trace_waves), LDS-staged tables; A/B
-        // switches PTX_TRACE_OCC / PTX_TRACE_NOLDS.  Measured at 1080p with 768-pixel segments:
+        // switches PTX_AB=TRACE_OCC=n / TRACE_NOLDS.  Measured at 1080p with 768-pixel segments:
         // 4 waves/SIMD (no spill) is fastest for every pipeline (with the flat node loop: reuse
         // 369-373 vs 339-340, ReSTIR 1301 vs 1235, TEST_MCPT 1359 vs 1261, GI 720 vs 714 at 5,
         // which spills 48-64 B/lane); 5 only for bands above 4 Mpx; 6+ spills in the node loop.
-        static const int env_occ = getenv("PTX_TRACE_OCC") ? atoi(getenv("PTX_TRACE_OCC")) : 0;
+        static const int env_occ = ab_knob("TRACE_OCC", 0);
         const int occ = env_occ ? env_occ : w.trace_waves == 4u ? 4 : 5;
-        const bool tables_fit = tables_fit_lds(sc) && !getenv("PTX_TRACE_NOLDS");
+        static const bool no_lds = ab_knob("TRACE_NOLDS", 0) != 0;
+        const bool tables_fit = tables_fit_lds(sc) && !no_lds;
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
                  : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
                  : occ == 6  ? trace_queue<false, 6> : occ == 5 ? trace_queue<false, 5> : trace_queue<false, 4>;
@@ -1110,7 +1111,7 @@ hipError_t launch_trace_rays_sm(const Scene &sc, const float4 *rays, float4 *hit
 
 hipError_t wave_gbuffer(const Scene &sc, const WaveBufs &w, uint4 *gbuf, uint32_t depth, hipStream_t s) {
     if (!tables_fit_lds(sc)) return hipErrorInvalidValue;  // caller falls back to gbuffer_kernel
-    static const bool rootq = getenv("PTX_GBUF_ROOTQ") != nullptr;  // A/B
+    static const bool rootq = ab_knob("GBUF_ROOTQ", 0) != 0;  // A/B
     if (rootq)
         hipLaunchKernelGGL(wgbuffer<true>, dim3(w.seg_px / WB * w.seg_count), dim3(WB),
                            tables_lds_bytes(sc) + stack_lds_bytes(depth), s, sc,

@@ -120,6 +120,12 @@ class Renderer:
         buf = ctypes.create_string_buffer(bytes(unique_id), N.PTX_COMM_ID_BYTES)
         self._call("ptx_comm_init", self._h, buf, N.PTX_COMM_ID_BYTES, rank, world)
 
+    def comm_info(self) -> dict:
+        """The handle's communicator: rank, world size (1 without one), halo bytes sent so far."""
+        rank, world, sent = ctypes.c_int(0), ctypes.c_int(1), ctypes.c_uint64(0)
+        self._call("ptx_comm_info", self._h, ctypes.byref(rank), ctypes.byref(world), ctypes.byref(sent))
+        return {"rank": rank.value, "world": world.value, "halo_bytes_sent": sent.value}
+
     @staticmethod
     def comm_init_all(renderers) -> None:
         """ncclCommInitAll over the band renderers of this process (one per GPU)."""

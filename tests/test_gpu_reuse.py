@@ -246,6 +246,32 @@ def test_c3_full_hd_reuse_windows_bit_exact(scene3, oracle_mod):
     assert np.isfinite(img).all()
 
 
+def test_c3_4k_one_handle_windows_bit_exact(scene3, oracle_mod):
+    """configs[3]'s frame on ONE handle -- C3, 3840x2160, reuse pipeline, 2 frames with history --
+    under the 4K launch parameters (above 4 Mpx per band: trace at 5 waves per SIMD, frames not
+    pipelined) vs the oracle on 3 row windows: the top edge, rows straddling the cut at row 1081
+    of a cost-balanced 8-band split (and the 2-band cut at 1080), and the bottom edge.  The
+    8-band tests (test_gpu_bands.py) compare bands with this one handle."""
+    O, W, H, R = oracle_mod, 3840, 2160, 30
+    windows = [(0, 8), (1076, 1086), (2152, 2160)]
+    r = reuse_renderer(scene3, W, H)
+    frs = [oracle_frame(O, scene3, W, H) for _ in windows]
+    for f in (1, 2):
+        r.Update()
+        r.Render()
+        for (y0, y1), fr in zip(windows, frs):
+            fr.set_frame_index(f)
+            fr.run_reuse_frame(threads=16, rect=(0, max(0, y0 - 2 * R), W, min(H, y1 + 2 * R)))
+    hist, img = r.read_history(), r.read_image()
+    for (y0, y1), fr in zip(windows, frs):
+        assert_same(hist[y0:y1], fr.res_hist[y0:y1], f"spatial output rows {y0}..{y1}")
+        assert_same(img[y0:y1], fr.accum[y0:y1], f"radiance rows {y0}..{y1}")
+    assert np.isfinite(img).all()
+    st = r.stats()
+    assert st["frames"] == 2
+    r.close()
+
+
 @pytest.mark.gpu
 def test_pipelined_frames_interleaved_with_host_ops(scene3, oracle_mod, native):
     """Frame pipelining (ptx_render runs frame N's G-buffer + PT_1 beside frame N-1's spatial
@@ -303,3 +329,60 @@ def test_pipelined_frames_beside_another_handle(scene1, scene3, oracle_mod):
     assert_same(r.read_image(), fr.accum, "accumulated radiance")
     r.close()
     other.close()
+
+
+def test_write_buffer_passes_beside_a_rendering_handle(scene1, scene3, oracle_mod, native):
+    """Host copies into a handle's buffers (ptx_write_buffer) and its pass-by-pass launches
+    while ANOTHER handle keeps pipelined frames in flight (never synchronised in between): every
+    copy runs on the handle's own stream and is waited for there, so each pass reads exactly the
+    bytes written (a null-stream copy is ordered before nothing on the handles' non-blocking
+    streams).  Both handles match the oracle bit for bit."""
+    O = oracle_mod
+    Wb, Hb = 96, 64
+    frb = oracle_frame(O, scene3, Wb, Hb)
+    b = reuse_renderer(scene3, Wb, Hb)
+    nb = 0
+
+    def tick():
+        nonlocal nb
+        nb += 1
+        b.Update()
+        b.Render()
+        frb.set_frame_index(nb)
+        frb.run_reuse_frame(threads=8)
+
+    W, H = 64, 48
+    fr = oracle_frame(O, scene1, W, H)
+    fr.set_frame_index(1)
+    fr.run_reuse_frame(threads=8)
+    fr.set_frame_index(2)
+    for p in (O.PASS_GBUFFER, O.PASS_INIT):
+        fr.run(p)
+    hist_prev = fr.res_hist.copy()
+    a = reuse_renderer(scene1, W, H)
+    a.set_uniform(fr.uniform)
+    tick()
+    a.write_buffer(native.PTX_BUF_GBUFFER, fr.gbuffer)
+    tick()
+    a.write_buffer(native.PTX_BUF_RESERVOIR, fr.reservoir)
+    a.write_buffer(native.PTX_BUF_RESERVOIR_HIST, hist_prev)
+    tick()
+    a.write_buffer(native.PTX_BUF_ACCUM, fr.accum)
+    a.run_pass(native.PTX_PASS_SPATIAL)  # (makes the handle trust the history, as in the pass test)
+    tick()
+    a.write_buffer(native.PTX_BUF_RESERVOIR_HIST, hist_prev)
+    a.run_pass(native.PTX_PASS_TEMPORAL)
+    tick()
+    fr.run(O.PASS_TEMPORAL)
+    assert_same(a.read_reservoir(), fr.reservoir, "temporal output")
+    a.run_pass(native.PTX_PASS_SPATIAL)
+    tick()
+    fr.run(O.PASS_SPATIAL)
+    assert_same(a.read_history(), fr.res_hist, "spatial output")
+    a.run_pass(native.PTX_PASS_FINAL)
+    fr.run(O.PASS_FINAL, reservoir=fr.res_hist)
+    assert_same(a.read_image(), fr.accum, "PT_4 on the spatial output")
+    assert_same(b.read_history(), frb.res_hist, "the other handle's spatial output")
+    assert_same(b.read_image(), frb.accum, "the other handle's radiance")
+    a.close()
+    b.close()

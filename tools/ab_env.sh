@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # A/B of environment knobs on one box: for each "VAR=val ..." line of $AB (newline-separated),
-# one bench run (BENCH_ARGS) -> value per line.  usage: AB=$'PTX_TRACE_SPLIT=1\nPTX_TRACE_SPLIT=2' bash tools/ab_env.sh
+# one bench run (BENCH_ARGS) -> value per line.  usage: AB=$'PTX_AB=TRACE_SPLIT=1\nPTX_AB=TRACE_SPLIT=2' bash tools/ab_env.sh
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Per-kernel A/B: rocprofv3 --kernel-trace --stats of a short single-sequence bench per library
-# (PTX_PIPELINE_FRAMES=0: kernels do not share the chip with a second frame), then the
+# (PTX_AB=PIPELINE_FRAMES=0: kernels do not share the chip with a second frame), then the
 # average duration of every kernel side by side.  usage: LIBS="libptx_a.so libptx.so" bash tools/ab_kernels.sh
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for L in $LIBS; do
-  PTX_LIB_PATH=$P/$L PTX_PIPELINE_FRAMES=0 PTX_TRACE_DYN=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$L" -o run --output-format csv -- \
+  PTX_LIB_PATH=$P/$L PTX_AB=PIPELINE_FRAMES=0,TRACE_DYN=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$L" -o run --output-format csv -- \
       python3 "$R/bench.py" --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/$L.log" 2>&1 || { echo "$L rc=$?"; tail -5 "$OUT/$L.log"; exit 1; }
 done
 python3 - "$OUT" $LIBS <<'PY'

@@ -1,7 +1,7 @@
 """Throughput of H whole-frame handles rendering concurrently (each on its own streams) vs one:
 an upper-bound experiment for pipelining consecutive frames.
 
-usage: PTX_WAVE_STREAMS=2 python tools/concurrent_handles.py --handles 2 [--steps 20]"""
+usage: PTX_AB=WAVE_STREAMS=2 python tools/concurrent_handles.py --handles 2 [--steps 20]"""
 import argparse
 import json
 import os
@@ -44,7 +44,7 @@ def main():
         r.synchronize()
     dt = time.perf_counter() - t
     frames = a.steps * a.handles
-    print(json.dumps({"handles": a.handles, "streams": os.environ.get("PTX_WAVE_STREAMS", "3"),
+    print(json.dumps({"handles": a.handles, "streams": os.environ.get("PTX_AB", ""),
                       "ms_per_frame": 1e3 * dt / frames, "msamples_s": frames * a.width * a.height / dt / 1e6}))
 
 

@@ -8,11 +8,10 @@ cd /tmp && export TMPDIR=/tmp
 # one launch sequence per pass: per-kernel durations then match bench.py's launch-timing
 # region (PTX_FLAG_SINGLE_STREAM); the two-stream production overlap is measured by the
 # bench's headline value, not by per-kernel averages
-export PTX_WAVE_STREAMS=${PTX_WAVE_STREAMS:-1}
-# one frame in flight (frame pipelining overlaps consecutive frames' kernels); the reuse
-# pipeline's whole-band sequences use the dynamic trace batches (PTX_TRACE_DYN=1 here makes
+# and one frame in flight (frame pipelining overlaps consecutive frames' kernels); the reuse
+# pipeline's whole-band sequences use the dynamic trace batches (EXTRA_AB=TRACE_DYN=1 makes
 # the production region run the same kernel mode as bench.py's launch-timed region)
-export PTX_PIPELINE_FRAMES=0
+export PTX_AB="WAVE_STREAMS=1,PIPELINE_FRAMES=0${EXTRA_AB:+,$EXTRA_AB}"
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \

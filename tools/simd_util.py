@@ -4,7 +4,7 @@
 Runs each pass of one 1080p frame with PTX_FLAG_COUNT_WORK and PTX_TRACE_PROF=1 and prints,
 per region (instance transform, root test, node loop, leaf block, triangle loop), the
 wave-level executions, the mean active lanes per execution (of 64) and per-query averages.
-usage: PTX_TRACE_PROF=1 python tools/simd_util.py [--workload restir|mcpt]
+usage: python tools/simd_util.py [--workload restir|mcpt]
 """
 import argparse
 import os
@@ -14,7 +14,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("PTX_TRACE_PROF", "1")
+os.environ["PTX_AB"] = ",".join(v for v in (os.environ.get("PTX_AB", ""), "TRACE_PROF") if v)
 
 from pathtracerdemo_amd import _native as N  # noqa: E402
 from pathtracerdemo_amd.renderer import Renderer  # noqa: E402
