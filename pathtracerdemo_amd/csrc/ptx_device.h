@@ -391,7 +391,9 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t &total) {
     total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     return incl - v;
 }
-template <bool COUNT, bool PROF = false, bool ROOTQ = true, bool ANY = false, bool COOP = false>
+// UNI: `subs` is the workgroup's LDS copy of the root table (like `stack`): pops and root takes
+// share one code path (fewer exec-mask branches per node-loop iteration; same per-lane sequence).
+template <bool COUNT, bool PROF = false, bool ROOTQ = true, bool ANY = false, bool COOP = false, bool UNI = false>
 __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *subs, const Inst *insts, Ray ray,
                                               PassEps eps, uint32_t *stack, uint32_t stride, float t_max = 1e10f,
                                               CoopLds coop = CoopLds{nullptr}, bool want_pos = true) {
@@ -458,11 +460,32 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                 // lane's next node (its push + pop folded), tested in the same iteration.  Per
                 // lane the root tests, pops, tests and pushes are the reference's sequence.
                 for (;;) {
-                    if (__ballot(leaf == 0u && (sp >= 0 || mask != 0u)) == 0ull) break;
-                    if (PROF && leaf == 0u && (sp >= 0 || mask != 0u)) pf.hit(PROF_NODE);
+                    const bool want = leaf == 0u && (sp >= 0 || mask != 0u);
+                    if (__ballot(want) == 0ull) break;
+                    if (PROF && want) pf.hit(PROF_NODE);
                     uint32_t ref = 0u;
                     bool node = false;
-                    if (leaf == 0u && sp < 0 && mask != 0u) {
+                    if (UNI) {
+                        // One path for a pop and a root take (`subs` and the stack both in LDS):
+                        // the next reference is read from the stack top, or -- with an empty stack
+                        // -- from the next queued root's record, through one selected LDS address.
+                        // A root is re-tested only when a hit has moved the bound since the
+                        // pre-filter (else the pre-filter's result is the reference's test).
+                        // (predicated: lanes without work read a valid slot and keep their state)
+                        const bool from_root = sp < 0;
+                        const uint32_t k = (from_root && mask != 0u) ? (uint32_t)__builtin_ctz(mask) : 0u;
+                        const uint32_t *src = from_root ? &roots[s0 + k].ref : &stack[(uint32_t)(from_root ? 0 : sp) * stride];
+                        ref = *src;
+                        const bool tk_root = want && from_root;
+                        bool take = want;
+                        if (tk_root && !(ROOTQ && vy == vy_pf)) take = box_root(lo, inv, roots[s0 + k], vx, vy);
+                        mask = tk_root ? (mask & (mask - 1u)) : mask;
+                        sp = (want && !from_root) ? sp - 1 : sp;
+                        grp = (tk_root && take) ? s0 + k : grp;
+                        const bool is_leaf = (ref & LEAF_BIT) != 0u;
+                        leaf = (take && is_leaf) ? ref : leaf;
+                        node = take && !is_leaf;
+                    } else if (leaf == 0u && sp < 0 && mask != 0u) {
                         const uint32_t k = (uint32_t)__builtin_ctz(mask);
                         mask &= mask - 1u;
                         const SubRoot &R = roots[s0 + k];

@@ -49,7 +49,10 @@ namespace ptx {
 // Every lane of the wave calls the traversal every time -- lanes without a query (past the
 // segment's end, or whose Visibility walk is over) with a NaN bound, which no box overlaps --
 // so the whole wave takes part in the cooperative leaf phases.
-template <bool COUNT, bool PROF, bool OCC>
+#ifndef PTX_NODE_UNI
+#define PTX_NODE_UNI 1  // one pop / root-take path in the node loop when the tables sit in LDS
+#endif
+template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES = false>
 __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
                                             uint32_t *stack, CoopLds coop, const float4 *rays, float4 *res,
                                             uint32_t i, bool active) {
@@ -68,8 +71,8 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
         const float t_max = !active ? __builtin_nanf("") : vis ? fminf(remain, 1e10f) : 1e10f;
         // a Visibility hit's position is only needed to restart through a transmissive surface:
         // it is reconstructed below for those lanes only
-        Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP>(sc, subs, insts, r, eps, stack, WB, t_max, coop,
-                                                                   !vis);
+        Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP, LDS_TABLES && PTX_NODE_UNI>(
+            sc, subs, insts, r, eps, stack, WB, t_max, coop, !vis);
         if (active && !vis) {
             const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
             res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
@@ -183,7 +186,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                 const uint32_t j = w.seg_phys + w.seg_base + lo;
                 const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
                 const uint32_t i = (bi - pref[lo]) * 64u + lane;
-                trace_batch<COUNT, PROF, OCC>(sc, subs, insts, eps, stack, coop,
+                trace_batch<COUNT, PROF, OCC, LDS_TABLES>(sc, subs, insts, eps, stack, coop,
                                               w.rays + 2u * (size_t)j * w.ray_stride,
                                               w.res[round & 1u] + 2u * (size_t)j * w.ray_stride, i, i < n);
             }
@@ -211,7 +214,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     float4 *res = w.res[round & 1u] + 2u * (size_t)j * w.ray_stride;
     for (uint32_t i0 = share * WB; i0 < n; i0 += K * WB) {  // workgroup-uniform
         const uint32_t i = i0 + threadIdx.x;
-        trace_batch<COUNT, PROF, OCC>(sc, subs, insts, eps, stack, coop, rays, res, i, i < n);
+        trace_batch<COUNT, PROF, OCC, LDS_TABLES>(sc, subs, insts, eps, stack, coop, rays, res, i, i < n);
     }
 }
 
