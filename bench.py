@@ -140,18 +140,14 @@ def census(cs, W, H, pipeline, device, passes):
     return out
 
 
-def calibrate_band(cs, W, H, pipeline, device, row_begin, row_end, passes, frames=4):
-    """ms per frame of rows [row_begin, row_end) rendered alone on this rank's GPU (no halo
-    exchange; the pass groups of a band frame), after two untimed frames -- the measured
-    band cost the strong split is re-cut from (bands.recalibrated_costs)."""
-    from pathtracerdemo_amd import _native as N
+def calibrate_band(cs, W, H, pipeline, device, row_begin, row_end, passes, frames=4, overlap=False):
+    """ms per frame of rows [row_begin, row_end) rendered alone on this rank's GPU: the band
+    handle renders its frames exactly as a rank does (pipelined band frames, same launches) but
+    without the halo exchange (PTX_FLAG_HALO_SKIP), after two untimed frames -- the measured band
+    cost the strong split is re-cut from (bands.recalibrated_costs)."""
     from pathtracerdemo_amd.renderer import Renderer
-    pid = {"gbuffer": N.PTX_PASS_GBUFFER, "init": N.PTX_PASS_INIT, "final": N.PTX_PASS_FINAL,
-           "mcpt": N.PTX_PASS_MCPT, "temporal": N.PTX_PASS_TEMPORAL, "spatial": N.PTX_PASS_SPATIAL}
-    ids = [pid[p] for p in passes]
-    cut = ids.index(N.PTX_PASS_SPATIAL) if N.PTX_PASS_SPATIAL in ids else len(ids)
-    front, back = ids[:cut], ids[cut:]
-    r = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end)
+    r = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
+                 halo_overlap=overlap, halo_skip=(row_begin, row_end) != (0, H))
     r.Initialize(cs)
     t0 = 0.0
     for it in range(2 + frames):
@@ -159,9 +155,7 @@ def calibrate_band(cs, W, H, pipeline, device, row_begin, row_end, passes, frame
             r.synchronize()
             t0 = time.perf_counter()
         r.Update()
-        r.run_passes(front)
-        if back:
-            r.run_passes(back)
+        r.Render()
     r.synchronize()
     ms = (time.perf_counter() - t0) / frames * 1e3
     r.close()
@@ -236,7 +230,7 @@ def main():
             calib = {"rounds": []}
             for _ in range(3):
                 b0, b1 = all_bands[rank]
-                cal = calibrate_band(cs, W, H, pipeline, device, b0, b1, passes)
+                cal = calibrate_band(cs, W, H, pipeline, device, b0, b1, passes, overlap=args.halo_overlap)
                 gathered = [None] * world
                 dist.all_gather_object(gathered, cal)
                 calib["rounds"].append({"bands": [list(b) for b in all_bands],

@@ -99,6 +99,11 @@ extern "C" {
                                         the totals of PTX_BUF_COUNTERS stay zero              */
 #define PTX_FLAG_HALO_OVERLAP 128u /* band frames: the spatial pass of the interior rows runs while
                                         the halo is exchanged, the edge rows after it         */
+#define PTX_FLAG_HALO_SKIP 256u    /* a band handle WITHOUT a communicator: ptx_render runs the band
+                                        frame exactly as a rank does (pipelined, same launches)
+                                        but skips the halo exchange -- the halo rows keep what
+                                        they hold, so the edge rows are NOT the split frame's.
+                                        Timing only (a band timed alone: bench.py calibration) */
 /* no variant flag: the wavefront pipeline (compacted ray queues, one trace round per
    path vertex) -- the default */
 

@@ -30,6 +30,7 @@ PTX_FLAG_TIME_LAUNCHES = 16
 PTX_FLAG_SINGLE_STREAM = 32
 PTX_FLAG_ROW_CENSUS = 64
 PTX_FLAG_HALO_OVERLAP = 128
+PTX_FLAG_HALO_SKIP = 256  # band frame without the exchange: timing only (edge rows are not the split frame's)
 PTX_COMM_ID_BYTES = 128
 VARIANT_FLAGS = {"wave": 0, "simple": PTX_FLAG_SIMPLE_KERNELS}
 

@@ -658,11 +658,15 @@ static bool whole_band_sequences(const ptx_handle *h) {
 }
 bool pipelined(const ptx_handle *h) {
     static const bool off = ab_knob("PIPELINE_FRAMES", 1) == 0;  // A/B
+    // band handles (a rank's band of a split frame: communicator, halo rows or HALO_SKIP) pipeline
+    // their band frames the same way (ptx_comm.cpp band_prepare); PTX_AB=PIPELINE_BANDS=0: A/B
+    static const bool bands_off = ab_knob("PIPELINE_BANDS", 1) == 0;
     const uint32_t fl = h->cfg.flags;
+    const bool band = h->comm || h->halo_top || h->halo_bot;
     // at most ~4 Mpx per frame: a 3840x2160 frame's launches are large enough to fill the chip
     // on their own (configs[3] on one GPU: 384 Msamples/s unpipelined, 355 pipelined)
     const size_t px = (size_t)h->band_h * h->cfg.width;
-    return !off && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !h->comm && !h->halo_top && !h->halo_bot &&
+    return !off && !(band && bands_off) && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE &&
            px <= (size_t)4u << 20 &&
            !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK |
                    PTX_FLAG_TIME_LAUNCHES | PTX_FLAG_SINGLE_STREAM | PTX_FLAG_ROW_CENSUS)) &&
@@ -677,7 +681,7 @@ int quiesce(ptx_handle *h) {
     }
     return PTX_OK;
 }
-static void swap_frame_ctx(ptx_handle *h) {
+void swap_frame_ctx(ptx_handle *h) {
     ptx_handle::FrameCtx &a = h->alt;
     std::swap(h->d_gbuf, a.gbuf);
     std::swap(h->d_res, a.res);
@@ -705,7 +709,7 @@ static void swap_frame_ctx(ptx_handle *h) {
 }
 // the second context's G-buffer, reservoirs and stream (its queues, wave state and summaries
 // are allocated by wave_buffers / reuse_buffers on its first frame)
-static int ensure_alt(ptx_handle *h) {
+int ensure_alt(ptx_handle *h) {
     ptx_handle::FrameCtx &a = h->alt;
     if (!h->alt_stream) {
         HIP_CHECK(h, hipStreamCreateWithFlags(&h->alt_stream, hipStreamNonBlocking));
@@ -1114,6 +1118,13 @@ int ptx_render(ptx_handle *h, float *rgba_out) {
                 if ((rc = timed_launch(h, p))) return rc;
     } else if (has_reuse(h) && h->comm) {  // a band of a multi-GPU frame: halo over RCCL
         if (int rc = render_band_nccl(h)) return rc;
+        if (rgba_out) {
+            HIP_CHECK(h, hipMemcpyAsync(rgba_out, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost, h->stream));
+            HIP_CHECK(h, hipStreamSynchronize(h->stream));
+        }
+        return PTX_OK;
+    } else if (has_reuse(h) && (h->halo_top || h->halo_bot) && (h->cfg.flags & PTX_FLAG_HALO_SKIP)) {
+        if (int rc = render_band_solo(h)) return rc;  // (counts its frame)
         if (rgba_out) {
             HIP_CHECK(h, hipMemcpyAsync(rgba_out, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost, h->stream));
             HIP_CHECK(h, hipStreamSynchronize(h->stream));

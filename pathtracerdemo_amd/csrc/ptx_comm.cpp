@@ -141,8 +141,16 @@ BandSets band_sets(const ptx_handle *h, const WaveBufs &w) {
     return b;
 }
 
-// Layout, queue and reuse buffers of a band frame; 1 = not a wavefront band frame.
-int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w) {
+// Layout, queue and reuse buffers of a band frame.  Band frames are pipelined like whole-image
+// frames (pipelined(): two contexts in flight): the frame goes to the other context, and `pipe`
+// tells band_front to run its G-buffer + PT_1 beside the previous frame's exchange, spatial
+// pass and PT_4 (the previous context's stream), its temporal pass after them.  Per context: the
+// G-buffer and reservoirs with their halo rows (what this band sends and receives), summaries,
+// surface records, queues; shared: history, shift jobs, accumulation.  The previous frame's
+// sends read the other context's rows, and a context's next frame starts on its stream after
+// its back passes, which wait for that frame's exchange (ev_halo): nothing is overwritten in
+// flight.
+int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w, bool &pipe) {
     if (!has_reuse(h)) return fail(h, PTX_E_INVALID, "band frames need the reuse or GI pipeline");
     if (h->cfg.flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK))
         return fail(h, PTX_E_INVALID, "band frames run the wavefront kernels (no counting / A-B variants)");
@@ -151,6 +159,12 @@ int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w) {
         if (int rc = build_layout(h)) return rc;
     sc = make_scene(h);
     if (!tables_fit_lds(sc)) return fail(h, PTX_E_SCENE, "band frames need the LDS root / instance tables");
+    pipe = pipelined(h);
+    if (pipe) {
+        if (int rc = ensure_alt(h)) return rc;
+        HIP_CHECK(h, hipEventRecord(h->ev_prev, h->stream));
+        swap_frame_ctx(h);
+    }
     if (int rc = wave_buffers(h, w)) return rc;
     if (int rc = reuse_buffers(h)) return rc;
     hipError_t e = hipSuccess;
@@ -163,14 +177,23 @@ int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w) {
     return PTX_OK;
 }
 
-// G-buffer -> PT_1 -> temporal over the whole band, then ev_front on h->stream.
-int band_front(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *&frame_t) {
+// G-buffer -> PT_1 -> temporal over the whole band, then ev_front on h->stream.  Pipelined:
+// the temporal pass (it reads the previous frame's spatial output and shares its job buffers)
+// waits for ev_prev.
+int band_front(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *&frame_t, bool pipe) {
     frame_t = &h->ring[h->ring_pos];
     h->ring_pos = (h->ring_pos + 1) % kEventRing;
     resolve_event(*frame_t, h);
     HIP_CHECK(h, hipEventRecord(frame_t->start, h->stream));
     static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_TEMPORAL};
-    const hipError_t e = launch_wave_parts(h, sc, w, front, 3);
+    hipError_t e;
+    if (pipe) {
+        e = launch_wave_parts(h, sc, w, front, 2);
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
+        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, front + 2, 1);
+    } else {
+        e = launch_wave_parts(h, sc, w, front, 3);
+    }
     if (e != hipSuccess) return fail(h, PTX_E_HIP, "band front passes: %s", hipGetErrorString(e));
     HIP_CHECK(h, hipEventRecord(h->ev_front, h->stream));
     return PTX_OK;
@@ -304,9 +327,10 @@ int render_band_nccl(ptx_handle *h) {
     if (int rc = comm_health(h)) return rc;
     Scene sc{};
     WaveBufs w{};
-    if (int rc = band_prepare(h, sc, w)) return rc;
+    bool pipe = false;
+    if (int rc = band_prepare(h, sc, w, pipe)) return rc;
     TimedLaunch *ft = nullptr;
-    if (int rc = band_front(h, sc, w, ft)) return rc;
+    if (int rc = band_front(h, sc, w, ft, pipe)) return rc;
     hipStream_t xs;
     if (int rc = exchange_stream(h, xs)) return rc;
     NCCL_CHECK(h, rccl().group_start());
@@ -316,6 +340,21 @@ int render_band_nccl(ptx_handle *h) {
     if (h->halo_top) h->halo_bytes_sent += send_up(h).gb + send_up(h).rb;
     if (h->halo_bot) h->halo_bytes_sent += send_down(h).gb + send_down(h).rb;
     if (int r2 = halo_landed(h, xs)) return r2;
+    return band_back(h, sc, w, ft);
+}
+
+// PTX_FLAG_HALO_SKIP: the same band frame without the exchange (the halo rows keep what they
+// hold) -- a rank's band timed alone on one GPU (bench.py's band calibration, tools/band_alone.py).
+int render_band_solo(ptx_handle *h) {
+    Scene sc{};
+    WaveBufs w{};
+    bool pipe = false;
+    if (int rc = band_prepare(h, sc, w, pipe)) return rc;
+    TimedLaunch *ft = nullptr;
+    if (int rc = band_front(h, sc, w, ft, pipe)) return rc;
+    hipStream_t xs;
+    if (int rc = exchange_stream(h, xs)) return rc;
+    if (int rc = halo_landed(h, xs)) return rc;
     return band_back(h, sc, w, ft);
 }
 
@@ -425,8 +464,9 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
     std::vector<hipStream_t> xs(n);
     for (int i = 0; i < n; ++i) {
         HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
-        if (int rc = band_prepare(hs[i], sc[i], w[i])) return rc;
-        if (int rc = band_front(hs[i], sc[i], w[i], ft[i])) return rc;
+        bool pipe = false;
+        if (int rc = band_prepare(hs[i], sc[i], w[i], pipe)) return rc;
+        if (int rc = band_front(hs[i], sc[i], w[i], ft[i], pipe)) return rc;
     }
     for (int i = 0; i < n; ++i)
         if (int rc = exchange_stream(hs[i], xs[i])) return rc;

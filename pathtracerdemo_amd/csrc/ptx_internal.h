@@ -84,7 +84,7 @@ struct ptx_handle {
     uint32_t census_blocks = 0;
     // diagnostic build (PTX_WG_TIMES) with PTX_WGT=1 in the environment: per-wave timing records
     DevBuf d_wgt;
-    // Frame pipelining (pipelined(): whole-image reuse handles on their own streams): two frames
+    // Frame pipelining (pipelined(): reuse handles on their own streams, whole-image or band): two frames
     // in flight, each with its own G-buffer, reservoirs, neighbour summaries, wave state,
     // queues and streams.  Frame N's G-buffer + PT_1 run beside frame N-1's spatial pass + PT_4;
     // its temporal pass (which reads frame N-1's spatial output, d_hist, and reuses the shared
@@ -151,9 +151,14 @@ void mark_history(ptx_handle *h);
 // frames' streams (before anything that replaces shared buffers or the stream)
 bool pipelined(const ptx_handle *h);
 int quiesce(ptx_handle *h);
+// the second frame context's G-buffer, reservoirs and stream; swap the two contexts
+int ensure_alt(ptx_handle *h);
+void swap_frame_ctx(ptx_handle *h);
 // back to the first frame context (quiesce + swap) before the handle's stream or mode changes
 int leave_alt(ptx_handle *h);
-// ptx_comm.cpp: a frame of a band handle that owns a communicator; its teardown
+// ptx_comm.cpp: a frame of a band handle that owns a communicator; a band frame without the
+// exchange (PTX_FLAG_HALO_SKIP, timing only); the communicator's teardown
 int render_band_nccl(ptx_handle *h);
+int render_band_solo(ptx_handle *h);
 void comm_destroy(ptx_handle *h);
 }  // namespace ptx

@@ -24,7 +24,7 @@ class Renderer:
                  row_begin: int = 0, row_end: int = 0, count_work: bool = False, variant: str = "wave",
                  time_launches: bool = False, single_stream: bool = False, reuse_radius: int = 0,
                  reuse_neighbors: int = 0, temporal_cap: int = 0, row_census: bool = False,
-                 halo_overlap: bool = False):
+                 halo_overlap: bool = False, halo_skip: bool = False):
         self._lib = N.load()
         self.width, self.height = int(width), int(height)
         self.pipeline = pipeline
@@ -36,7 +36,8 @@ class Renderer:
                           | (N.PTX_FLAG_TIME_LAUNCHES if time_launches else 0)
                           | (N.PTX_FLAG_SINGLE_STREAM if single_stream else 0)
                           | (N.PTX_FLAG_ROW_CENSUS if row_census else 0)
-                          | (N.PTX_FLAG_HALO_OVERLAP if halo_overlap else 0))
+                          | (N.PTX_FLAG_HALO_OVERLAP if halo_overlap else 0)
+                          | (N.PTX_FLAG_HALO_SKIP if halo_skip else 0))
         self._h = ctypes.c_void_p()
         rc = self._lib.ptx_create(ctypes.byref(cfg), ctypes.byref(self._h))
         if rc != N.PTX_OK:

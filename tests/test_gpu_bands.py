@@ -149,3 +149,46 @@ def test_row_census(scene3, oracle_mod, native):
         if p in (native.PTX_PASS_INIT, native.PTX_PASS_SPATIAL):  # (temporal / final may trace nothing)
             assert tot[0] > 0
     assert_same(cen.read_history(), cnt.read_history(), "census handle frame")
+
+
+def test_halo_skip_band_interior_rows(scene3):
+    """PTX_FLAG_HALO_SKIP (a band timed alone, bench.py's calibration): the band renders its
+    frames through the rank's band path (pipelined) without the exchange.  Frame f's spatial pass
+    reads rows up to R away, whose temporal output carries frame f-1's spatial output there (the
+    history): a stale halo reaches f * R rows into the band after f frames, and the rows farther
+    than that from both band edges equal the whole frame's."""
+    W, H, R, b0, b1, F = 96, 200, 12, 50, 170, 3
+    one = make(scene3, W, H, radius=R)
+    band = make(scene3, W, H, radius=R, row_begin=b0, row_end=b1, halo_skip=True)
+    for _ in range(F):
+        for r in (one, band):
+            r.Update()
+            r.Render()
+    lo, hi = F * R, (b1 - b0) - F * R
+    assert_same(band.read_history()[lo:hi], one.read_history()[b0 + lo:b0 + hi], "interior spatial output")
+    assert_same(band.read_image()[lo:hi], one.read_image()[b0 + lo:b0 + hi], "interior radiance")
+    assert band.stats()["frames"] == 3
+    one.close()
+    band.close()
+
+
+def test_pipelined_band_frames_with_host_reads(scene3):
+    """Band frames run two in flight (the next frame's G-buffer + PT_1 beside this frame's
+    exchange, spatial pass and PT_4): host reads between frames see the latest frame, and the
+    split still equals the single handle after every frame."""
+    from pathtracerdemo_amd.renderer import Renderer
+    W, H = 160, 120
+    one = make(scene3, W, H)
+    bands = [make(scene3, W, H, row_begin=a, row_end=b) for a, b in ((0, 37), (37, 90), (90, 120))]
+    img = np.zeros((H, W, 4), np.float32)
+    for f in range(4):
+        one.Update()
+        one.Render()
+        for b in bands:
+            b.Update()
+        Renderer.render_bands(bands, img if f % 2 else None)
+        hist = np.concatenate([b.read_history() for b in bands])
+        assert_same(hist, one.read_history(), f"spatial output, frame {f + 1}")
+        assert_same(np.concatenate([b.read_image() for b in bands]), one.read_image(), f"radiance, frame {f + 1}")
+    for r in [one] + bands:
+        r.close()

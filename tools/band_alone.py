@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-band frame time of a strong-scaled frame, one band per PROCESS (as a rank sees it:
-one handle, its own streams), each timed alone on the idle GPU with bench.calibrate_band.
+one handle, its own streams), each timed alone on the idle GPU with bench.calibrate_band
+(the band path a rank runs, pipelined, without the exchange: PTX_FLAG_HALO_SKIP).
 `tools/band_timing.py` times all bands from one process, where 9 handles' streams share the
 process's hardware queues.  usage: python tools/band_alone.py [--world 8] [--bands census|calibrated]
 prints one JSON line: bands, per-band ms, max/mean, implied speedup over the one-GPU frame."""
@@ -13,11 +14,11 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run_band(W, H, b0, b1, scene):
+def run_band(W, H, b0, b1, scene, overlap=False):
     code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
             f"from pathtracerdemo_amd.scene.world import compile_scene; "
             f"cs = compile_scene({scene!r}); "
-            f"print(bench.calibrate_band(cs, {W}, {H}, 'reuse', 0, {b0}, {b1}, bench.PASSES['reuse'], frames=6))")
+            f"print(bench.calibrate_band(cs, {W}, {H}, 'reuse', 0, {b0}, {b1}, bench.PASSES['reuse'], frames=6, overlap={overlap}))")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     if out.returncode != 0:
         sys.exit(f"band {b0}-{b1} failed: {out.stderr[-2000:]}")
@@ -31,6 +32,7 @@ def main():
     ap.add_argument("--scene", default="c3_interior_32")
     ap.add_argument("--bands", default=None, help="JSON list of [b0, b1]; default: equal bands")
     ap.add_argument("--recut", type=int, default=0, help="re-cut rounds from the measured times")
+    ap.add_argument("--overlap", action="store_true", help="bands with PTX_FLAG_HALO_OVERLAP")
     args = ap.parse_args()
     sys.path.insert(0, ROOT)
     import numpy as np
@@ -40,7 +42,7 @@ def main():
     costs = np.ones(H)
     rounds = []
     for it in range(args.recut + 1):
-        ms = [run_band(W, H, b0, b1, args.scene) for b0, b1 in bands]
+        ms = [run_band(W, H, b0, b1, args.scene, args.overlap) for b0, b1 in bands]
         rounds.append({"bands": bands, "band_ms": [round(v, 4) for v in ms],
                        "max_over_mean": round(max(ms) / (sum(ms) / len(ms)), 4), "sum_ms": round(sum(ms), 3)})
         print(json.dumps(rounds[-1]), flush=True)
