@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -99,6 +100,73 @@ static inline float as_f32(uint32_t u) {
     float f;
     std::memcpy(&f, &u, 4);
     return f;
+}
+
+// The instance cull's world box (Inst::wlo / whi / wpad / wscale, inst_may_hit in ptx_device.h):
+// the union of the instance's sub-mesh root boxes in local space, mapped to world space through
+// the inverse of M^-1 (the matrix the kernels transform rays with; M itself may differ from that
+// inverse by rounding) in double precision, its 8 corners' bounds rounded outward to f32.  The
+// pad covers the f32 rounding of the kernels' ray transform with >= 40x margin: 1e-5 of the
+// local box's and M^-1's translation magnitudes mapped through |A^-1| (A = M^-1's linear part),
+// and per ray 1e-5 * cond(A) * max|o| (wscale).  Never culled (wpad = -1): a projective or
+// singular M^-1, non-finite values, an instance without sub-meshes.
+static void inst_world_box(Inst &I, const SubRoot *roots, uint32_t nsub) {
+    I.wpad = -1.0f;
+    I.wscale = 0.0f;
+    for (int k = 0; k < 3; ++k) I.wlo[k] = I.whi[k] = 0.0f;
+    const float *m = I.minv;  // column-major: local = A * world + t
+    if (nsub == 0 || m[3] != 0.0f || m[7] != 0.0f || m[11] != 0.0f || m[15] != 1.0f) return;
+    double A[3][3], t[3];
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) A[r][c] = m[4 * c + r];
+        t[r] = m[12 + r];
+    }
+    const double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) - A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                       A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+    if (!std::isfinite(det) || std::fabs(det) < 1e-30) return;
+    double B[3][3];  // A^-1
+    B[0][0] = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det;
+    B[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+    B[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det;
+    B[1][0] = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+    B[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det;
+    B[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+    B[2][0] = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det;
+    B[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+    B[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+    double lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) { lo[k] = HUGE_VAL; hi[k] = -HUGE_VAL; }
+    for (uint32_t s = 0; s < nsub; ++s) {
+        const float *ax[3] = {roots[s].x, roots[s].y, roots[s].z};
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], (double)ax[k][0]); hi[k] = std::max(hi[k], (double)ax[k][1]); }
+    }
+    double lmax = 0.0, tmax = 0.0, na = 0.0, nb = 0.0;  // magnitudes, |A|inf, |A^-1|inf
+    for (int k = 0; k < 3; ++k) {
+        if (!std::isfinite(lo[k]) || !std::isfinite(hi[k]) || lo[k] > hi[k]) return;
+        lmax = std::max({lmax, std::fabs(lo[k]), std::fabs(hi[k])});
+        tmax = std::max(tmax, std::fabs(t[k]));
+        na = std::max(na, std::fabs(A[k][0]) + std::fabs(A[k][1]) + std::fabs(A[k][2]));
+        nb = std::max(nb, std::fabs(B[k][0]) + std::fabs(B[k][1]) + std::fabs(B[k][2]));
+    }
+    double wlo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, whi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL}, wmax = 0.0;
+    for (int c = 0; c < 8; ++c) {
+        const double p[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
+        for (int r = 0; r < 3; ++r) {
+            const double w = B[r][0] * (p[0] - t[0]) + B[r][1] * (p[1] - t[1]) + B[r][2] * (p[2] - t[2]);
+            wlo[r] = std::min(wlo[r], w);
+            whi[r] = std::max(whi[r], w);
+            wmax = std::max(wmax, std::fabs(w));
+        }
+    }
+    const double pad = 1e-5 * (1.0 + wmax) + 1e-5 * nb * (lmax + tmax);
+    const double scale = 1e-5 * std::max(1.0, na * nb);
+    if (!std::isfinite(pad) || !std::isfinite(scale) || !std::isfinite(wmax)) return;
+    for (int k = 0; k < 3; ++k) {
+        I.wlo[k] = std::nextafter((float)wlo[k], -HUGE_VALF);
+        I.whi[k] = std::nextafter((float)whi[k], HUGE_VALF);
+    }
+    I.wpad = std::nextafter((float)pad, HUGE_VALF);
+    I.wscale = std::nextafter((float)scale, HUGE_VALF);
 }
 
 // ---------------------------------------------------------------- layout derivation
@@ -244,6 +312,7 @@ int build_layout(ptx_handle *h) {
         // instance reduce to x + 0 (inst_point, ptx_device.h) with the same bits
         static const float kId[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
         if (!std::memcmp(I.m, kId, sizeof kId) && !std::memcmp(I.minv, kId, sizeof kId)) I.mesh |= kInstIdentity;
+        inst_world_box(I, subs.data() + I.sub_base, I.nsub);
     }
     if (tris.empty()) tris.resize(12, 0.0f);
     if (tverts.empty()) tverts.resize(20, 0.0f);

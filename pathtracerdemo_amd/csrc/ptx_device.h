@@ -58,10 +58,15 @@ struct alignas(16) SubRoot {    // 32 B: the root box by axis, {min, max} pairs 
     float x[2], y[2], z[2];
     uint32_t ref, pad;
 };
-struct alignas(16) Inst {       // 144 B
+struct alignas(16) Inst {       // 176 B
     float m[16];
     float minv[16];
     uint32_t mesh, sub_base, nsub, tri_base;  // mesh: | kInstIdentity when M and M^-1 are exactly I
+    // Conservative world-space box of the instance's sub-mesh roots (inst_may_hit): the local
+    // root boxes' union mapped back through (M^-1)^-1 in double precision, rounded outward; a ray
+    // is tested against it padded by wpad + wscale * max|o| (wpad < 0: never culled)
+    float wlo[3], wpad;
+    float whi[3], wscale;
 };
 constexpr uint32_t kInstIdentity = 0x80000000u;
 
@@ -337,6 +342,32 @@ __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, Pa
     const float U = best.s.bu, V = best.s.bv, W = 1.0f - U - V;
     best.pos = (A * U + B * V) + C * W;
 }
+// Instance cull (not in the reference, which transforms every ray into every instance and tests
+// every sub-mesh root, SH/PT_1_InitPass.wgsl:613-624): may this ray (world origin o, reciprocal
+// direction winv) reach a root of instance I within [0, vy]?  The test is conservative: a ray
+// whose local-space root test passes (the point lo + t ld, lo = M^-1 o, ld = M^-1 (o + d) - lo,
+// lies in a root box for some t in [vx, vy]) runs within the f32 rounding of the transform -- a
+// relative 1e-7 of the coordinates -- of the world box the host maps the local union box to,
+// and the box is padded by 1e-5 of the coordinates' magnitude (>= 40x that rounding) plus
+// 2^-12 * max|o| for the ray origin's own rounding, so such a ray always passes here.  A NaN bound
+// (an idle lane) never passes, as no root test would.  The counting build checks the claim on
+// every query it traces (CNT_CULL_MISS: a culled lane whose root pre-filter passed) without
+// culling; the other builds skip an instance when no lane of the wave may reach it.
+constexpr int CNT_CULL_MISS = 5;
+__device__ __forceinline__ bool inst_may_hit(const Inst &I, f3 o, f3 winv, float omax, float vy) {
+    if (!(I.wpad >= 0.0f)) return true;
+    const float p = I.wpad + I.wscale * omax;
+    const float t0x = ((I.wlo[0] - p) - o.x) * winv.x, t1x = ((I.whi[0] + p) - o.x) * winv.x;
+    const float t0y = ((I.wlo[1] - p) - o.y) * winv.y, t1y = ((I.whi[1] + p) - o.y) * winv.y;
+    const float t0z = ((I.wlo[2] - p) - o.z) * winv.z, t1z = ((I.whi[2] + p) - o.z) * winv.z;
+    const float tmin = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z));
+    const float tmax = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z));
+    return tmin <= tmax && tmax >= 0.0f && tmin <= vy + fabsf(vy) * 0x1p-10f + 1e-3f;
+}
+#ifndef PTX_INST_CULL
+#define PTX_INST_CULL 1
+#endif
+
 // TraceRay (SH/PT_1_InitPass.wgsl:605-715; PT_01:509-621): closest hit over every
 // instance and sub-mesh root, ordered-stack BLAS traversal, ties replace (`if (best < t)
 // continue`).  `stack` is this thread's column of the workgroup's LDS stack
@@ -408,9 +439,15 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     uint32_t n_aabb = 0, n_tri = 0;
     bool stop = false;
     const bool wave_coop = COOP && __ballot(1) == ~0ull;  // wave-uniform
+    // instance cull inputs (inst_may_hit): a ray with a non-finite component is never culled
+    const bool rfin = finite3(ray.o) && finite3(ray.d);
+    const f3 winv = mk(__builtin_amdgcn_rcpf(ray.d.x), __builtin_amdgcn_rcpf(ray.d.y), __builtin_amdgcn_rcpf(ray.d.z));
+    const float omax = fmaxf(fmaxf(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z));
     // (with COOP an occluded lane keeps iterating, without work, so the wave stays whole)
     for (uint32_t ii = 0; ii < sc.n_inst && (COOP || !stop); ++ii) {
         const Inst &I = insts[ii];
+        const bool may = !PTX_INST_CULL || !rfin || inst_may_hit(I, ray.o, winv, omax, vy);
+        if (PTX_INST_CULL && !COUNT && __ballot(may) == 0ull) continue;  // (wave-uniform)
         if (PROF) pf.hit(PROF_INST);
         // TransformRayWithMat4x4(InRay, M^-1, false), SH/PT_1_InitPass.wgsl:486-496
         // (the identity shortcut of inst_point is not used here: at the trace kernel's 128-VGPR
@@ -440,6 +477,8 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                     if (PROF) pf.hit(PROF_ROOT);
                     if (box_root(lo, inv, roots[s0 + k], vx, vy)) mask |= 1u << k;
                 }
+                if (COUNT && PTX_INST_CULL && !may && mask != 0u && t_max == t_max)
+                    atomicAdd(&sc.counters[CNT_CULL_MISS], 1ull);
             } else {
                 if (PROF) pf.hit(PROF_ROOT);
                 if (box_root(lo, inv, roots[s0 + kk], vx, vy)) mask = 1u << kk;

@@ -202,8 +202,10 @@ class Renderer:
     def read_counters(self) -> dict:
         c = np.zeros(8, dtype=np.uint64)
         self._call("ptx_read_buffer", self._h, N.PTX_BUF_COUNTERS, c.ctypes.data, c.nbytes)
+        # cull_misses: queries of the counting build whose instance cull would have skipped an
+        # instance with a root its pre-filter passes (the cull's conservativeness check: always 0)
         return {"rays": int(c[0]), "instance_xforms": int(c[1]), "aabb_tests": int(c[2]), "tri_tests": int(c[3]),
-                "hits": int(c[4])}
+                "hits": int(c[4]), "cull_misses": int(c[5])}
 
     def stats(self) -> dict:
         s = N.PtxStats()

@@ -294,7 +294,8 @@ def test_trace_work_counters_match_oracle(scene1, oracle_mod):
     r.reset_stats()
     got = r.trace(rays, 1)
     np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
-    assert r.read_counters() == c_or
+    c_gpu = r.read_counters()
+    assert {k: c_gpu[k] for k in c_or} == c_or
 
 
 def test_work_counters_match_oracle(scene1, oracle_mod, native):
@@ -308,4 +309,5 @@ def test_work_counters_match_oracle(scene1, oracle_mod, native):
     r.run_pass(native.PTX_PASS_GBUFFER)
     r.synchronize()
     c_gpu = r.read_counters()
-    assert c_gpu == c_or
+    assert {k: c_gpu[k] for k in c_or} == c_or
+    assert c_gpu["cull_misses"] == 0  # (the instance cull, evaluated on every G-buffer ray)

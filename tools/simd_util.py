@@ -27,8 +27,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="restir", choices=["restir", "mcpt", "reuse"])
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--scene", default=None, help="default: c3_interior_32 (reuse), dummy_scene_1 (others)")
 args = ap.parse_args()
-cs = compile_scene("c3_interior_32" if args.workload == "reuse" else "dummy_scene_1")
+cs = compile_scene(args.scene or ("c3_interior_32" if args.workload == "reuse" else "dummy_scene_1"))
 r = Renderer(args.width, args.height, device=0, pipeline=args.workload, count_work=True)
 r.Initialize(cs)
 r.Update()
