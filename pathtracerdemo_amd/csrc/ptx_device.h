@@ -670,6 +670,220 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     }
     return best;
 }
+// The same walk with the instance loop flattened into the lanes (trace_queue's form: whole-wave
+// calls, root and instance tables in LDS).  Each lane keeps its own place in the instance list:
+// a lane whose roots and stack of one instance are exhausted moves on to the next instance its
+// ray may reach (inst_may_hit) at the next refill -- after the current leaf phase -- instead of
+// idling until every lane of the wave has finished that instance; lanes in different instances
+// share the node loop and the cooperative leaf phases (the owner's triangle base travels with
+// its ray).  Per lane the order of instances, roots, pops, node tests, pushes and triangle
+// tests is the reference's (SH/PT_1_InitPass.wgsl:605-715), so hits, ties and work counts are
+// unchanged; a leaf phase in which a lane computed a NaN t runs its leaves sequentially.
+template <bool COUNT, bool PROF = false, bool ANY = false>
+__device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *subs, const Inst *insts, Ray ray,
+                                               PassEps eps, uint32_t *stack, uint32_t stride, float t_max,
+                                               CoopLds coop, bool want_pos) {
+    Prof pf{};
+    Hit best;
+    best.valid = false;
+    best.t = 0.0f;
+    best.s = Compact{0u, 0u, 0u, 0u, 0.0f, 0.0f};
+    best.pos = mk(0.0f, 0.0f, 0.0f);
+    const float vx = 1e-4f;
+    float vy = t_max;
+    uint32_t n_aabb = 0, n_tri = 0;
+    const bool counted = t_max == t_max;  // a NaN bound: an idle lane keeping its wave whole
+    const bool rfin = finite3(ray.o) && finite3(ray.d);
+    const float omax = fmaxf(fmaxf(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z));
+    uint32_t next = 0u;                       // the next instance to consider
+    uint32_t cur = 0u, s0 = 0u, nsub = 0u;    // the instance walked, its root chunk, its root count
+    uint32_t sub_base = 0u, tri_base = 0u;
+    bool done = !counted;                     // (no box passes a NaN bound: nothing to walk)
+    f3 lo = mk(0.0f, 0.0f, 0.0f), ld = lo, inv = lo;
+    uint32_t mask = 0u, grp = 0u, leaf = 0u;
+    int sp = -1;
+    float vy_pf = vy;
+    for (;;) {
+        // refill: a lane with no leaf, no stack and no queued root takes its instance's next
+        // chunk of 32 roots or its next instance (transform + root pre-filter)
+        for (;;) {
+            const bool need = !done && leaf == 0u && sp < 0 && mask == 0u;
+            if (__ballot(need) == 0ull) break;
+            if (need) {
+                bool may = true;
+                if (s0 + 32u < nsub) {
+                    s0 += 32u;
+                } else {
+                    const f3 winv = mk(__builtin_amdgcn_rcpf(ray.d.x), __builtin_amdgcn_rcpf(ray.d.y),
+                                       __builtin_amdgcn_rcpf(ray.d.z));
+                    // (COUNT: every instance is walked; the cull is only checked below)
+                    while (next < sc.n_inst) {
+                        may = !PTX_INST_CULL || !rfin || inst_may_hit(insts[next], ray.o, winv, omax, vy);
+                        if (may || COUNT) break;
+                        ++next;
+                    }
+                    if (next >= sc.n_inst) {
+                        done = true;
+                    } else {
+                        cur = next++;
+                        const Inst &I = insts[cur];
+                        if (PROF) pf.hit(PROF_INST);
+                        // TransformRayWithMat4x4(InRay, M^-1, false), SH/PT_1_InitPass.wgsl:486-496
+                        lo = xform_point(I.minv, ray.o);
+                        const f3 le = xform_point(I.minv, ray.o + ray.d);
+                        ld = le - lo;
+                        inv = mk(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
+                        sub_base = I.sub_base;
+                        nsub = I.nsub;
+                        tri_base = I.tri_base;
+                        s0 = 0u;
+                        n_aabb += nsub;  // the reference tests every sub-mesh root once
+                    }
+                }
+                if (!done && nsub != 0u) {
+                    // pre-filter: every root of the chunk against the best t at this point (the
+                    // reference tests root s with the best t after roots < s, never larger; the
+                    // exact test is repeated when a root is taken, below)
+                    const uint32_t nc = nsub - s0 < 32u ? nsub - s0 : 32u;
+#pragma unroll 1
+                    for (uint32_t k = 0; k < nc; ++k) {
+                        if (PROF) pf.hit(PROF_ROOT);
+                        if (box_root(lo, inv, subs[sub_base + s0 + k], vx, vy)) mask |= 1u << k;
+                    }
+                    vy_pf = vy;
+                    if (COUNT && PTX_INST_CULL && !may && mask != 0u) atomicAdd(&sc.counters[CNT_CULL_MISS], 1ull);
+                }
+            }
+        }
+        // node loop: pops and root takes through one LDS read (as trace_core_tab UNI)
+        for (;;) {
+            const bool want = leaf == 0u && (sp >= 0 || mask != 0u);
+            if (__ballot(want) == 0ull) break;
+            if (PROF && want) pf.hit(PROF_NODE);
+            const bool from_root = sp < 0;
+            const uint32_t k = (from_root && mask != 0u) ? (uint32_t)__builtin_ctz(mask) : 0u;
+            const SubRoot *R = subs + (sub_base + s0 + k);
+            const uint32_t *src = from_root ? &R->ref : &stack[(uint32_t)(from_root ? 0 : sp) * stride];
+            const uint32_t ref = *src;
+            const bool tk_root = want && from_root;
+            bool take = want;
+            if (tk_root && !(vy == vy_pf)) take = box_root(lo, inv, *R, vx, vy);
+            mask = tk_root ? (mask & (mask - 1u)) : mask;
+            sp = (want && !from_root) ? sp - 1 : sp;
+            grp = (tk_root && take) ? s0 + k : grp;
+            const bool is_leaf = (ref & LEAF_BIT) != 0u;
+            leaf = (take && is_leaf) ? ref : leaf;
+            if (!(take && !is_leaf)) continue;
+            const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + ref);
+            float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+            uint32_t lref = __float_as_uint(q3.x), rref = __float_as_uint(q3.y);
+            float tl, tr;
+            bool hl, hr;
+            box_pair(lo, inv, q0, q1, q2, vx, vy, hl, hr, tl, tr);
+            n_aabb += 2;
+            const bool both = hl && hr;
+            const uint32_t near = tl < tr ? lref : rref, far = tl < tr ? rref : lref;
+            stack[(uint32_t)(sp + 1) * stride] = both ? far : (hl ? lref : rref);
+            stack[(uint32_t)(sp + 2) * stride] = near;
+            sp += both ? 2 : ((hl || hr) ? 1 : 0);
+        }
+        const unsigned long long holders = __ballot(leaf != 0u);
+        if (holders == 0ull) {
+            if (__ballot(!done) == 0ull) break;  // every lane has walked every instance
+            continue;
+        }
+        // cooperative leaf phase (trace_core_tab COOP), the owner's triangle base included
+        if (PROF) pf.hit(PROF_LEAF);
+        const uint32_t lane = __lane_id();
+        const uint32_t cnt = leaf ? (leaf >> 24) & 0x7Fu : 0u, lfirst = leaf & LEAF_FIRST_MASK;
+        uint32_t total;
+        const uint32_t excl = wave_excl_sum(cnt, total);
+        __hip_atomic_store(&coop.key[lane], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        bool nan_seen = false;
+        for (uint32_t c0 = 0; c0 < total; c0 += 64u) {
+            const uint32_t u = c0 + lane;
+            __hip_atomic_store(&coop.mark[lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            if (cnt != 0u && excl >= c0 && excl - c0 < 64u)
+                __hip_atomic_store(&coop.mark[excl - c0], lane + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            uint32_t m = __hip_atomic_load(&coop.mark[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const unsigned long long before = __ballot(cnt != 0u && excl < c0);
+            if (lane == 0u && before != 0ull) m = max(m, 64u - (uint32_t)__builtin_clzll(before));
+            const int owner = (int)wave_incl_max(m) - 1;
+            // triangle u of the deal: the owner's leaf triangle lfirst + (u - excl), in its instance
+            const uint32_t tri = u + __shfl(lfirst - excl, owner);
+            const uint32_t tb = __shfl(tri_base, owner);
+            const f3 olo = mk(__shfl(lo.x, owner), __shfl(lo.y, owner), __shfl(lo.z, owner));
+            const f3 old = mk(__shfl(ld.x, owner), __shfl(ld.y, owner), __shfl(ld.z, owner));
+            const float ovy = __shfl(vy, owner);
+            if (u < total) {
+                if (PROF) pf.hit(PROF_TRI);
+                const float4 *tp = sc.tris + 3u * (tb + tri);
+                const float t = ray_tri(olo, old, tp[0], tp[1], tp[2], eps.det_eps);
+                if (t != t) nan_seen = true;
+                else if (!(ovy < t))
+                    atomicMin(&coop.key[owner],
+                              ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)(0xffffffffu - tri));
+            }
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (__ballot(nan_seen) == 0ull) {
+            if (leaf) {
+                const unsigned long long key = __hip_atomic_load(&coop.key[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                n_tri += cnt;
+                if (key != ~0ull) {
+                    vy = __uint_as_float((uint32_t)(key >> 32));
+                    best.valid = true;
+                    best.s.inst = cur;
+                    best.s.mat = grp;
+                    best.s.prim = 0xffffffffu - (uint32_t)key;
+                }
+            }
+        } else if (leaf) {  // a NaN t somewhere in the wave: this phase's leaves one by one
+            const uint32_t first = leaf & LEAF_FIRST_MASK, count = (leaf >> 24) & 0x7Fu;
+            const float4 *tp = sc.tris + 3u * (tri_base + first);
+            for (uint32_t k = 0; k < count; ++k) {
+                if (PROF) pf.hit(PROF_TRI);
+                const float t = ray_tri(lo, ld, tp[3u * k + 0u], tp[3u * k + 1u], tp[3u * k + 2u], eps.det_eps);
+                ++n_tri;
+                if (vy < t) continue;
+                vy = t;
+                best.valid = true;
+                best.s.inst = cur;
+                best.s.mat = grp;
+                best.s.prim = first + k;
+                if (ANY) break;
+            }
+        }
+        leaf = 0u;
+        if (ANY && best.valid && !done) {  // occluded: no more work for this lane
+            done = true;
+            sp = -1;
+            mask = 0u;
+        }
+    }
+    if (PROF && counted) {
+        for (int r = 0; r < PROF_REGIONS; ++r) {
+            if (pf.wave[r]) atomicAdd(&sc.counters[8 + 2 * r], (unsigned long long)pf.wave[r]);
+            if (pf.lane[r]) atomicAdd(&sc.counters[9 + 2 * r], (unsigned long long)pf.lane[r]);
+        }
+    }
+    if (COUNT && counted) {
+        atomicAdd(&sc.counters[CNT_RAYS], 1ull);
+        atomicAdd(&sc.counters[CNT_INST], (unsigned long long)sc.n_inst);
+        atomicAdd(&sc.counters[CNT_AABB], (unsigned long long)n_aabb);
+        atomicAdd(&sc.counters[CNT_TRI], (unsigned long long)n_tri);
+        if (best.valid) atomicAdd(&sc.counters[CNT_HITS], 1ull);
+    }
+    if (best.valid) {
+        best.t = vy;
+        if (!ANY && want_pos) complete_hit(sc, ray, eps, best, insts);
+    }
+    return best;
+}
+
 // Sub-root and instance tables staged in LDS when they fit: every ray tests every root of
 // every instance, ~16 table reads per query otherwise paid as scalar-load round trips.  The
 // tables sit at the start of the kernel's dynamic LDS, sized to the scene (32 B per sub-mesh

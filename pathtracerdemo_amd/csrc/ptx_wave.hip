@@ -52,7 +52,13 @@ namespace ptx {
 #ifndef PTX_NODE_UNI
 #define PTX_NODE_UNI 1  // one pop / root-take path in the node loop when the tables sit in LDS
 #endif
-template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES = false>
+#ifndef PTX_FLAT_INST
+#define PTX_FLAT_INST 1  // the instance loop flattened into the lanes (trace_core_flat) for scenes
+#endif                   // of >= kFlatMinInstances instances (host side, wave_trace)
+// Measured same box (1080p): furnished C3 (13 instances) +9.7 %, GI on C3 (3) +3.2 %, reuse on
+// C3 +0.6 %, TEST_MCPT on C1 (2 instances) -3.2 %: flattened from 3 instances up.
+constexpr uint32_t kFlatMinInstances = 3u;
+template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES = false, bool FLAT = false>
 __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
                                             uint32_t *stack, CoopLds coop, const float4 *rays, float4 *res,
                                             uint32_t i, bool active) {
@@ -71,8 +77,10 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
         const float t_max = !active ? __builtin_nanf("") : vis ? fminf(remain, 1e10f) : 1e10f;
         // a Visibility hit's position is only needed to restart through a transmissive surface:
         // it is reconstructed below for those lanes only
-        Hit h = trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP, LDS_TABLES && PTX_NODE_UNI>(
-            sc, subs, insts, r, eps, stack, WB, t_max, coop, !vis);
+        Hit h = (LDS_TABLES && FLAT)
+                    ? trace_core_flat<COUNT, PROF, OCC>(sc, subs, insts, r, eps, stack, WB, t_max, coop, !vis)
+                    : trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP, LDS_TABLES && PTX_NODE_UNI>(
+                          sc, subs, insts, r, eps, stack, WB, t_max, coop, !vis);
         if (active && !vis) {
             const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
             res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
@@ -130,7 +138,7 @@ __device__ __forceinline__ void dyn_prefix(const WaveBufs &w, uint32_t round, ui
     __syncthreads();
 }
 
-template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true, bool OCC = false>
+template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true, bool OCC = false, bool FLAT = false>
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     PTX_WAVE_TIMER(sc, KID_TRACE);
@@ -186,7 +194,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                 const uint32_t j = w.seg_phys + w.seg_base + lo;
                 const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
                 const uint32_t i = (bi - pref[lo]) * 64u + lane;
-                trace_batch<COUNT, PROF, OCC, LDS_TABLES>(sc, subs, insts, eps, stack, coop,
+                trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
                                               w.rays + 2u * (size_t)j * w.ray_stride,
                                               w.res[round & 1u] + 2u * (size_t)j * w.ray_stride, i, i < n);
             }
@@ -214,7 +222,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     float4 *res = w.res[round & 1u] + 2u * (size_t)j * w.ray_stride;
     for (uint32_t i0 = share * WB; i0 < n; i0 += K * WB) {  // workgroup-uniform
         const uint32_t i = i0 + threadIdx.x;
-        trace_batch<COUNT, PROF, OCC, LDS_TABLES>(sc, subs, insts, eps, stack, coop, rays, res, i, i < n);
+        trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop, rays, res, i, i < n);
     }
 }
 
@@ -1051,10 +1059,15 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
     // dynamic LDS: scene tables (the LDS-table variants) + batch prefix (dynamic batches) + stacks
     const size_t lds = (tables_fit_lds(sc) ? tables_lds_bytes(sc) : 0u) +
                        (w.dyn ? 4u * (size_t)((w.seg_count + 4u) & ~3u) : 0u) + stack_lds_bytes(depth);
+    static const uint32_t flat_min = (uint32_t)ab_knob("FLAT_MIN_INST", (int)kFlatMinInstances);  // A/B
+    const bool flat = PTX_FLAT_INST && sc.n_inst >= flat_min;
     if (occ_only && tables_fit_lds(sc)) {  // occlusion rounds (GI spatial)
         if (sc.counters)
             hipLaunchKernelGGL((trace_queue<true, 6, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
                                (uint32_t)round, eps);
+        else if (flat)
+            hipLaunchKernelGGL((trace_queue<false, TRACE_OCC_WAVES, false, true, true, true>), dim3(trace_grid(w)), dim3(WB), lds,
+                               s, sc, w, (uint32_t)round, eps);
         else
             hipLaunchKernelGGL((trace_queue<false, TRACE_OCC_WAVES, false, true, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
                                (uint32_t)round, eps);
@@ -1090,7 +1103,9 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
         const bool tables_fit = tables_fit_lds(sc) && !no_lds;
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
                  : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
-                 : occ == 6  ? trace_queue<false, 6> : occ == 5 ? trace_queue<false, 5> : trace_queue<false, 4>;
+                 : occ == 6  ? trace_queue<false, 6>
+                 : occ == 5  ? (flat ? trace_queue<false, 5, false, true, false, true> : trace_queue<false, 5>)
+                             : (flat ? trace_queue<false, 4, false, true, false, true> : trace_queue<false, 4>);
         hipLaunchKernelGGL(k, dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     }
     return hipGetLastError();
