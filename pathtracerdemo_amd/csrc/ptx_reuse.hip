@@ -23,12 +23,23 @@ constexpr uint32_t SALT_TEMPORAL = 0x54454D50u, SALT_SPATIAL = 0x53504154u;
 
 // Job state, SoA float4 slots (slot k of job j at jstate[k * njobs + j]):
 // HDR {i | length << 8 | phase << 16, rSeed[1], ray idx, sample ref}; F {f, prod | q};
-// CUR {pos, inst << 16 | mat}; NRM {nrm, beta}; PREV {prev pos, rr_p}; RRF {rr_f, -}
+// CUR {pos, inst << 16 | mat}; NRM {nrm, beta}; PREV {prev pos, rr_p}; RRF {rr_f, -}.
+// A FRESH job (its first regenerated ray just emitted from the domain's primary hit: i == 1,
+// phase 0 -- most jobs of a start kernel) stores 48 B instead of 96: HDR {.. | 1 << 24, domain
+// pixel, ray idx, ref}, F {rr_f, prod}, RRF {beta, rr_p, -, -}.  Everything else is a copy of
+// data the next step can gather with the same bits: f = (1, 1, 1), the current vertex = the
+// domain's surface record, the previous one = its camera point (x0_of), rSeed[1] = word 1 of
+// the sample's reservoir.
 enum : uint32_t { JS_HDR, JS_F, JS_CUR, JS_NRM, JS_PREV, JS_RRF, JS_COUNT };
+constexpr uint32_t kJobFresh = 1u << 24;
+#ifndef PTX_JOB_FRESH
+#define PTX_JOB_FRESH 1  // (A/B: 0 stores every job in the full 96-byte layout)
+#endif
 
 struct Job {
     uint32_t i, length, phase, seed1, idx, matref;
     int32_t ref;  // reservoir index of the sample (band-relative; halo rows are < 0 or >= npix)
+    int32_t dom;  // band index of the domain pixel (its camera point and primary hit)
     f3 f;
     float prod;   // pdf product of the regenerated directions; q once the light ray is out
     Surface cur;
@@ -43,6 +54,13 @@ __device__ __forceinline__ const uint4 *res_at(const uint4 *base, int32_t idx) {
 __device__ __forceinline__ void job_store(const ReuseArgs &A, uint32_t jid, const Job &s) {
     const size_t n = A.njobs;
     float4 *st = A.jstate;
+    if (PTX_JOB_FRESH && s.i == 1u && s.phase == 0u) {  // fresh: 48 B (see above)
+        st[JS_HDR * n + jid] = make_float4(asf(1u | (s.length << 8) | kJobFresh), asf((uint32_t)s.dom), asf(s.idx),
+                                           asf((uint32_t)s.ref));
+        st[JS_F * n + jid] = make_float4(s.rr_f.x, s.rr_f.y, s.rr_f.z, s.prod);
+        st[JS_RRF * n + jid] = make_float4(s.beta, s.rr_p, 0.0f, 0.0f);
+        return;
+    }
     st[JS_HDR * n + jid] = make_float4(asf(s.i | (s.length << 8) | (s.phase << 16)), asf(s.seed1), asf(s.idx),
                                        asf((uint32_t)s.ref));
     st[JS_F * n + jid] = make_float4(s.f.x, s.f.y, s.f.z, s.prod);
@@ -57,8 +75,21 @@ __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, ui
     const float4 *st = A.jstate;
     const float4 hd = st[JS_HDR * n + jid], fv = st[JS_F * n + jid];
     const uint32_t hw = asu(hd.x);
-    s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = hw >> 16;
-    s.seed1 = asu(hd.y); s.idx = asu(hd.z); s.ref = (int32_t)asu(hd.w);
+    s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = (hw >> 16) & 0xffu;
+    s.idx = asu(hd.z); s.ref = (int32_t)asu(hd.w);
+    if (hw & kJobFresh) {  // the fresh layout: gather what it leaves out (same bits)
+        const float4 rf = st[JS_RRF * n + jid];
+        s.dom = (int32_t)asu(hd.y);
+        s.seed1 = res_at(A.cur, s.ref)[0].y;
+        s.f = mk(1.0f, 1.0f, 1.0f); s.prod = fv.w;
+        s.rr_f = mk(fv.x, fv.y, fv.z);
+        s.beta = rf.x; s.rr_p = rf.y;
+        (void)surf_load(sc, A.surf, s.dom, s.cur, s.matref);  // (a job exists only where it is valid)
+        const int32_t W = (int32_t)sc.width, q = s.dom >= 0 ? s.dom / W : -((-s.dom + W - 1) / W);
+        s.prev = x0_of(sc, (uint32_t)(s.dom - q * W), (uint32_t)((int32_t)sc.row_begin + q));
+        return;
+    }
+    s.seed1 = asu(hd.y);
     s.f = mk(fv.x, fv.y, fv.z); s.prod = fv.w;
     if (s.phase != 0u) return;
     const float4 cu = st[JS_CUR * n + jid], nr = st[JS_NRM * n + jid];
@@ -87,8 +118,8 @@ __device__ __forceinline__ bool rr_step(Job &s, const Surface &X, f3 L, f3 fv, f
 // A fresh job: sample `ref` (length >= 2) replayed from the domain's camera point x0 and
 // primary-hit surface X1 (flat material index matref).
 __device__ __forceinline__ void job_init(Job &s, f3 x0, const Surface &X1, uint32_t matref, int32_t ref,
-                                         uint32_t length, uint32_t seed1) {
-    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = seed1; s.idx = 0u; s.ref = ref;
+                                         uint32_t length, uint32_t seed1, int32_t dom) {
+    s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = seed1; s.idx = 0u; s.ref = ref; s.dom = dom;
     s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
     s.prev = x0;
     s.cur = X1;
@@ -104,7 +135,7 @@ __device__ __forceinline__ bool job_begin(const Scene &sc, const ReuseArgs &A, J
     Surface X1;
     uint32_t matref;
     if (C == 0u || length < 2u || !surf_load(sc, A.surf, dom, X1, matref)) return false;
-    job_init(s, x0_of(sc, x, y), X1, matref, ref, length, rv[0].y);
+    job_init(s, x0_of(sc, x, y), X1, matref, ref, length, rv[0].y, dom);
     return true;
 }
 
@@ -516,7 +547,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                                                      : nbr_at(A, ni);
                     want = nb.valid && nb.length >= 2u && nb.p > 0.0f;
                     act = want && nb.C != 0u;
-                    if (act) { job_init(s, x0, X1, mref, ni, nb.length, b.y); s0 = b.x; }
+                    if (act) { job_init(s, x0, X1, mref, ni, nb.length, b.y, (int32_t)pix); s0 = b.x; }
                 } else if (present && canon) {  // this pixel's sample in the neighbour's domain
                     want = act = a.w != kNoSurface;
                     if (act) {
@@ -524,7 +555,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                         Xn.pos = mk(asf(a.x), asf(a.y), asf(a.z));
                         Xn.nrm = mk(asf(b.x), asf(b.y), asf(b.z));
                         Xn.mat = material_at(sc, a.w);
-                        job_init(s, x0_of(sc, nx, ny), Xn, a.w, (int32_t)pix, clen, c0.y);
+                        job_init(s, x0_of(sc, nx, ny), Xn, a.w, (int32_t)pix, clen, c0.y, ni);
                         s0 = c0.x;
                     }
                 }

@@ -18,7 +18,8 @@ for WL in ${WORKLOADS:-reuse restir mcpt gi}; do
   cp "$src/bench_trace.log" "$dst/bench_under_rocprof.log"
   tail -n 1 "gpurun_out/bench_${ROUND}_$WL.log" > "$dst/bench_line.json"
   # the timed roofline symbol only (GI: the closest-hit instance, not the any-hit one)
-  KN="trace_queue<false, 4, false, true, false>"
+  # (the closest-hit instance; prefix: the flattened variant adds ", true" -- scenes of >= 3 instances)
+  KN="trace_queue<false, 4, false, true, false"
   python3 tools/hbm_traffic.py "$dst" "$WL:${SCENE[$WL]}:trace_queue:1920x1080" "$KN" > /dev/null
   # the bench line carries the PMC traffic of THIS build's passes (the bench ran first and
   # looked up the previous entry)
