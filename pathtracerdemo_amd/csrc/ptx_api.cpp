@@ -373,6 +373,16 @@ void resolve_event(TimedLaunch &t, ptx_handle *h) {
     t.pending = false;
 }
 
+// Padded pixels per wavefront segment.  Measured round 3 (same box, 1080p, flattened instance
+// loop + fresh shift jobs): the reuse pipeline +1.5 % at 1024 (768: 378.1, 1024: 383.7, 1536:
+// 372.0, 2048: 369.3 Msamples/s; 4K ±0); GI -2.5 %, TEST_MCPT -4.4 %, ReSTIR -1.7 % at 1024, so
+// they keep kWaveSegPixels.  PTX_AB=SEG_PX=n: A/B.
+static uint32_t seg_pixels(const ptx_handle *h) {
+    static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);
+    if (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) return env_px;
+    return h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? 1024u : kWaveSegPixels;
+}
+
 // Wavefront buffers, sized for the largest round: PT_1 emits <= 2 rays per pixel, PT_4
 // <= 1, TEST_MCPT <= LightCount + 1 (all shadow rays of a vertex + the next path ray).
 int wave_buffers(ptx_handle *h, WaveBufs &w) {
@@ -381,8 +391,7 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t jpp = has_reuse(h) ? 2u * h->reuse_neighbors : 1u;
     const size_t per_px = std::max<size_t>(std::max<size_t>(2u, (size_t)nl + 1u), jpp);
     const size_t padded = (size_t)((h->cfg.width + 7u) / 8u) * ((h->band_h + 7u) / 8u) * 64u;
-    static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);  // A/B
-    const uint32_t seg_px = (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) ? env_px : kWaveSegPixels;
+    const uint32_t seg_px = seg_pixels(h);
     const size_t nseg = (padded + seg_px - 1u) / seg_px;
     // queue slots: the whole band, or two tile sets in flight at once (interior + edge rows of
     // a band's spatial pass: ceil(a/s) + ceil(b/s) <= ceil((a+b)/s) + 1)
@@ -1290,9 +1299,7 @@ int ptx_row_census(ptx_handle *h, uint64_t *out, size_t n_tile_rows) {
         for (int k = 0; k < 5; ++k) out[5u * r + k] += c[(size_t)kCensusWords * r + k];
     // queue slot s traced the rays of segment s: tiles [s*m, s*m + m) in raster order
     // (m = seg_px / 64); a slot spanning two tile rows is split by its tiles in each
-    static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);
-    const uint32_t seg_px = (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) ? env_px : kWaveSegPixels;
-    const uint32_t m = seg_px / 64u, ntiles = tile_rows * tiles_x;
+    const uint32_t m = seg_pixels(h) / 64u, ntiles = tile_rows * tiles_x;
     for (uint32_t s = 0; tile_rows + s < h->census_blocks && (size_t)s * m < ntiles; ++s) {
         const unsigned long long *b = c.data() + (size_t)kCensusWords * (tile_rows + s);
         const uint32_t t0 = s * m, t1 = std::min(ntiles, t0 + m), r0 = t0 / tiles_x, r1 = (t1 - 1u) / tiles_x;
