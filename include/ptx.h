@@ -201,6 +201,15 @@ int ptx_write_buffer(ptx_handle *h, int which, const void *host_src, size_t byte
  * for PTX_BUF_GBUFFER / PTX_BUF_RESERVOIR is valid until the next ptx_render.  Accumulation,
  * history and counters never move. */
 int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes);
+/* The reference's render pass (Renderer_TEST.Render, GC/Renderer_TEST.ts:233-255: a fullscreen
+ * quad, SH/VertexShader.wgsl + SH/FragmentShader.wgsl:7-10) onto a canvas_w x canvas_h canvas:
+ * canvas pixel (x, y), y = 0 the top row, shows texel (floor((2x+1)*600 / 2canvas_w),
+ * floor((2canvas_h-2y-1)*450 / 2canvas_h)) of the accumulated image -- the shader's fixed
+ * 600 x 450 window, flipped to screen order -- as unorm8 rgb (clamp, round to nearest even) with
+ * alpha 255; a texel outside the image reads 0.  out: canvas_w * canvas_h * 4 bytes, RGBA
+ * (bgra = 0, a 2D canvas's ImageData) or BGRA (bgra = 1, a bgra8unorm WebGPU canvas); blocking.
+ * Whole-image handles (a split frame is presented from its gathered rows by the host). */
+int ptx_present(ptx_handle *h, uint32_t canvas_w, uint32_t canvas_h, int bgra, uint8_t *out);
 /* Closest-hit queries (TraceRay, SH/PT_1_InitPass.wgsl:605-715) for arbitrary rays.
  * rays: n x {o.x,o.y,o.z,d.x, d.y,d.z,-,-} f32 (32 B); hits: n x {t, flags|inst|mat (u32 bits),
  * prim (u32 bits), bary.x, bary.y, pos.x, pos.y, pos.z} (32 B; flags bit31 = valid).

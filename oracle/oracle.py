@@ -231,6 +231,31 @@ class Frame:
         return bool(out[0]), out[1:4].copy(), float(out[4])
 
 
+def present(img: np.ndarray, canvas_w: int, canvas_h: int, bgra: bool = False) -> np.ndarray:
+    """Renderer_TEST.Render's render pass (GC/Renderer_TEST.ts:233-255): the fullscreen quad of
+    VertexShader.wgsl (PixelUV = (NDC + 1) / 2) and FragmentShader.wgsl:7-10 (texel
+    (floor(PixelUV.x * 600), floor(PixelUV.y * 450)) of the Scene texture, rgb, alpha 1) onto a
+    unorm8 canvas; canvas row 0 is the top (NDC y = +1).  `img`: the (H, W, 4) f32 texture, row 0 =
+    image row 0.  Exact integer texel arithmetic; out-of-bounds texels read 0; unorm8 = clamp to
+    [0, 1], x * 255 rounded half to even, NaN -> 0 (test restatement of ptx_present)."""
+    H, W = img.shape[:2]
+    px = np.arange(canvas_w, dtype=np.int64)
+    py = np.arange(canvas_h, dtype=np.int64)
+    tx = ((2 * px + 1) * 600) // (2 * canvas_w)
+    ty = ((2 * canvas_h - 2 * py - 1) * 450) // (2 * canvas_h)
+    out = np.zeros((canvas_h, canvas_w, 4), np.uint8)
+    ok = (ty[:, None] < H) & (tx[None, :] < W)
+    rgb = np.zeros((canvas_h, canvas_w, 3), np.float32)
+    yy, xx = np.broadcast_arrays(ty[:, None], tx[None, :])
+    rgb[ok] = img[yy[ok], xx[ok], :3]
+    c = np.nan_to_num(rgb, nan=0.0)
+    c = np.clip(c, np.float32(0.0), np.float32(1.0))
+    q = np.rint(c * np.float32(255.0)).astype(np.uint8)
+    out[..., :3] = q[..., ::-1] if bgra else q
+    out[..., 3] = 255
+    return out
+
+
 def pcg(seed: int) -> int:
     return int(lib().pto_pcg(seed & 0xFFFFFFFF))
 

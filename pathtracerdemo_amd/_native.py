@@ -40,7 +40,7 @@ EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame"
             "ptx_write_buffer", "ptx_device_pointer", "ptx_set_stream", "ptx_destroy", "ptx_last_error",
             "ptx_trace", "ptx_trace_device", "ptx_run_passes", "ptx_halo_rows", "ptx_halo_pack",
             "ptx_halo_unpack", "ptx_comm_unique_id", "ptx_comm_init", "ptx_comm_init_all", "ptx_render_bands",
-            "ptx_row_census", "ptx_comm_info"]
+            "ptx_row_census", "ptx_comm_info", "ptx_present"]
 
 
 class PtxConfig(ctypes.Structure):
@@ -108,6 +108,7 @@ def load(path: str = LIB_PATH):
     lib.ptx_set_stream.argtypes = [H, P]
     lib.ptx_trace.argtypes = [H, P, P, ctypes.c_size_t, ctypes.c_int]
     lib.ptx_trace_device.argtypes = [H, P, P, ctypes.c_size_t, ctypes.c_int]
+    lib.ptx_present.argtypes = [H, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P]
     lib.ptx_run_passes.argtypes = [H, P, ctypes.c_int]
     lib.ptx_halo_rows.argtypes = [H, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                   ctypes.POINTER(ctypes.c_size_t)]

@@ -68,6 +68,29 @@ static hipError_t copy_sync(ptx_handle *h, void *dst, const void *src, size_t by
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     return e;
 }
+// Device -> caller memory after everything enqueued on h->stream, through the handle's pinned
+// staging buffer in chunks of up to 8 MB: the caller's memory may be any host memory, and
+// pageable device-to-host async copies into a V8 ArrayBuffer (the Node host) came back
+// incomplete for multi-MB transfers; a pinned destination is a plain DMA.
+int read_to_host(ptx_handle *h, void *dst, const void *src, size_t bytes) {
+    constexpr size_t kChunk = (size_t)8 << 20;
+    const size_t want = std::min(bytes, kChunk);
+    if (want > h->host_stage_bytes) {
+        if (h->host_stage) (void)hipHostFree(h->host_stage);
+        h->host_stage = nullptr;
+        h->host_stage_bytes = 0;
+        HIP_CHECK(h, hipHostMalloc(&h->host_stage, want, hipHostMallocDefault));
+        h->host_stage_bytes = want;
+    }
+    for (size_t off = 0; off < bytes; off += kChunk) {
+        const size_t n = std::min(kChunk, bytes - off);
+        HIP_CHECK(h, hipMemcpyAsync(h->host_stage, (const char *)src + off, n, hipMemcpyDeviceToHost, h->stream));
+        HIP_CHECK(h, hipStreamSynchronize(h->stream));
+        std::memcpy((char *)dst + off, h->host_stage, n);
+    }
+    return PTX_OK;
+}
+
 int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
     if (b.bytes == bytes && b.p) return PTX_OK;
     free_buf(b);
@@ -1196,17 +1219,13 @@ int ptx_render(ptx_handle *h, float *rgba_out) {
                 if ((rc = timed_launch(h, p))) return rc;
     } else if (has_reuse(h) && h->comm) {  // a band of a multi-GPU frame: halo over RCCL
         if (int rc = render_band_nccl(h)) return rc;
-        if (rgba_out) {
-            HIP_CHECK(h, hipMemcpyAsync(rgba_out, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost, h->stream));
-            HIP_CHECK(h, hipStreamSynchronize(h->stream));
-        }
+        if (rgba_out)
+            if (int rc = read_to_host(h, rgba_out, h->d_accum.p, h->d_accum.bytes)) return rc;
         return PTX_OK;
     } else if (has_reuse(h) && (h->halo_top || h->halo_bot) && (h->cfg.flags & PTX_FLAG_HALO_SKIP)) {
         if (int rc = render_band_solo(h)) return rc;  // (counts its frame)
-        if (rgba_out) {
-            HIP_CHECK(h, hipMemcpyAsync(rgba_out, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost, h->stream));
-            HIP_CHECK(h, hipStreamSynchronize(h->stream));
-        }
+        if (rgba_out)
+            if (int rc = read_to_host(h, rgba_out, h->d_accum.p, h->d_accum.bytes)) return rc;
         return PTX_OK;
     } else if (has_reuse(h)) {
         if (h->halo_top || h->halo_bot)
@@ -1221,10 +1240,8 @@ int ptx_render(ptx_handle *h, float *rgba_out) {
         if (int rc = timed_launch(h, PTX_PASS_MCPT)) return rc;
     }
     h->frames++;
-    if (rgba_out) {
-        HIP_CHECK(h, hipMemcpyAsync(rgba_out, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost, h->stream));
-        HIP_CHECK(h, hipStreamSynchronize(h->stream));
-    }
+    if (rgba_out)
+        if (int rc = read_to_host(h, rgba_out, h->d_accum.p, h->d_accum.bytes)) return rc;
     return PTX_OK;
 }
 
@@ -1321,7 +1338,7 @@ int ptx_read_buffer(ptx_handle *h, int which, void *host_dst, size_t bytes) {
     DevBuf b;
     if (!buffer_view(h, which, b) || bytes > b.bytes)
         return fail(h, PTX_E_INVALID, "read of %zu bytes from buffer %d", bytes, which);
-    HIP_CHECK(h, copy_sync(h, host_dst, b.p, bytes, hipMemcpyDeviceToHost));
+    if (int rc = read_to_host(h, host_dst, b.p, bytes)) return rc;
     return PTX_OK;
 }
 
@@ -1344,6 +1361,23 @@ int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes) 
     *dev_ptr = b.p;
     if (bytes) *bytes = b.bytes;
     return PTX_OK;
+}
+
+int ptx_present(ptx_handle *h, uint32_t canvas_w, uint32_t canvas_h, int bgra, uint8_t *out) {
+    if (!h || !out) return PTX_E_INVALID;
+    if (canvas_w == 0 || canvas_h == 0 || (uint64_t)canvas_w * canvas_h > (1ull << 28))
+        return fail(h, PTX_E_INVALID, "ptx_present: canvas %ux%u", canvas_w, canvas_h);
+    if (h->cfg.row_begin != 0 || h->band_h != h->cfg.height)
+        return fail(h, PTX_E_INVALID, "ptx_present: a band handle (rows %u..%u) holds part of the texture: present the "
+                                      "gathered frame on the host", h->cfg.row_begin, h->cfg.row_end);
+    if (!h->d_accum.p) return fail(h, PTX_E_INVALID, "ptx_present: nothing rendered");
+    HIP_CHECK(h, hipSetDevice(h->device));
+    const size_t bytes = (size_t)canvas_w * canvas_h * 4u;
+    if (int rc = alloc_buf(h, h->d_canvas, bytes)) return rc;
+    const hipError_t e = launch_present((const float4 *)h->d_accum.p, h->cfg.width, h->cfg.height, canvas_w, canvas_h,
+                                        bgra != 0, (uint32_t *)h->d_canvas.p, h->stream);
+    if (e != hipSuccess) return fail(h, PTX_E_HIP, "ptx_present: %s", hipGetErrorString(e));
+    return read_to_host(h, out, h->d_canvas.p, bytes);
 }
 
 int ptx_trace_device(ptx_handle *h, const void *rays_dev, void *hits_dev, size_t n, int eps_mode) {
@@ -1377,9 +1411,7 @@ int ptx_trace(ptx_handle *h, const float *rays, float *hits, size_t n, int eps_m
     if (int rc = alloc_buf(h, h->d_qhits, std::max(h->d_qhits.bytes, n * 32u))) return rc;
     HIP_CHECK(h, hipMemcpyAsync(h->d_qrays.p, rays, n * 32u, hipMemcpyHostToDevice, h->stream));
     if (int rc = ptx_trace_device(h, h->d_qrays.p, h->d_qhits.p, n, eps_mode)) return rc;
-    HIP_CHECK(h, hipMemcpyAsync(hits, h->d_qhits.p, n * 32u, hipMemcpyDeviceToHost, h->stream));
-    HIP_CHECK(h, hipStreamSynchronize(h->stream));
-    return PTX_OK;
+    return read_to_host(h, hits, h->d_qhits.p, n * 32u);
 }
 
 int ptx_set_stream(ptx_handle *h, void *hip_stream) {
@@ -1406,7 +1438,8 @@ int ptx_destroy(ptx_handle *h) {
         if (t.start) (void)hipEventDestroy(t.start);
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
-    for (DevBuf *b : {&h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
+    if (h->host_stage) (void)hipHostFree(h->host_stage);
+    for (DevBuf *b : {&h->d_canvas, &h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
                       &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_surf, &h->d_direct, &h->d_census})

@@ -522,11 +522,9 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
         for (int i = 0; i < n; ++i) {
             ptx_handle *h = hs[i];
             HIP_CHECK(hs[i], hipSetDevice(h->device));
-            HIP_CHECK(h, hipMemcpyAsync((char *)rgba_out + off, h->d_accum.p, h->d_accum.bytes, hipMemcpyDeviceToHost,
-                                        h->stream));
+            if (int rc = read_to_host(h, (char *)rgba_out + off, h->d_accum.p, h->d_accum.bytes)) return rc;
             off += h->d_accum.bytes;
         }
-        for (int i = 0; i < n; ++i) HIP_CHECK(hs[i], hipStreamSynchronize(hs[i]->stream));
     }
     return PTX_OK;
 }

@@ -110,6 +110,10 @@ struct ptx_handle {
     hipStream_t xstream = nullptr;
     hipEvent_t ev_front = nullptr, ev_halo = nullptr;
     uint64_t halo_bytes_sent = 0;  // halo bytes this handle's communicator has sent (ptx_comm_info)
+    // ptx_present's canvas on the device; the pinned staging buffer of read_to_host
+    DevBuf d_canvas;
+    void *host_stage = nullptr;
+    size_t host_stage_bytes = 0;
     // stats
     TimedLaunch ring[kEventRing];
     int ring_pos = 0;
@@ -128,6 +132,8 @@ int fail(ptx_handle *h, int code, const char *fmt, ...);
     } while (0)
 void free_buf(DevBuf &b);
 int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes);
+// device -> caller memory after the work enqueued on h->stream (pinned staging, blocking)
+int read_to_host(ptx_handle *h, void *dst, const void *src, size_t bytes);
 // first band row of the halo-extended G-buffer / reservoir allocations
 uint4 *gbuf_band(ptx_handle *h);
 uint4 *res_band(ptx_handle *h);

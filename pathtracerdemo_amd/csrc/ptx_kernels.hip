@@ -392,4 +392,41 @@ hipError_t launch_trace_rays(const Scene &sc, const float4 *rays, float4 *hits, 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- present (the reference's render pass)
+// Renderer_TEST.Render's render pass (GC/Renderer_TEST.ts:233-255) draws a fullscreen quad
+// (SH/VertexShader.wgsl: PixelUV = (NDC + 1) / 2) whose fragment shader loads texel
+// (floor(PixelUV.x * 600), floor(PixelUV.y * 450)) of the Scene texture -- a fixed 600 x 450
+// window whatever the canvas size (SH/FragmentShader.wgsl:7-10) -- and writes rgb with alpha 1
+// to the canvas (its preferred format, unorm8).  Canvas pixel (px, py), py = 0 the top row, is
+// the fragment at NDC y = 1 - (2 py + 1) / ch, so PixelUV = ((2 px + 1) / 2cw, 1 - (2 py + 1) / 2ch):
+// the texel is floor((2 px + 1) * 600 / 2cw), floor((2 ch - 2 py - 1) * 450 / 2ch) in exact
+// integer arithmetic (the rasterizer's own rounding of PixelUV is implementation-defined, and
+// matters only where the product is an exact integer).  A texel outside the texture reads as
+// 0 (WGSL leaves out-of-bounds textureLoad implementation-defined).  unorm8: clamp to [0, 1],
+// x * 255 rounded to nearest even (NaN -> 0).  bgra: the byte order of a bgra8unorm canvas.
+__device__ __forceinline__ uint32_t unorm8(float x) {
+    const float c = fminf(fmaxf(x, 0.0f), 1.0f);  // (NaN -> 0: maxNum)
+    return (uint32_t)__builtin_rintf(c * 255.0f);
+}
+__global__ __launch_bounds__(BLOCK) void present_kernel(const float4 *tex, uint32_t W, uint32_t H, uint32_t cw,
+                                                        uint32_t ch, uint32_t bgra, uint32_t *out) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= cw * ch) return;
+    const uint32_t px = i % cw, py = i / cw;
+    const uint64_t tx = ((uint64_t)(2u * px + 1u) * 600u) / (2ull * cw);
+    const uint64_t ty = ((uint64_t)(2u * ch - 2u * py - 1u) * 450u) / (2ull * ch);
+    float4 c = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+    if (tx < W && ty < H) c = tex[ty * W + tx];
+    const uint32_t r = unorm8(c.x), g = unorm8(c.y), b = unorm8(c.z);
+    out[i] = bgra ? (b | (g << 8) | (r << 16) | (255u << 24)) : (r | (g << 8) | (b << 16) | (255u << 24));
+}
+hipError_t launch_present(const float4 *tex, uint32_t W, uint32_t H, uint32_t cw, uint32_t ch, bool bgra,
+                          uint32_t *out, hipStream_t s) {
+    const uint32_t n = cw * ch;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(present_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, tex, W, H, cw, ch,
+                       bgra ? 1u : 0u, out);
+    return hipGetLastError();
+}
+
 }  // namespace ptx

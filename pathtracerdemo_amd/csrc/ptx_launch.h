@@ -24,6 +24,9 @@ hipError_t launch_init(const Scene &sc, const uint4 *gbuf, uint4 *reservoir, uin
 hipError_t launch_final(const Scene &sc, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
                         uint32_t stack_depth, hipStream_t s);
 hipError_t launch_mcpt(const Scene &sc, float4 *accum, uint32_t stack_depth, hipStream_t s);
+// the reference's render pass: the Scene texture's fixed 600 x 450 window onto a cw x ch unorm8 canvas
+hipError_t launch_present(const float4 *tex, uint32_t W, uint32_t H, uint32_t cw, uint32_t ch, bool bgra,
+                          uint32_t *out, hipStream_t s);
 
 // closest-hit queries for a ray array (ptx_kernels.hip)
 hipError_t launch_trace_rays(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,

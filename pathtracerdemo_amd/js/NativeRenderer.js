@@ -6,8 +6,11 @@
  * Same surface: constructor, async Initialize(world), Update(), Render(), GetCamera(),
  * ResetFrameCount(); WebGPUEngine's loop (GC/service/WebGPUEngine.ts:199-200) calls
  * Update() then Render() per tick exactly as before.  Instead of a canvas it renders into
- * the accumulated RGBA f32 image (ReadImage / RenderAsync(out)); presenting it is the
- * caller's (putImageData), the WebGPU present pass being out of scope (SURVEY.md §8b).
+ * the accumulated RGBA f32 image (ReadImage / RenderAsync(out)); Present(canvasW, canvasH)
+ * runs the reference's render pass on the GPU (the fullscreen quad + FragmentShader.wgsl's fixed
+ * 600 x 450 texel window, unorm8) into bytes a canvas takes as they are: RGBA for a 2D canvas's
+ * putImageData, BGRA for a bgra8unorm WebGPU canvas.  presentImage does the same on the host for
+ * a frame gathered from row bands (renderBands).
  *
  * `world` is the reference's own World (./world.js: World.LoadFromScene over the Scene JSON,
  * meshes in ResourceManager.MeshPool), serialized here by SerializeWorldData exactly as
@@ -120,6 +123,17 @@ class NativeRenderer {
     return img;
   }
 
+  /**
+   * Renderer_TEST.Render's render pass (Renderer_TEST.ts:233-255) onto a canvasW x canvasH canvas
+   * (default: the image size): Uint8ClampedArray of canvasW * canvasH * 4 bytes, RGBA (bgra false:
+   * ImageData for putImageData) or BGRA (bgra true); row 0 = the canvas's top row.
+   */
+  Present(canvasW = this.Width, canvasH = this.Height, bgra = false, out = null) {
+    const px = out || new Uint8ClampedArray(canvasW * canvasH * 4);
+    addon.present(this.Handle, canvasW, canvasH, bgra, px);
+    return px;
+  }
+
   RunPass(pass) { addon.runPass(this.Handle, pass); }
   Synchronize() { addon.synchronize(this.Handle); }
   GetStats() { return addon.getStats(this.Handle); }
@@ -132,4 +146,37 @@ class NativeRenderer {
   }
 }
 
-module.exports = { NativeRenderer, buildUniform, addon, PASS, BUF, FLAGS, UNIFORM_WORDS };
+/**
+ * The same render pass on the host, for a frame gathered from row bands (Renderer.renderBands'
+ * image, rows 0 .. height): canvas pixel (x, y) shows texel (floor((2x+1)*600 / 2canvasW),
+ * floor((2canvasH-2y-1)*450 / 2canvasH)) -- FragmentShader.wgsl:7-10's PixelUV * (600, 450) of the
+ * quad's VertexShader.wgsl UV at the pixel centre, in exact integers -- clamped to [0, 1] and
+ * rounded half to even to unorm8 (ptx_present's rules; out-of-bounds texels read 0).
+ */
+function presentImage(img, width, height, canvasW, canvasH, bgra = false, out = null) {
+  const px = out || new Uint8ClampedArray(canvasW * canvasH * 4);
+  const f = new Float32Array(1);
+  const unorm8 = (x) => {
+    if (!(x > 0)) return 0; // (NaN, <= 0)
+    if (x >= 1) return 255;
+    f[0] = Math.fround(x * 255); // the f32 product, then round half to even
+    const v = f[0], fl = Math.floor(v), d = v - fl;
+    return d > 0.5 || (d === 0.5 && (fl % 2) === 1) ? fl + 1 : fl;
+  };
+  for (let y = 0; y < canvasH; y++) {
+    const ty = Math.floor(((2 * canvasH - 2 * y - 1) * 450) / (2 * canvasH));
+    for (let x = 0; x < canvasW; x++) {
+      const tx = Math.floor(((2 * x + 1) * 600) / (2 * canvasW));
+      const o = 4 * (y * canvasW + x);
+      let r = 0, g = 0, b = 0;
+      if (tx < width && ty < height) {
+        const i = 4 * (ty * width + tx);
+        r = unorm8(img[i]); g = unorm8(img[i + 1]); b = unorm8(img[i + 2]);
+      }
+      px[o] = bgra ? b : r; px[o + 1] = g; px[o + 2] = bgra ? r : b; px[o + 3] = 255;
+    }
+  }
+  return px;
+}
+
+module.exports = { NativeRenderer, buildUniform, presentImage, addon, PASS, BUF, FLAGS, UNIFORM_WORDS };

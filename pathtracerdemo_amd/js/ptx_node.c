@@ -632,6 +632,39 @@ static napi_value js_last_error(napi_env env, napi_callback_info info) {
     return s;
 }
 
+/* present(handle, canvasW, canvasH, bgra, out: Uint8Array | Uint8ClampedArray of canvasW * canvasH * 4):
+ * the reference's render pass onto the canvas (ptx_present, include/ptx.h) */
+static napi_value js_present(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    if (argc < 5) {
+        napi_throw_type_error(env, NULL, "present(handle, canvasW, canvasH, bgra, out)");
+        return NULL;
+    }
+    uint32_t cw = 0, ch = 0;
+    bool bgra = false;
+    CHECK_NAPI(env, napi_get_value_uint32(env, argv[1], &cw));
+    CHECK_NAPI(env, napi_get_value_uint32(env, argv[2], &ch));
+    CHECK_NAPI(env, napi_get_value_bool(env, argv[3], &bgra));
+    void *p;
+    size_t n, es;
+    napi_typedarray_type t;
+    if (typed_view(env, argv[4], &p, &n, &es, &t) || (t != napi_uint8_array && t != napi_uint8_clamped_array)) {
+        napi_throw_type_error(env, NULL, "out must be a Uint8Array or Uint8ClampedArray");
+        return NULL;
+    }
+    if (n < (size_t)cw * ch * 4u) {
+        napi_throw_range_error(env, NULL, "out holds fewer than canvasW * canvasH * 4 bytes");
+        return NULL;
+    }
+    int rc = ptx_present(H->h, cw, ch, bgra ? 1 : 0, (uint8_t *)p);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_present");
+    return NULL;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     static const struct {
         const char *name;
@@ -648,6 +681,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"renderBands", js_render_bands},   {"renderBandsAsync", js_render_bands_async},
         {"commUniqueId", js_comm_unique_id}, {"commInit", js_comm_init},
         {"commInitAll", js_comm_init_all},  {"rowCensus", js_row_census},
+        {"present", js_present},
     };
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
         napi_value f;

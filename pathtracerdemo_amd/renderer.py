@@ -214,6 +214,15 @@ class Renderer:
                 "kernel_launches": list(s.kernel_launches), "triangles": s.triangles, "bvh_nodes": s.bvh_nodes,
                 "instances": s.instances, "max_bvh_depth": s.max_bvh_depth, "device_bytes": s.device_bytes}
 
+    def Present(self, canvas_w: int | None = None, canvas_h: int | None = None, bgra: bool = False) -> np.ndarray:
+        """The reference's render pass (Renderer_TEST.Render's fullscreen quad + FragmentShader.wgsl)
+        onto a canvas_w x canvas_h canvas (default: the image size): (canvas_h, canvas_w, 4) uint8,
+        RGBA (a 2D canvas's ImageData) or BGRA (a bgra8unorm WebGPU canvas); include/ptx.h ptx_present."""
+        cw, ch = int(canvas_w or self.width), int(canvas_h or self.height)
+        out = np.zeros((ch, cw, 4), np.uint8)
+        self._call("ptx_present", self._h, cw, ch, 1 if bgra else 0, out.ctypes.data)
+        return out
+
     def trace(self, rays: np.ndarray, eps_mode: int = 1) -> np.ndarray:
         """Closest hits for an (n, 8) f32 ray array {o.xyz, d.xyz, -, -}; returns (n, 8) f32
         {t, flags|inst|mat bits, prim bits, bary.x, bary.y, pos.xyz} (include/ptx.h)."""

@@ -1,0 +1,39 @@
+"""The reference's render pass on the GPU (ptx_present; Renderer_TEST.Render's fullscreen quad,
+GC/Renderer_TEST.ts:233-255, VertexShader.wgsl + FragmentShader.wgsl:7-10): the Scene texture's
+fixed 600 x 450 texel window onto a unorm8 canvas.  Byte-exact against oracle.present (the
+numpy restatement) on rendered frames of every pipeline, for canvases larger, equal to and
+smaller than the window, RGBA and BGRA; a band handle is refused (it holds part of the texture)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CANVASES = [(600, 450, False), (1920, 1080, True), (96, 64, False), (257, 131, True), (1, 1, False)]
+
+
+@pytest.mark.parametrize("pipeline,W,H", [("restir", 600, 450), ("reuse", 320, 200), ("mcpt", 640, 480), ("gi", 160, 96)])
+def test_present_bytes_match_the_render_pass(scene1, oracle_mod, pipeline, W, H):
+    from pathtracerdemo_amd.renderer import Renderer
+    r = Renderer(W, H, device=0, pipeline=pipeline)
+    r.Initialize(scene1)
+    for _ in range(2):
+        r.Update()
+        r.Render()
+    img = r.read_image()
+    for cw, ch, bgra in CANVASES:
+        got = r.Present(cw, ch, bgra=bgra)
+        np.testing.assert_array_equal(got, oracle_mod.present(img, cw, ch, bgra), f"{pipeline} {cw}x{ch} bgra={bgra}")
+    assert (r.Present()[..., 3] == 255).all()
+    r.close()
+
+
+def test_present_refuses_a_band(scene3):
+    from pathtracerdemo_amd import _native as native
+    from pathtracerdemo_amd.renderer import Renderer
+    r = Renderer(64, 48, device=0, pipeline="restir", row_begin=16, row_end=48)
+    r.Initialize(scene3)
+    r.Update()
+    r.Render()
+    with pytest.raises(native.PtxError):
+        r.Present(64, 48)
+    r.close()

@@ -24,7 +24,7 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 EXPORTS = ["abiVersion", "create", "uploadScene", "setFrame", "render", "renderAsync", "runPass", "runPasses",
            "resetAccumulation", "synchronize", "getStats", "resetStats", "readBuffer", "writeBuffer",
            "trace", "destroy", "lastError", "renderBands", "renderBandsAsync", "commUniqueId", "commInit",
-           "commInitAll", "rowCensus"]
+           "commInitAll", "rowCensus", "present"]
 
 
 @pytest.fixture(scope="module")
@@ -68,13 +68,36 @@ def test_js_uniform_matches_python_host(scene1, scene_dir):
         np.testing.assert_array_equal(np.array(g, dtype=np.uint64).astype(np.uint32), ref)
 
 
+CANVASES = [[600, 450, 0], [96, 64, 1], [1920, 1080, 0], [257, 131, 1]]
+
+
+def test_js_present_image_matches_the_render_pass_restatement(oracle_mod, tmp_path):
+    """presentImage (the reference's render pass on the host, for frames gathered from bands):
+    the 600 x 450 texel window of FragmentShader.wgsl through VertexShader.wgsl's quad onto
+    canvases of several sizes, unorm8 RGBA / BGRA -- equal byte for byte to oracle.present,
+    including out-of-range values (negative, > 1, NaN, inf) and texels outside a small image."""
+    rng = np.random.default_rng(3)
+    for W, H in ((640, 480), (300, 200)):
+        img = rng.uniform(-0.2, 1.2, size=(H, W, 4)).astype(np.float32)
+        img.reshape(-1)[rng.integers(0, img.size, 64)] = np.nan
+        img.reshape(-1)[rng.integers(0, img.size, 16)] = np.inf
+        img[::7, ::5, :3] = np.float32(0.5) / np.float32(255.0) + np.float32(0.0)  # near half-way cases
+        f = str(tmp_path / f"img{W}.f32")
+        img.tofile(f)
+        node("present_host.js", json.dumps({"img": f, "width": W, "height": H, "canvases": CANVASES, "out": f}))
+        for i, (cw, ch, bgra) in enumerate(CANVASES):
+            got = np.fromfile(f"{f}.{i}", dtype=np.uint8).reshape(ch, cw, 4)
+            np.testing.assert_array_equal(got, oracle_mod.present(img, cw, ch, bool(bgra)), f"{W}x{H} -> {cw}x{ch}")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("pipeline,frames", [("restir", 3), ("mcpt", 1), ("reuse", 3), ("gi", 3)])
 def test_native_renderer_frames_bit_exact(scene1, scene_dir, oracle_mod, tmp_path, pipeline, frames):
     W, H = 96, 64
     out = str(tmp_path / "img.f32")
     info = json.loads(node("render_frames.js", json.dumps(
-        {"sceneDir": scene_dir, "width": W, "height": H, "pipeline": pipeline, "frames": frames, "out": out})))
+        {"sceneDir": scene_dir, "width": W, "height": H, "pipeline": pipeline, "frames": frames, "out": out,
+         "present": CANVASES})))
     assert info["frames"] == frames
     img = np.fromfile(out, dtype=np.float32).reshape(H, W, 4)
     fr = oracle_mod.Frame(uniform_for(scene1, W, H, 1), scene1.scene, scene1.geometry, scene1.accel)
@@ -88,6 +111,9 @@ def test_native_renderer_frames_bit_exact(scene1, scene_dir, oracle_mod, tmp_pat
             fr.run(oracle_mod.PASS_RESTIR if pipeline == "restir" else oracle_mod.PASS_MCPT)
     np.testing.assert_array_equal(np.array(info["uniform"], dtype=np.uint64).astype(np.uint32), fr.uniform)
     np.testing.assert_array_equal(img.view(np.uint32), fr.accum.view(np.uint32))
+    for i, (cw, ch, bgra) in enumerate(CANVASES):  # Present: the render pass on the GPU
+        got = np.fromfile(f"{out}.present{i}", dtype=np.uint8).reshape(ch, cw, 4)
+        np.testing.assert_array_equal(got, oracle_mod.present(fr.accum, cw, ch, bool(bgra)), f"canvas {cw}x{ch}")
 
 
 # ---------------------------------------------------------------- the reference's World on Node
