@@ -12,16 +12,20 @@
  * Arithmetic follows wgpu-matrix's storage semantics (f64 math, f32 stores: ./wgpu_math.js),
  * so the three arrays are bit-identical to the Python scene compiler's
  * (pathtracerdemo_amd/scene/world.py) and to the golden `scene_sha256`
- * (tests/test_node_host.py).  What the Node host cannot do is Mesh.Load itself: GLB parsing
- * (three's GLTFLoader) and the SAH BLAS build (three-mesh-bvh) are not installed here, so
- * ResourceManager.LoadCompiledAssets reads each mesh's post-constructor state
- * (geometry, BVH-reordered indices, BLAS roots, materials) from
- * pathtracerdemo_amd/scene/export.py's export_meshes.  A host that has three-mesh-bvh can
- * build the same Mesh with `new Mesh({...})` from its `_roots` and geometry attributes.
+ * (tests/test_node_host.py).  Mesh.Load (Structs.ts:108-141) runs here too: ./gltf.js reads the
+ * GLB and bakes its node transforms in three.js's operation order, ./bvh.js builds the SAH BLAS
+ * (restatements of three's GLTFLoader and three-mesh-bvh, which are not installed here -- the
+ * same ones the Python scene compiler uses, bit for bit).  ResourceManager.LoadAssets(names,
+ * assetDir) fills the MeshPool from `<assetDir>/<name>.glb` as the reference's does;
+ * LoadCompiledAssets still reads a mesh state exported by pathtracerdemo_amd/scene/export.py,
+ * and a host that has three-mesh-bvh can build the same Mesh with `new Mesh({...})` from its
+ * `_roots` and geometry attributes.
  */
 const fs = require('fs');
 const path = require('path');
 const { mat4, quat, vec3, vec4 } = require('./wgpu_math');
+const { loadGlbGeometry } = require('./gltf');
+const { buildBlas } = require('./bvh');
 
 /** ResourceManager.MergeArrays (ResourceManager.ts:23-43): concatenation + element offsets. */
 function MergeArrays(arrays) {
@@ -198,10 +202,23 @@ class RectLight extends Light {
   }
 }
 
-/** ResourceManager.ts:1-21, with the loader swapped for compiled mesh state (see top). */
+/** Mesh.Load (Structs.ts:108-141): the GLB's primitives baked and merged with one group each,
+ * then the constructor's SAH BLAS build (one root per group, maxLeafTris 10). */
+Mesh.Load = async function Load(Name, AssetDir) {
+  const g = loadGlbGeometry(path.join(AssetDir, Name + '.glb'));
+  const bvh = buildBlas(g.positions, g.index, g.groups);
+  return new Mesh({ blasRoots: bvh.roots, positions: g.positions, normals: g.normals, uvs: g.uvs, index: bvh.index,
+    materials: g.materials, maxBvhDepth: bvh.maxDepth });
+};
+
+/** ResourceManager.ts:1-21 (LoadAssets from `<assetDir>/<name>.glb`), plus LoadCompiledAssets (see top). */
 const ResourceManager = {
   MeshPool: new Map(),
   MergeArrays,
+
+  async LoadAssets(names, assetDir) {
+    await Promise.all(names.map(async (name) => { ResourceManager.MeshPool.set(name, await Mesh.Load(name, assetDir)); }));
+  },
 
   /** Reads <dir>/<name>/ (export.export_meshes) into MeshPool for each name. */
   LoadCompiledAssets(dir, names) {

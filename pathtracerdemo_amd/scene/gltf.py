@@ -49,29 +49,54 @@ class GltfPrimitive:
     material: GltfMaterial = field(default_factory=GltfMaterial)
 
 
-def _quat_to_mat(q):
+def _compose(t, q, s) -> np.ndarray:
+    """three.js Matrix4.compose(position, quaternion, scale): column-major 16 f64, the library's
+    own operation order (so the JS host, js/gltf.js, computes the same bits)."""
     x, y, z, w = (float(c) for c in q)
-    # three.js Matrix4.compose (f64)
+    sx, sy, sz = (float(c) for c in s)
     x2, y2, z2 = x + x, y + y, z + z
     xx, xy, xz = x * x2, x * y2, x * z2
     yy, yz, zz = y * y2, y * z2, z * z2
     wx, wy, wz = w * x2, w * y2, w * z2
-    return np.array([[1 - (yy + zz), xy - wz, xz + wy],
-                     [xy + wz, 1 - (xx + zz), yz - wx],
-                     [xz - wy, yz + wx, 1 - (xx + yy)]], dtype=np.float64)
+    return [(1 - (yy + zz)) * sx, (xy + wz) * sx, (xz - wy) * sx, 0.0,
+            (xy - wz) * sy, (1 - (xx + zz)) * sy, (yz + wx) * sy, 0.0,
+            (xz + wy) * sz, (yz - wx) * sz, (1 - (xx + yy)) * sz, 0.0,
+            float(t[0]), float(t[1]), float(t[2]), 1.0]
 
 
-def _node_local_matrix(node) -> np.ndarray:
+def _node_local_matrix(node) -> list:
     if "matrix" in node:
-        return np.array(node["matrix"], dtype=np.float64).reshape(4, 4).T  # column-major in glTF
-    t = node.get("translation", [0.0, 0.0, 0.0])
-    r = node.get("rotation", [0.0, 0.0, 0.0, 1.0])
-    s = node.get("scale", [1.0, 1.0, 1.0])
-    m = np.eye(4, dtype=np.float64)
-    rot = _quat_to_mat(r)
-    m[:3, :3] = rot * np.array(s, dtype=np.float64)[None, :]
-    m[:3, 3] = t
-    return m
+        return [float(v) for v in node["matrix"]]  # column-major in glTF, as Matrix4.fromArray
+    return _compose(node.get("translation", [0.0, 0.0, 0.0]), node.get("rotation", [0.0, 0.0, 0.0, 1.0]),
+                    node.get("scale", [1.0, 1.0, 1.0]))
+
+
+def _multiply(a, b) -> list:
+    """three.js Matrix4.multiplyMatrices(a, b) (column-major), term order as the library's."""
+    out = [0.0] * 16
+    for r in range(4):
+        for c in range(4):
+            out[4 * c + r] = a[r] * b[4 * c] + a[4 + r] * b[4 * c + 1] + a[8 + r] * b[4 * c + 2] + a[12 + r] * b[4 * c + 3]
+    return out
+
+
+def _normal_matrix(m) -> list:
+    """three.js Matrix3.getNormalMatrix(m): the upper 3x3, inverted by cofactors, transposed
+    (column-major 9 f64); a singular matrix gives zeros."""
+    n11, n21, n31 = m[0], m[1], m[2]
+    n12, n22, n32 = m[4], m[5], m[6]
+    n13, n23, n33 = m[8], m[9], m[10]
+    t11 = n33 * n22 - n32 * n23
+    t12 = n32 * n13 - n33 * n12
+    t13 = n23 * n12 - n22 * n13
+    det = n11 * t11 + n21 * t12 + n31 * t13
+    if det == 0:
+        return [0.0] * 9
+    d = 1 / det
+    inv = [t11 * d, (n31 * n23 - n33 * n21) * d, (n32 * n21 - n31 * n22) * d,
+           t12 * d, (n33 * n11 - n31 * n13) * d, (n31 * n12 - n32 * n11) * d,
+           t13 * d, (n21 * n13 - n23 * n11) * d, (n22 * n11 - n21 * n12) * d]
+    return [inv[0], inv[3], inv[6], inv[1], inv[4], inv[7], inv[2], inv[5], inv[8]]  # transpose
 
 
 class Glb:
@@ -138,9 +163,9 @@ class Glb:
         scene = js["scenes"][js.get("scene", 0)]
         out: list[GltfPrimitive] = []
 
-        def visit(node_idx: int, parent: np.ndarray):
+        def visit(node_idx: int, parent):
             node = js["nodes"][node_idx]
-            world = parent @ _node_local_matrix(node)
+            world = _multiply(parent, _node_local_matrix(node))  # Object3D.updateMatrixWorld
             if "mesh" in node:
                 for prim in js["meshes"][node["mesh"]]["primitives"]:
                     if prim.get("mode", 4) != 4:
@@ -149,11 +174,12 @@ class Glb:
             for child in node.get("children", []):
                 visit(child, world)
 
+        identity = [1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0]
         for root in scene["nodes"]:
-            visit(root, np.eye(4, dtype=np.float64))
+            visit(root, identity)
         return out
 
-    def _bake(self, prim, world: np.ndarray) -> GltfPrimitive:
+    def _bake(self, prim, world) -> GltfPrimitive:
         attrs = prim["attributes"]
         pos = self.accessor(attrs["POSITION"]).astype(np.float64)
         nrm = self.accessor(attrs["NORMAL"]).astype(np.float64) if "NORMAL" in attrs else None
@@ -162,15 +188,25 @@ class Glb:
             idx = self.accessor(prim["indices"]).reshape(-1).astype(np.uint32)
         else:
             idx = np.arange(pos.shape[0], dtype=np.uint32)
-        # Vector3.applyMatrix4 (with the projective w, exactly 1 for affine nodes)
-        h = np.concatenate([pos, np.ones((pos.shape[0], 1))], axis=1) @ world.T
-        p_world = (h[:, :3] / h[:, 3:4]).astype(np.float32)
+        e = world
+        x, y, z = pos[:, 0], pos[:, 1], pos[:, 2]
+        # BufferGeometry.applyMatrix4 -> Vector3.applyMatrix4: w = 1 / (e3 x + e7 y + e11 z + e15),
+        # each coordinate (e0 x + e4 y + e8 z + e12) * w, in f64, stored to the f32 attribute
+        w = 1 / (e[3] * x + e[7] * y + e[11] * z + e[15])
+        p_world = np.stack([(e[0] * x + e[4] * y + e[8] * z + e[12]) * w,
+                            (e[1] * x + e[5] * y + e[9] * z + e[13]) * w,
+                            (e[2] * x + e[6] * y + e[10] * z + e[14]) * w], axis=1).astype(np.float32)
         if nrm is None:
             raise ValueError("primitives without normals are not supported")
-        # BufferAttribute.applyNormalMatrix: Matrix3.getNormalMatrix = inverse-transpose, then normalize()
-        nm = np.linalg.inv(world[:3, :3]).T
-        n = nrm @ nm.T
-        ln = np.sqrt((n * n).sum(axis=1, keepdims=True))
-        n = np.where(ln > 0, n / np.where(ln > 0, ln, 1.0), 0.0).astype(np.float32)
-        return GltfPrimitive(positions=p_world, normals=n, uvs=uv, indices=idx,
+        # BufferAttribute.applyNormalMatrix(Matrix3.getNormalMatrix(m)) -> Vector3.applyMatrix3,
+        # then normalize(): divideScalar(length() || 1), f64, stored to f32
+        n = _normal_matrix(world)
+        x, y, z = nrm[:, 0], nrm[:, 1], nrm[:, 2]
+        nx = n[0] * x + n[3] * y + n[6] * z
+        ny = n[1] * x + n[4] * y + n[7] * z
+        nz = n[2] * x + n[5] * y + n[8] * z
+        ln = np.sqrt(nx * nx + ny * ny + nz * nz)
+        ln = np.where(ln == 0, 1.0, ln)
+        nrm_w = np.stack([nx / ln, ny / ln, nz / ln], axis=1).astype(np.float32)
+        return GltfPrimitive(positions=p_world, normals=nrm_w, uvs=uv, indices=idx,
                              material=self.material(prim.get("material")))
