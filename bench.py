@@ -96,6 +96,7 @@ def parse():
                     help="C-oracle CPU baseline threads (default: every logical CPU of the host, os.cpu_count(); "
                          "a 16-thread figure is reported beside it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs3", action="store_true", help="skip the configs3_one_gpu line (profiling runs)")
     ap.add_argument("--variant", choices=["wave", "simple"], default="wave",
                     help="kernel variant (A/B): wavefront queues, or 1 thread/pixel")
     return ap.parse_args()
@@ -411,7 +412,7 @@ def main():
     # configs[3]'s 3840x2160 frame on this one GPU: the single-GPU reference of the strong
     # split the N > 1 lines run (their per-GPU efficiency is value_N / (N x this value))
     one_gpu_4k = None
-    if world == 1 and pipeline == "reuse" and (W, H) == (1920, 1080) and args.variant == "wave":
+    if world == 1 and pipeline == "reuse" and (W, H) == (1920, 1080) and args.variant == "wave" and not args.no_configs3:
         one_gpu_4k = one_gpu_rate(cs, 3840, 2160, pipeline, device, max(5, args.steps // 2), args.warmup)
     if world > 1:
         workload = (f"{args.scene} {pipeline} {W}x{H} split over {world} GPUs, 1 spp/frame (configs[3])"

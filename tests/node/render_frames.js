@@ -27,6 +27,11 @@ async function main() {
   }
   const img = r.ReadImage();
   fs.writeFileSync(req.out, Buffer.from(img.buffer, img.byteOffset, img.byteLength));
+  // the render pass on the GPU (Present) for each requested canvas [w, h, bgra]
+  (req.present || []).forEach(([cw, ch, bgra], i) => {
+    const px = r.Present(cw, ch, !!bgra);
+    fs.writeFileSync(`${req.out}.present${i}`, Buffer.from(px.buffer, px.byteOffset, px.byteLength));
+  });
   const st = r.GetStats();
   r.Destroy();
   process.stdout.write(JSON.stringify({ frames: st.frames, uniform: Array.from(r.Uniform) }));

@@ -15,11 +15,11 @@ export PTX_AB="WAVE_STREAMS=1,PIPELINE_FRAMES=0${EXTRA_AB:+,$EXTRA_AB}"
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-    python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline $ARGS > "$OUT/bench_trace.log" 2>&1 || { echo "trace rc=$?"; exit 1; }
+    python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-configs3 $ARGS > "$OUT/bench_trace.log" 2>&1 || { echo "trace rc=$?"; exit 1; }
 echo "trace ok"; tail -n 1 "$OUT/bench_trace.log"
 if [ "${NO_PMC:-0}" = "1" ]; then exit 0; fi
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C -d "$OUT/pmc_$C" -o run --output-format csv -- \
-      python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline $ARGS > "$OUT/bench_$C.log" 2>&1 || { echo "pmc $C rc=$?"; exit 1; }
+      python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-configs3 $ARGS > "$OUT/bench_$C.log" 2>&1 || { echo "pmc $C rc=$?"; exit 1; }
   echo "pmc $C ok"
 done
