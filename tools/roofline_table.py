@@ -32,7 +32,8 @@ rows = [
     ("frame-level frac (§8d)", lambda d, w: f"{d['roofline']['frame']['frac']:.3f}"),
     ("HBM traffic per trace launch (PMC)",
      lambda d, w: f"{d['roofline']['traffic'] / 1e6:.0f} MB" if d['roofline'].get('traffic') else "–"),
-    ("CPU baseline (C oracle, 16 threads)", lambda d, w: f"{d['cpu_baseline']['value']:.2f} Msamples/s"),
+    ("CPU baseline (C oracle; threads)",
+     lambda d, w: f"{d['cpu_baseline']['value']:.2f} Msamples/s ({d['cpu_baseline']['cores']})"),
     ("JS CPU baseline (reference pipeline, Node workers)",
      lambda d, w: f"{d['ts_cpu_baseline']['value']:.2f} Msamples/s" if d.get("ts_cpu_baseline") else "–"),
 ]
