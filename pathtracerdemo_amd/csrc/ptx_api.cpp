@@ -644,6 +644,14 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     // (PTX_AB=PIPE_STREAMS=k: A/B)
     static const int env_pk = ab_knob("PIPE_STREAMS", 0);
     int k = h->alt_stream && pipelined(h) ? (env_pk > 0 ? env_pk : 1) : env_k > 0 ? env_k : 3;
+    // a pipelined frame's spatial pass + PT_4 (the serial back half every frame waits for) as
+    // two launch sequences: one half's trace rounds overlap the other's logic kernels.  Same
+    // box, 1080p C3 reuse: 1 sequence 387.2, 2: 396.1, 3: 369.7 Msamples/s (3 contexts' streams
+    // oversubscribe the 4 hardware queues).  PTX_AB=PIPE_BACK_STREAMS=k: A/B.
+    static const int env_bk = ab_knob("PIPE_BACK_STREAMS", 2);
+    if (env_bk > 0 && h->alt_stream && pipelined(h))
+        for (int i = 0; i < npasses; ++i)
+            if (passes[i] == PTX_PASS_SPATIAL) k = env_bk;
     if (h->cfg.flags & PTX_FLAG_SINGLE_STREAM) k = 1;
     k = std::max(1, std::min<int>(k, ptx_handle::kMaxSplit));
     if ((uint32_t)k > std::max(w.nseg, then ? then->nseg : 0u)) k = (int)std::max(w.nseg, then ? then->nseg : 0u);
