@@ -870,7 +870,7 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
             if (pf.lane[r]) atomicAdd(&sc.counters[9 + 2 * r], (unsigned long long)pf.lane[r]);
         }
     }
-    if (COUNT && counted) {
+    if ((COUNT || PROF) && counted) {  // (PROF alone: the culled walk's executed tests)
         atomicAdd(&sc.counters[CNT_RAYS], 1ull);
         atomicAdd(&sc.counters[CNT_INST], (unsigned long long)sc.n_inst);
         atomicAdd(&sc.counters[CNT_AABB], (unsigned long long)n_aabb);

@@ -1086,9 +1086,16 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
             hipLaunchKernelGGL(trace_queue_sm<false>, dim3(w.seg_count), dim3(WB), lds, s, sc,
                                w.rays + 2u * (size_t)pb * w.ray_stride, res, cnt,
                                w.ray_stride, 0u, eps);
-    } else if (sc.counters && ab_knob("TRACE_PROF", 0))  // SIMD-utilisation diagnostics
-        hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round,
-                           eps);
+    } else if (sc.counters && ab_knob("TRACE_PROF", 0)) {  // SIMD-utilisation diagnostics
+        if (flat && tables_fit_lds(sc))  // (the production walk: flattened instances, LDS tables, and
+            // COUNT off so that the instance cull applies as in production -- the PROF regions
+            // still count into sc.counters; the work counters stay zero)
+            hipLaunchKernelGGL((trace_queue<false, 6, true, true, false, true>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
+                               (uint32_t)round, eps);
+        else
+            hipLaunchKernelGGL((trace_queue<true, 6, true, false>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w,
+                               (uint32_t)round, eps);
+    }
     else if (sc.counters)
         hipLaunchKernelGGL((trace_queue<true, 6, false, false>), dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
     else {

@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """SIMD utilisation of the wavefront trace kernel by traversal region (diagnostic build).
 
-Runs each pass of one 1080p frame with PTX_FLAG_COUNT_WORK and PTX_TRACE_PROF=1 and prints,
+Runs each pass of one 1080p frame with PTX_FLAG_COUNT_WORK and PTX_AB=TRACE_PROF and prints,
 per region (instance transform, root test, node loop, leaf block, triangle loop), the
 wave-level executions, the mean active lanes per execution (of 64) and per-query averages.
+On scenes the production walk flattens (>= 3 instances, tables in LDS) the profiled kernel is
+that walk with the instance cull applied (its AABB / triangle counts are the tests executed);
+otherwise the counting walk (every instance visited, the reference's counts).
 usage: python tools/simd_util.py [--workload restir|mcpt]
 """
 import argparse
