@@ -774,9 +774,10 @@ bool pipelined(const ptx_handle *h) {
     const bool band = h->comm || h->halo_top || h->halo_bot;
     // at most ~4 Mpx per frame: a 3840x2160 frame's launches are large enough to fill the chip
     // on their own (configs[3] on one GPU: 384 Msamples/s unpipelined, 355 pipelined)
+    static const size_t max_px = (size_t)ab_knob("PIPE_MAX_KPX", 4096) << 10;  // A/B
     const size_t px = (size_t)h->band_h * h->cfg.width;
     return !off && !(band && bands_off) && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE &&
-           px <= (size_t)4u << 20 &&
+           px <= max_px &&
            !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK |
                    PTX_FLAG_TIME_LAUNCHES | PTX_FLAG_SINGLE_STREAM | PTX_FLAG_ROW_CENSUS)) &&
            (h->alt_active ? h->stream == h->alt_stream : h->stream == h->own_stream);
