@@ -524,6 +524,9 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.nbr_out = (uint4 *)h->d_nbr.p + (size_t)h->halo_top * h->cfg.width;
     A.nbr = A.nbr_out;
     A.surf = h->d_surf.p ? (const uint4 *)h->d_surf.p + 2u * (size_t)h->halo_top * h->cfg.width : nullptr;
+    static const bool fold_off = ab_knob("FOLD_LAST_STEP", 1) == 0;  // A/B
+    A.fold_last = (pass == PTX_PASS_SPATIAL && !fold_off) ? 1u : 0u;
+    A.ray_cap = (uint32_t)std::min<size_t>(h->wave_ray_cap, 0xffffffffu);
     return A;
 }
 
@@ -579,6 +582,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
                 event_end(t, st);
             }
             if (e != hipSuccess) break;
+            if (r == nr && A.fold_last) continue;  // (the combine finishes these jobs)
             TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
             e = wave_reuse_round(sc, wj, pass == PTX_PASS_TEMPORAL, r, A, st);
             event_end(t, st);

@@ -110,7 +110,14 @@ struct ReuseArgs {
     const uint4 *nbr;   // spatial: per-pixel neighbour summary (wave_reuse_summary), cur's addressing
     uint4 *nbr_out;     // the same buffer: the temporal pass writes its output's summaries
     const uint4 *surf;  // primary-hit surface records (WaveBufs::surf), cur's addressing
+    // spatial: the last step launch is folded into the combine -- the light rays emitted for
+    // the last trace round leave {ray index, -, -, kJobPending} in jres, and the combine reads
+    // their Visibility result and the job's F slot itself (wjob_step's phase-1 arithmetic)
+    uint32_t fold_last;
+    uint32_t ray_cap;   // ray slots of the wave buffers: a stale jres word (a slot the combine
+                        // loads but does not use) never sends the fold's gather out of bounds
 };
+constexpr uint32_t kJobPending = 0xFFFFFFFFu;  // jres.w of such a job (a NaN: never a stored q)
 // rounds of {trace, step} between a reuse pass's start and combine launches
 int reuse_rounds(int pass_temporal, const ReuseArgs &A);
 hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,
