@@ -432,10 +432,14 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
         free_buf(h->d_wrays);
         free_buf(h->d_wres0);
         free_buf(h->d_wres1);
+        free_buf(h->d_wres2);
         h->wave_ray_cap = 0;
         if (int rc = alloc_buf(h, h->d_wrays, cap * 32u)) return rc;
         if (int rc = alloc_buf(h, h->d_wres0, cap * 32u)) return rc;
         if (int rc = alloc_buf(h, h->d_wres1, cap * 32u)) return rc;
+        // the spatial reuse pass keeps one result buffer per trace round (ReuseArgs::fold_last)
+        if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE)
+            if (int rc = alloc_buf(h, h->d_wres2, cap * 32u)) return rc;
         h->wave_ray_cap = cap;
     }
     w.surf = nullptr;
@@ -453,6 +457,8 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     w.rays = (float4 *)h->d_wrays.p;
     w.res[0] = (float4 *)h->d_wres0.p;
     w.res[1] = (float4 *)h->d_wres1.p;
+    w.res[2] = (float4 *)h->d_wres2.p;
+    w.nres = 2;
     w.act[0] = (uint32_t *)h->d_wact0.p;
     w.act[1] = (uint32_t *)h->d_wact1.p;
     // one stride for every pass: passes of different kinds run concurrently on the two
@@ -572,8 +578,10 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         return e;
     }
     if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL) {
-        const ReuseArgs A = reuse_args(h, pass);
-        const WaveBufs &wj = w;
+        ReuseArgs A = reuse_args(h, pass);
+        WaveBufs wj = w;
+        if (A.fold_last && wj.res[2]) wj.nres = 3;  // light segments finished by the combine
+        else A.fold_last = 0u;
         const int nr = reuse_rounds(pass == PTX_PASS_TEMPORAL, A);
         for (int r = 0; e == hipSuccess && r <= nr + 1; ++r) {
             if (r > 0 && r <= nr) {
@@ -805,6 +813,7 @@ void swap_frame_ctx(ptx_handle *h) {
     std::swap(h->d_wrays, a.wrays);
     std::swap(h->d_wres0, a.wres0);
     std::swap(h->d_wres1, a.wres1);
+    std::swap(h->d_wres2, a.wres2);
     std::swap(h->d_wact0, a.wact0);
     std::swap(h->d_wact1, a.wact1);
     std::swap(h->d_wctr, a.wctr);
@@ -1454,11 +1463,11 @@ int ptx_destroy(ptx_handle *h) {
     if (h->host_stage) (void)hipHostFree(h->host_stage);
     for (DevBuf *b : {&h->d_canvas, &h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
-                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wact0, &h->d_wact1, &h->d_wctr,
+                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wres2, &h->d_wact0, &h->d_wact1, &h->d_wctr,
                       &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_surf, &h->d_direct, &h->d_census})
         free_buf(*b);
     ptx_handle::FrameCtx &a = h->alt;
-    for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wact0, &a.wact1, &a.wctr})
+    for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wres2, &a.wact0, &a.wact1, &a.wctr})
         free_buf(*b);
     if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

@@ -70,7 +70,7 @@ struct ptx_handle {
     uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
     DevBuf d_qrays, d_qhits;  // staging for ptx_trace (host arrays)
     // wavefront variant: pixel state, ray queue + ping-pong results / active lists, counters
-    DevBuf d_wstate, d_wrays, d_wres0, d_wres1, d_wact0, d_wact1, d_wctr;
+    DevBuf d_wstate, d_wrays, d_wres0, d_wres1, d_wres2, d_wact0, d_wact1, d_wctr;
     size_t wave_ray_cap = 0;
     // second stream: the two halves of the segments run as independent launch sequences so
     // one half's latency-bound traces overlap the other's ALU-bound shading
@@ -92,7 +92,7 @@ struct ptx_handle {
     // ptx_render swaps the members above with `alt` per frame, so everything else always sees
     // the latest frame's buffers; the shared ones (accumulation, history, jobs, scene) never move.
     struct FrameCtx {
-        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wact0, wact1, wctr;
+        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wres2, wact0, wact1, wctr;
         size_t wave_ray_cap = 0;
         uint32_t wave_slots = 0;
         hipStream_t stream = nullptr;

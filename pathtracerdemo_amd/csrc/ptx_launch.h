@@ -60,7 +60,9 @@ struct WaveBufs {
     uint32_t cluster;    // segment layout: 16/cluster runs of `cluster` adjacent 8x8 tiles
     uint32_t ray_stride; // ray slots per segment (seg_px * max rays per pixel per round)
     float4 *rays;        // 2 float4 per ray: {o, remain}, {d, kind}
-    float4 *res[2];      // 2 float4 per ray, ping-pong by round parity
+    float4 *res[3];      // 2 float4 per ray, ping-pong by round parity (nres = 2) or one per
+    uint32_t nres;       // round (nres = 3: the spatial reuse pass, whose combine reads every
+                         // round's light-ray results; res_buf)
     uint32_t *act[2];    // active pixel / job lists (nseg * act_stride), ping-pong
     uint32_t act_stride; // list entries per segment (seg_px; seg_px * jobs per pixel for reuse)
     uint32_t *cnt;       // 2 * kWaveMaxRounds * nseg counts
@@ -110,9 +112,11 @@ struct ReuseArgs {
     const uint4 *nbr;   // spatial: per-pixel neighbour summary (wave_reuse_summary), cur's addressing
     uint4 *nbr_out;     // the same buffer: the temporal pass writes its output's summaries
     const uint4 *surf;  // primary-hit surface records (WaveBufs::surf), cur's addressing
-    // spatial: the last step launch is folded into the combine -- the light rays emitted for
-    // the last trace round leave {ray index, -, -, kJobPending} in jres, and the combine reads
-    // their Visibility result and the job's F slot itself (wjob_step's phase-1 arithmetic)
+    // spatial: a job's light segment is finished by the combine -- every light ray a job emits
+    // leaves {ray index, result buffer, -, kJobPending} in jres (the pass keeps one result
+    // buffer per trace round, WaveBufs::nres = 3), and the combine reads its Visibility result
+    // and the job's F slot itself (wjob_step's phase-1 arithmetic); no step launch after the
+    // last trace round, and the steps see heavy jobs only
     uint32_t fold_last;
     uint32_t ray_cap;   // ray slots of the wave buffers: a stale jres word (a slot the combine
                         // loads but does not use) never sends the fold's gather out of bounds

@@ -195,6 +195,18 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
     return ray;
 }
 
+// After job_emit: store a live job's state and queue it for the next step -- except a job whose
+// light ray just went out in a pass that folds light segments into its combine
+// (ReuseArgs::fold_last): its jres slot names the ray and its result buffer instead, and no
+// step sees it again (its F slot, stored here, is what the combine multiplies).
+__device__ __forceinline__ void job_finish(const Seg &g, const JobLists &JL, const ReuseArgs &A, bool live,
+                                           const Job &s, uint32_t jid) {
+    if (live) job_store(A, jid, s);
+    const bool fold = live && A.fold_last && s.phase != 0u;
+    if (fold) A.jres[jid] = make_float4(asf(s.idx), asf(g.out_sel), 0.0f, asf(kJobPending));
+    job_keep(g, JL, live && !fold, live && s.phase != 0u, jid);
+}
+
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
 void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
     PTX_WAVE_TIMER(sc, KID_JOB_STEP);
@@ -236,11 +248,7 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
             }
         }
         const bool live = job_emit(sc, g, A, emit, s, jid, 0u);  // (s.i >= 2 here)
-        if (live) job_store(A, jid, s);
-        // a light ray for the last trace round: the combine finishes the job (ReuseArgs::fold_last)
-        const bool fold = live && A.fold_last && round + 1u == (uint32_t)kWaveRoundsReuse;
-        if (fold) A.jres[jid] = make_float4(asf(s.idx), 0.0f, 0.0f, asf(kJobPending));
-        job_keep(g, JL, live && !fold, live && s.phase != 0u, jid);
+        job_finish(g, JL, A, live, s, jid);
     }
     job_seg_end(w, g, JL);
 }
@@ -259,11 +267,11 @@ __device__ __forceinline__ SelF job_f(float4 r) { return SelF{r.w > 0.0f, mk(r.x
 // A job result as the combine reads it: a job folded into the combine (ReuseArgs::fold_last)
 // is finished here with wjob_step's phase-1 arithmetic -- its light segment's Visibility
 // result (res) and the F slot of its state.
-__device__ __forceinline__ float4 job_result(const ReuseArgs &A, const float4 *res, float4 r, uint32_t jid) {
+__device__ __forceinline__ float4 job_result(const ReuseArgs &A, const WaveBufs &w, float4 r, uint32_t jid) {
     // (a slot the combine loads but never uses may hold anything: a stale or uninitialised
     // word pair is kept inside the buffers, its value is discarded by the caller)
-    if (asu(r.w) != kJobPending || asu(r.x) >= A.ray_cap) return r;
-    const float4 a = res[2u * asu(r.x)], fv = A.jstate[JS_F * (size_t)A.njobs + jid];
+    if (asu(r.w) != kJobPending || asu(r.x) >= A.ray_cap || asu(r.y) >= w.nres) return r;
+    const float4 a = w.res[asu(r.y)][2u * asu(r.x)], fv = A.jstate[JS_F * (size_t)A.njobs + jid];
     const f3 f = mk(fv.x, fv.y, fv.z) * (mk(a.y, a.z, a.w) * a.x);
     const float qv = fv.w;
     const bool valid = qv > 0.0f && qv <= 3.402823466e38f;
@@ -578,8 +586,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 if (want && !act) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
             const bool live = job_emit(sc, g, A, act, s, jid, s0);
-            if (live) job_store(A, jid, s);
-            job_keep(g, JL, live, live && s.phase != 0u, jid);
+            job_finish(g, JL, A, live, s, jid);
         }
     }
     job_seg_end(w, g, JL);
@@ -624,7 +631,7 @@ __device__ __forceinline__ float neighbour_weight(const CombineCanon &c, float M
 // summary and job results are gathered up front (one memory round trip instead of 2 MT
 // dependent ones); MT = 0: any count, gathered per neighbour.
 template <uint32_t MT>
-__device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &A, const float4 *lres, uint32_t x,
+__device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &A, const WaveBufs &w, uint32_t x,
                                               uint32_t y, uint32_t pix) {
     uint4 *out = A.hist + 8u * (size_t)pix;
     const uint4 *rc = A.cur + 8u * (size_t)pix;
@@ -652,8 +659,8 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
 #pragma unroll
         for (uint32_t m = 0; m < MT; ++m) {  // (job results of absent neighbours are never used)
             nv[m] = A.nbr[nid[m]];
-            Fr[m] = job_result(A, lres, jr[2u * m], pix * A.jpp + 2u * m);
-            B[m] = job_result(A, lres, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u);
+            Fr[m] = job_result(A, w, jr[2u * m], pix * A.jpp + 2u * m);
+            B[m] = job_result(A, w, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u);
         }
         Nbr nb[MT];
 #pragma unroll
@@ -689,7 +696,7 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
                 const Nbr nb = nbr_at(A, band_index(sc, nx, ny));
                 if (nb.valid) {
                     Csum += nb.C;
-                    Q = canon_q(c, Mf, nb.C, job_result(A, lres, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u));
+                    Q = canon_q(c, Mf, nb.C, job_result(A, w, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u));
                 }
             }
             sumQ += Q;
@@ -704,7 +711,7 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
             int32_t nidx = 0;
             if (spatial_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
                 nidx = band_index(sc, nx, ny);
-                wn = neighbour_weight(c, Mf, nbr_at(A, nidx), job_result(A, lres, jr[2u * m], pix * A.jpp + 2u * m), pf,
+                wn = neighbour_weight(c, Mf, nbr_at(A, nidx), job_result(A, w, jr[2u * m], pix * A.jpp + 2u * m), pf,
                                       qf, fj);
             }
             if (wrs_update(w_sum, wn, seed)) { src = nidx; p_sel = pf; q_sel = qf; f_sel = fj; }
@@ -725,7 +732,6 @@ constexpr uint32_t kShflLanes = 4u;  // lanes per pixel (M + 1 with M = 3)
 __global__ __launch_bounds__(WB) void wspatial_combine_shfl(Scene sc, WaveBufs w, ReuseArgs A) {
     PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE);
     constexpr uint32_t M = 3u;
-    const float4 *lres = w.res[(kWaveRoundsReuse - 1) & 1];  // the last trace round's results
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
     const uint32_t lane = __lane_id(), r = lane & 3u, base = lane & ~3u;
     for (uint32_t k = 0; k < w.seg_px; k += WB / kShflLanes) {  // workgroup-uniform
@@ -753,8 +759,8 @@ __global__ __launch_bounds__(WB) void wspatial_combine_shfl(Scene sc, WaveBufs w
             if (pres) nid = band_index(sc, nx, ny);
             const uint4 nv = A.nbr[nid];
             const float4 *jr = A.jres + (size_t)pix * A.jpp;
-            Fr = job_result(A, lres, jr[2u * m], pix * A.jpp + 2u * m);
-            B = job_result(A, lres, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u);
+            Fr = job_result(A, w, jr[2u * m], pix * A.jpp + 2u * m);
+            B = job_result(A, w, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u);
             nb = nv.w != kNbrEscape ? Nbr{(nv.w >> 31) != 0u, (nv.w >> 24) & 0x7fu, nv.w & 0xffffffu, asf(nv.x),
                                           asf(nv.y), asf(nv.z)}
                                     : nbr_at(A, nid);
@@ -814,7 +820,6 @@ __global__ __launch_bounds__(WB) void wspatial_combine_shfl(Scene sc, WaveBufs w
 
 __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, ReuseArgs A) {
     PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE);
-    const float4 *lres = w.res[(kWaveRoundsReuse - 1) & 1];  // the last trace round's results
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
     for (uint32_t k = 0; k < w.seg_px; k += WB) {
         const uint32_t q = seg_pixel(w, j, k);
@@ -826,8 +831,8 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
             for (int t = 0; t < 8; ++t) out[t] = make_uint4(0u, 0u, 0u, 0u);
             continue;
         }
-        if (A.neighbors == 3u) combine_pixel<3>(sc, A, lres, x, y, pix);
-        else combine_pixel<0>(sc, A, lres, x, y, pix);
+        if (A.neighbors == 3u) combine_pixel<3>(sc, A, w, x, y, pix);
+        else combine_pixel<0>(sc, A, w, x, y, pix);
     }
 }
 

@@ -196,7 +196,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                 const uint32_t i = (bi - pref[lo]) * 64u + lane;
                 trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
                                               w.rays + 2u * (size_t)j * w.ray_stride,
-                                              w.res[round & 1u] + 2u * (size_t)j * w.ray_stride, i, i < n);
+                                              res_buf(w, round) + 2u * (size_t)j * w.ray_stride, i, i < n);
             }
             bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
         }
@@ -219,7 +219,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     if (COUNT && sc.census)  // row census: this slot's queries count into its own block
         sc.counters = sc.census + (size_t)kCensusWords * ((sc.row_end - sc.row_begin + 7u) / 8u + j);
     const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
-    float4 *res = w.res[round & 1u] + 2u * (size_t)j * w.ray_stride;
+    float4 *res = res_buf(w, round) + 2u * (size_t)j * w.ray_stride;
     for (uint32_t i0 = share * WB; i0 < n; i0 += K * WB) {  // workgroup-uniform
         const uint32_t i = i0 + threadIdx.x;
         trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop, rays, res, i, i < n);
@@ -1077,7 +1077,7 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
     if (refill) {
         const uint32_t pb = w.seg_phys + w.seg_base;
         const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.cnt_stride + pb;
-        float4 *res = w.res[round & 1] + 2u * (size_t)pb * w.ray_stride;
+        float4 *res = w.res[w.nres == 3u ? round % 3 : round & 1] + 2u * (size_t)pb * w.ray_stride;
         if (sc.counters)
             hipLaunchKernelGGL(trace_queue_sm<true>, dim3(w.seg_count), dim3(WB), lds, s, sc,
                                w.rays + 2u * (size_t)pb * w.ray_stride, res, cnt,

@@ -35,11 +35,17 @@ struct Seg {
     uint32_t rbase;            // first ray slot of the segment
     float4 *rays, *res_out;    // rays emitted this round + their result/payload slots
     const float4 *res_in;      // results of the previous trace round
+    uint32_t out_sel;          // res_out's index in WaveBufs::res
     uint32_t *act_out;         // active list written this round (segment-local)
     const uint32_t *act_in;    // active list of the previous round
     uint32_t n_in;             // its length
     uint32_t *l_ray, *l_act;   // LDS counters
 };
+// The result buffer of trace round `round`.
+__device__ __forceinline__ uint32_t res_sel(const WaveBufs &w, uint32_t round) {
+    return w.nres == 3u ? round % 3u : round & 1u;
+}
+__device__ __forceinline__ float4 *res_buf(const WaveBufs &w, uint32_t round) { return w.res[res_sel(w, round)]; }
 __device__ __forceinline__ Seg seg_begin(const WaveBufs &w, uint32_t round, uint32_t *lds) {
     Seg g;
     g.j = w.seg_base + blockIdx.x;
@@ -47,8 +53,9 @@ __device__ __forceinline__ Seg seg_begin(const WaveBufs &w, uint32_t round, uint
     g.round = round;
     g.rbase = g.pj * w.ray_stride;
     g.rays = w.rays;
-    g.res_out = w.res[round & 1u];
-    g.res_in = w.res[(round + 1u) & 1u];
+    g.res_out = res_buf(w, round);
+    g.res_in = round ? res_buf(w, round - 1u) : w.res[1];  // (round 0 reads no results)
+    g.out_sel = res_sel(w, round);
     g.act_out = w.act[round & 1u] + (size_t)g.pj * w.act_stride;
     g.act_in = w.act[(round + 1u) & 1u] + (size_t)g.pj * w.act_stride;
     g.n_in = round ? w.cnt[(2u * (round - 1u)) * w.cnt_stride + g.pj] : 0u;

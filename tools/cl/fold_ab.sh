@@ -1,4 +1,4 @@
-# the spatial pass's last job step folded into the combine (ReuseArgs::fold_last): GPU suite, then
+# the spatial pass's light segments finished by the combine (ReuseArgs::fold_last): GPU suite, then
 # same-box A/B against PTX_AB=FOLD_LAST_STEP=0 on the headline (3 reps) and the furnished scene
 set -o pipefail
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/fold_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/fold_tests.log; exit 1; }
