@@ -531,7 +531,7 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.nbr = A.nbr_out;
     A.surf = h->d_surf.p ? (const uint4 *)h->d_surf.p + 2u * (size_t)h->halo_top * h->cfg.width : nullptr;
     static const bool fold_off = ab_knob("FOLD_LAST_STEP", 1) == 0;  // A/B
-    A.fold_last = (pass == PTX_PASS_SPATIAL && !fold_off) ? 1u : 0u;
+    A.fold_last = ((pass == PTX_PASS_SPATIAL || pass == PTX_PASS_TEMPORAL) && !fold_off) ? 1u : 0u;
     A.ray_cap = (uint32_t)std::min<size_t>(h->wave_ray_cap, 0xffffffffu);
     return A;
 }

@@ -368,8 +368,7 @@ void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
             if (active && A.use_init) active = temporal_from_init(sc, w, A, s, pix);
         }
         const bool live = job_emit(sc, g, A, active, s, pix, active ? A.cur[8u * (size_t)pix].x : 0u);
-        if (live) job_store(A, pix, s);
-        job_keep(g, JL, live, live && s.phase != 0u, pix);
+        job_finish(g, JL, A, live, s, pix);
     }
     job_seg_end(w, g, JL);
 }
@@ -392,7 +391,7 @@ __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, Re
         const uint4 *hv = A.hist + 8u * (size_t)pix;
         uint32_t seed = reuse_seed(sc, x, y, SALT_TEMPORAL);
         const uint4 r5 = rv[5], r7 = rv[7];
-        const float4 er = (r7.y != 0u && r5.w >= 2u) ? A.jres[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float4 er = (r7.y != 0u && r5.w >= 2u) ? job_result(A, w, A.jres[pix], pix) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float2 ec = make_float2(er.w > 0.0f ? luminance(mk(er.x, er.y, er.z)) : 0.0f, er.w);
         const bool canon_ok = ec.y > 0.0f && ec.x > 0.0f;
         const uint4 h5 = hv[5], h6 = hv[6], h7 = hv[7];
