@@ -511,6 +511,9 @@ int reuse_buffers(ptx_handle *h) {
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) return alloc_buf(h, h->d_jres, njobs * 4u);  // ray index per job
     if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
     if (int rc = alloc_buf(h, h->d_nbr, px_with_halo(h) * 16u)) return rc;
+    const size_t npix = (size_t)h->band_h * h->cfg.width;
+    if (int rc = alloc_buf(h, h->d_tjstate, npix * 6u * 16u)) return rc;
+    if (int rc = alloc_buf(h, h->d_tjres, npix * 16u)) return rc;
     return alloc_buf(h, h->d_jres, njobs * 16u);
 }
 static ReuseArgs reuse_args(ptx_handle *h, int pass) {
@@ -518,9 +521,10 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.gbuf = gbuf_band(h);
     A.cur = res_band(h);
     A.hist = (uint4 *)h->d_hist.p;
-    A.jstate = (float4 *)h->d_jstate.p;
-    A.jres = (float4 *)h->d_jres.p;
-    A.jpp = pass == PTX_PASS_TEMPORAL ? 1u : 2u * h->reuse_neighbors;
+    const bool temporal = pass == PTX_PASS_TEMPORAL;
+    A.jstate = (float4 *)(temporal ? h->d_tjstate.p : h->d_jstate.p);
+    A.jres = (float4 *)(temporal ? h->d_tjres.p : h->d_jres.p);
+    A.jpp = temporal ? 1u : 2u * h->reuse_neighbors;
     A.njobs = h->band_h * h->cfg.width * A.jpp;
     A.radius = h->reuse_radius;
     A.neighbors = h->reuse_neighbors;
@@ -577,13 +581,18 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         }
         return e;
     }
-    if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL) {
-        ReuseArgs A = reuse_args(h, pass);
+    if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL || pass == kPassTemporalJobs ||
+        pass == kPassTemporalCombine) {
+        const bool temporal = pass != PTX_PASS_SPATIAL;
+        ReuseArgs A = reuse_args(h, temporal ? PTX_PASS_TEMPORAL : PTX_PASS_SPATIAL);
         WaveBufs wj = w;
         if (A.fold_last && wj.res[2]) wj.nres = 3;  // light segments finished by the combine
         else A.fold_last = 0u;
-        const int nr = reuse_rounds(pass == PTX_PASS_TEMPORAL, A);
-        for (int r = 0; e == hipSuccess && r <= nr + 1; ++r) {
+        const int nr = reuse_rounds(temporal, A);
+        // (the temporal pass in parts: its jobs = rounds 0..nr, its combine = round nr + 1)
+        const int r_first = pass == kPassTemporalCombine ? nr + 1 : 0;
+        const int r_last = pass == kPassTemporalJobs ? nr : nr + 1;
+        for (int r = r_first; e == hipSuccess && r <= r_last; ++r) {
             if (r > 0 && r <= nr) {
                 TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
                 e = wave_trace(sc, wj, r - 1, 1, h->stack_depth, st);
@@ -592,7 +601,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
             if (e != hipSuccess) break;
             if (r == nr && A.fold_last) continue;  // (the combine finishes these jobs)
             TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
-            e = wave_reuse_round(sc, wj, pass == PTX_PASS_TEMPORAL, r, A, st);
+            e = wave_reuse_round(sc, wj, temporal, r, A, st);
             event_end(t, st);
         }
         return e;
@@ -674,7 +683,8 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     for (int i = 0; i < npasses; ++i) {
         if (passes[i] == PTX_PASS_SPATIAL) {
             if (summaries && (e = spatial_summaries(h, h->stream)) != hipSuccess) return e;
-        } else if (passes[i] != PTX_PASS_FINAL && passes[i] != PTX_PASS_TEMPORAL) {
+        } else if (passes[i] != PTX_PASS_FINAL && passes[i] != PTX_PASS_TEMPORAL && passes[i] != kPassTemporalJobs &&
+                   passes[i] != kPassTemporalCombine) {
             h->nbr_valid = false;  // G-buffer / PT_1 / MCPT rewrite what the summaries describe
         }
     }
@@ -685,7 +695,8 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     for (int i = 0; i < npasses && i < 8; ++i) {
         if (passes[i] == PTX_PASS_GBUFFER) surf_ok = false;
         else if (passes[i] == PTX_PASS_INIT && w.surf) surf_ok = true;
-        else if ((passes[i] == PTX_PASS_TEMPORAL || passes[i] == PTX_PASS_SPATIAL) && w.surf) {
+        else if ((passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalJobs || passes[i] == PTX_PASS_SPATIAL) &&
+                 w.surf) {
             need_surf[i] = !surf_ok;
             surf_ok = true;
         }
@@ -749,7 +760,7 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     }
     // the temporal pass rewrote the reservoirs PT_1's state describes, and summarised them
     for (int i = 0; i < npasses; ++i)
-        if (passes[i] == PTX_PASS_TEMPORAL) {
+        if (passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalCombine) {
             h->init_state_valid = false;
             h->nbr_valid = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
         }
@@ -814,6 +825,8 @@ void swap_frame_ctx(ptx_handle *h) {
     std::swap(h->d_wres0, a.wres0);
     std::swap(h->d_wres1, a.wres1);
     std::swap(h->d_wres2, a.wres2);
+    std::swap(h->d_tjstate, a.tjstate);
+    std::swap(h->d_tjres, a.tjres);
     std::swap(h->d_wact0, a.wact0);
     std::swap(h->d_wact1, a.wact1);
     std::swap(h->d_wctr, a.wctr);
@@ -889,12 +902,15 @@ static int timed_wave_frame(ptx_handle *h) {
         // G-buffer + PT_1 of this frame overlap the previous frame's spatial pass + PT_4; the
         // temporal pass reads that frame's spatial output (d_hist) and shares its job buffers
         if (int rc = reuse_buffers(h)) return rc;
-        static const int front[2] = {PTX_PASS_GBUFFER, PTX_PASS_INIT};
-        static const int temporal[1] = {PTX_PASS_TEMPORAL};
+        // (the temporal pass's shift jobs read only this frame's PT_1 output: they run before the
+        // wait, its combine after; PTX_AB=TEMPORAL_SPLIT=0: the whole pass after the wait)
+        static const bool split = ab_knob("TEMPORAL_SPLIT", 1) != 0;
+        static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, kPassTemporalJobs};
+        static const int temporal[1] = {PTX_PASS_TEMPORAL}, temporal_b[1] = {kPassTemporalCombine};
         static const int back[2] = {PTX_PASS_SPATIAL, PTX_PASS_FINAL};
-        e = launch_wave_parts(h, sc, w, front, 2);
+        e = launch_wave_parts(h, sc, w, front, split ? 3 : 2);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
-        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, temporal, 1);
+        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, split ? temporal_b : temporal, 1);
         if (e == hipSuccess) e = launch_wave_parts(h, sc, w, back, 2);
         if (e == hipSuccess) mark_history(h);
     } else if (has_reuse(h)) {
@@ -1295,7 +1311,7 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
     out->max_bvh_depth = h->max_depth;
     out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
                         h->d_subs.bytes + h->d_insts.bytes + h->d_mats.bytes + h->d_tverts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
-                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_nbr.bytes + h->d_surf.bytes + h->d_direct.bytes;
+                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_tjstate.bytes + h->d_tjres.bytes + h->d_nbr.bytes + h->d_surf.bytes + h->d_direct.bytes;
     return PTX_OK;
 }
 
@@ -1464,10 +1480,10 @@ int ptx_destroy(ptx_handle *h) {
     for (DevBuf *b : {&h->d_canvas, &h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wres2, &h->d_wact0, &h->d_wact1, &h->d_wctr,
-                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_nbr, &h->d_surf, &h->d_direct, &h->d_census})
+                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_tjstate, &h->d_tjres, &h->d_nbr, &h->d_surf, &h->d_direct, &h->d_census})
         free_buf(*b);
     ptx_handle::FrameCtx &a = h->alt;
-    for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wres2, &a.wact0, &a.wact1, &a.wctr})
+    for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wres2, &a.wact0, &a.wact1, &a.wctr, &a.tjstate, &a.tjres})
         free_buf(*b);
     if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

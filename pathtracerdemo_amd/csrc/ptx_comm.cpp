@@ -186,11 +186,12 @@ int band_front(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *&
     resolve_event(*frame_t, h);
     HIP_CHECK(h, hipEventRecord(frame_t->start, h->stream));
     static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_TEMPORAL};
+    static const int front_split[4] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, kPassTemporalJobs, kPassTemporalCombine};
     hipError_t e;
-    if (pipe) {
-        e = launch_wave_parts(h, sc, w, front, 2);
+    if (pipe) {  // (the temporal jobs before the wait, the temporal combine after: timed_wave_frame)
+        e = launch_wave_parts(h, sc, w, front_split, 3);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
-        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, front + 2, 1);
+        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, front_split + 3, 1);
     } else {
         e = launch_wave_parts(h, sc, w, front, 3);
     }

@@ -25,6 +25,12 @@ struct TimedLaunch {
 
 using namespace ptx;
 
+// Internal pass codes (launch_wave_parts): the temporal pass in two parts -- its shift jobs
+// (start, trace rounds; they read only this frame's PT_1 output) and its combine (reads the
+// previous frame's spatial output) -- so a pipelined frame runs the jobs before waiting for
+// the previous frame.
+constexpr int kPassTemporalJobs = 0x100, kPassTemporalCombine = 0x101;
+
 struct ptx_handle {
     ptx_config cfg{};
     int device = 0;
@@ -50,6 +56,9 @@ struct ptx_handle {
     DevBuf d_gbuf, d_res, d_accum, d_counters, d_queue;
     // reuse pipeline: spatial output / history, shift-job state and results
     DevBuf d_hist, d_jstate, d_jres, d_nbr;
+    // the temporal pass's shift jobs, per frame context: its jobs run before the previous
+    // frame's spatial pass (which owns d_jstate / d_jres) has finished
+    DevBuf d_tjstate, d_tjres;
     // reservoir size in uint4 (8: the reference's 128-byte Reservoir; 4: the GI reservoir)
     // and the GI pipeline's per-pixel direct light
     uint32_t res_u4 = 8;
@@ -92,7 +101,7 @@ struct ptx_handle {
     // ptx_render swaps the members above with `alt` per frame, so everything else always sees
     // the latest frame's buffers; the shared ones (accumulation, history, jobs, scene) never move.
     struct FrameCtx {
-        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wres2, wact0, wact1, wctr;
+        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wres2, wact0, wact1, wctr, tjstate, tjres;
         size_t wave_ray_cap = 0;
         uint32_t wave_slots = 0;
         hipStream_t stream = nullptr;

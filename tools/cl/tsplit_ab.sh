@@ -1,0 +1,8 @@
+# the temporal pass split around the previous-frame wait (its shift jobs before, its combine
+# after; per-context temporal job buffers): GPU suite, then same-box A/B against
+# PTX_AB=TEMPORAL_SPLIT=0 on the headline (3 reps) and the furnished scene
+set -o pipefail
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/tsplit_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/tsplit_tests.log; exit 1; }
+tail -1 gpurun_out/tsplit_tests.log
+AB=$'PTX_AB=\nPTX_AB=TEMPORAL_SPLIT=0' REPS=3 TAG=ab_tsplit BENCH_ARGS="--no-configs3" bash tools/ab_env.sh || exit 1
+AB=$'PTX_AB=\nPTX_AB=TEMPORAL_SPLIT=0' REPS=1 TAG=ab_tsplit_f BENCH_ARGS="--no-configs3 --scene c3_furnished" bash tools/ab_env.sh || exit 1
