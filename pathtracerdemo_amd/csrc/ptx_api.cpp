@@ -795,9 +795,11 @@ bool pipelined(const ptx_handle *h) {
     static const bool bands_off = ab_knob("PIPELINE_BANDS", 1) == 0;
     const uint32_t fl = h->cfg.flags;
     const bool band = h->comm || h->halo_top || h->halo_bot;
-    // at most ~4 Mpx per frame: a 3840x2160 frame's launches are large enough to fill the chip
-    // on their own (configs[3] on one GPU: 384 Msamples/s unpipelined, 355 pipelined)
-    static const size_t max_px = (size_t)ab_knob("PIPE_MAX_KPX", 4096) << 10;  // A/B
+    // up to 16 Mpx per frame.  (Round 2 capped it at 4 Mpx -- configs[3]'s 3840x2160 frame on one
+    // GPU then measured 384 Msamples/s unpipelined, 355 pipelined; with the temporal jobs ahead of
+    // the previous-frame wait and the light segments folded into the combines, same box: 465.7
+    // unpipelined, 474.9 pipelined.)  PTX_AB=PIPE_MAX_KPX=<n>: A/B
+    static const size_t max_px = (size_t)ab_knob("PIPE_MAX_KPX", 16384) << 10;
     const size_t px = (size_t)h->band_h * h->cfg.width;
     return !off && !(band && bands_off) && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE &&
            px <= max_px &&

@@ -248,8 +248,8 @@ def test_c3_full_hd_reuse_windows_bit_exact(scene3, oracle_mod):
 
 def test_c3_4k_one_handle_windows_bit_exact(scene3, oracle_mod):
     """configs[3]'s frame on ONE handle -- C3, 3840x2160, reuse pipeline, 2 frames with history --
-    under the 4K launch parameters (above 4 Mpx per band: trace at 5 waves per SIMD, frames not
-    pipelined) vs the oracle on 3 row windows: the top edge, rows straddling the cut at row 1081
+    under the 4K launch parameters (above 4 Mpx per band: trace at 5 waves per SIMD; frames
+    pipelined, two in flight) vs the oracle on 3 row windows: the top edge, rows straddling the cut at row 1081
     of a cost-balanced 8-band split (and the 2-band cut at 1080), and the bottom edge.  The
     8-band tests (test_gpu_bands.py) compare bands with this one handle."""
     O, W, H, R = oracle_mod, 3840, 2160, 30
