@@ -357,7 +357,7 @@ int build_layout(ptx_handle *h) {
     if ((size_t)h->stack_depth * kBlock * 4u > 160u * 1024u)
         return fail(h, PTX_E_SCENE, "BLAS depth %u needs more LDS than a CU has", max_depth);
     h->layout_valid = true;
-    h->surf_valid = h->alt.surf_valid = false;  // the surface records name the old layout's materials
+    h->surf_valid = h->alt.surf_valid = h->alt2.surf_valid = false;  // the surface records name the old layout's materials
     return PTX_OK;
 }
 
@@ -805,18 +805,32 @@ bool pipelined(const ptx_handle *h) {
            px <= max_px &&
            !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK |
                    PTX_FLAG_TIME_LAUNCHES | PTX_FLAG_SINGLE_STREAM | PTX_FLAG_ROW_CENSUS)) &&
-           (h->alt_active ? h->stream == h->alt_stream : h->stream == h->own_stream);
+           h->stream == (h->ctx_idx == 0 ? h->own_stream : h->ctx_idx == 1 ? h->alt_stream : h->alt2_stream);
+}
+int pipe_depth() {
+    static const int d = ab_knob("PIPE_DEPTH", 2) == 3 ? 3 : 2;
+    return d;
 }
 int quiesce(ptx_handle *h) {
-    for (hipStream_t q : {h->stream, h->alt.stream})
+    for (hipStream_t q : {h->stream, h->alt.stream, h->alt2.stream})
         if (q) HIP_CHECK(h, hipStreamSynchronize(q));
     for (int k = 1; k < ptx_handle::kMaxSplit; ++k) {
         if (h->sub[k]) HIP_CHECK(h, hipStreamSynchronize(h->sub[k]));
         if (h->alt.sub[k]) HIP_CHECK(h, hipStreamSynchronize(h->alt.sub[k]));
+        if (h->alt2.sub[k]) HIP_CHECK(h, hipStreamSynchronize(h->alt2.sub[k]));
     }
     return PTX_OK;
 }
+static void swap_two(ptx_handle *h);
+// The next context (round robin over pipe_depth() contexts): the members become the next
+// context's, `alt` (and `alt2`) the ones after it.
 void swap_frame_ctx(ptx_handle *h) {
+    swap_two(h);
+    if (pipe_depth() == 3) std::swap(h->alt, h->alt2);
+    h->ctx_idx = (h->ctx_idx + 1) % pipe_depth();
+    h->alt_active = h->ctx_idx != 0;
+}
+static void swap_two(ptx_handle *h) {
     ptx_handle::FrameCtx &a = h->alt;
     std::swap(h->d_gbuf, a.gbuf);
     std::swap(h->d_res, a.res);
@@ -843,25 +857,35 @@ void swap_frame_ctx(ptx_handle *h) {
     std::swap(h->init_state_valid, a.init_state_valid);
     std::swap(h->nbr_valid, a.nbr_valid);
     std::swap(h->surf_valid, a.surf_valid);
-    h->alt_active = !h->alt_active;
 }
 // the second context's G-buffer, reservoirs and stream (its queues, wave state and summaries
 // are allocated by wave_buffers / reuse_buffers on its first frame)
 int ensure_alt(ptx_handle *h) {
-    ptx_handle::FrameCtx &a = h->alt;
-    if (!h->alt_stream) {
+    if (!h->alt_stream) {  // (called with the first context in the members: alt is the second)
         HIP_CHECK(h, hipStreamCreateWithFlags(&h->alt_stream, hipStreamNonBlocking));
-        a.stream = h->alt_stream;
+        h->alt.stream = h->alt_stream;
+    }
+    if (pipe_depth() == 3 && !h->alt2_stream) {
+        HIP_CHECK(h, hipStreamCreateWithFlags(&h->alt2_stream, hipStreamNonBlocking));
+        h->alt2.stream = h->alt2_stream;
     }
     if (!h->ev_prev) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_prev, hipEventDisableTiming));
-    DevBuf &g = h->alt_active ? h->d_gbuf : a.gbuf, &r = h->alt_active ? h->d_res : a.res;
-    if (!g.p) {
-        if (int rc = alloc_buf(h, g, h->d_gbuf.bytes ? h->d_gbuf.bytes : a.gbuf.bytes)) return rc;
-        HIP_CHECK(h, memset_sync(h, g.p, 0, g.bytes));
+    // every context's G-buffer and reservoirs (the other buffers come with its first frame)
+    DevBuf *gs[3] = {&h->d_gbuf, &h->alt.gbuf, &h->alt2.gbuf}, *rs[3] = {&h->d_res, &h->alt.res, &h->alt2.res};
+    size_t gbytes = 0, rbytes = 0;
+    for (int c = 0; c < 3; ++c) {
+        gbytes = std::max(gbytes, gs[c]->bytes);
+        rbytes = std::max(rbytes, rs[c]->bytes);
     }
-    if (!r.p) {
-        if (int rc = alloc_buf(h, r, h->d_res.bytes ? h->d_res.bytes : a.res.bytes)) return rc;
-        HIP_CHECK(h, memset_sync(h, r.p, 0, r.bytes));
+    for (int c = 0; c < pipe_depth(); ++c) {
+        if (!gs[c]->p) {
+            if (int rc = alloc_buf(h, *gs[c], gbytes)) return rc;
+            HIP_CHECK(h, memset_sync(h, gs[c]->p, 0, gs[c]->bytes));
+        }
+        if (!rs[c]->p) {
+            if (int rc = alloc_buf(h, *rs[c], rbytes)) return rc;
+            HIP_CHECK(h, memset_sync(h, rs[c]->p, 0, rs[c]->bytes));
+        }
     }
     return PTX_OK;
 }
@@ -869,7 +893,7 @@ int ensure_alt(ptx_handle *h) {
 int leave_alt(ptx_handle *h) {
     if (!h->alt_active) return PTX_OK;
     if (int rc = quiesce(h)) return rc;
-    swap_frame_ctx(h);
+    while (h->ctx_idx != 0) swap_frame_ctx(h);
     return PTX_OK;
 }
 
@@ -1123,7 +1147,7 @@ int ptx_upload_scene(ptx_handle *h, const uint32_t *scene, size_t n_scene, const
     h->hist_valid = false;
     h->init_state_valid = false;
     h->nbr_valid = false;
-    h->surf_valid = h->alt.surf_valid = false;
+    h->surf_valid = h->alt.surf_valid = h->alt2.surf_valid = false;
     if (h->frame_set) return build_layout(h);
     return PTX_OK;
 }
@@ -1469,7 +1493,7 @@ int ptx_destroy(ptx_handle *h) {
     (void)quiesce(h);
     if (h->xstream) (void)hipStreamSynchronize(h->xstream);
     comm_destroy(h);
-    if (h->alt_active) swap_frame_ctx(h);
+    while (h->ctx_idx != 0) swap_frame_ctx(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (hipStream_t q : h->sub)
         if (q) (void)hipStreamSynchronize(q);
@@ -1484,15 +1508,19 @@ int ptx_destroy(ptx_handle *h) {
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wres2, &h->d_wact0, &h->d_wact1, &h->d_wctr,
                       &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_tjstate, &h->d_tjres, &h->d_nbr, &h->d_surf, &h->d_direct, &h->d_census})
         free_buf(*b);
-    ptx_handle::FrameCtx &a = h->alt;
-    for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wres2, &a.wact0, &a.wact1, &a.wctr, &a.tjstate, &a.tjres})
-        free_buf(*b);
-    if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
-    for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {
-        if (a.ev_join[q]) (void)hipEventDestroy(a.ev_join[q]);
-        if (a.sub[q]) (void)hipStreamDestroy(a.sub[q]);
+    for (ptx_handle::FrameCtx *ap : {&h->alt, &h->alt2}) {
+        ptx_handle::FrameCtx &a = *ap;
+        for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wres2, &a.wact0, &a.wact1,
+                          &a.wctr, &a.tjstate, &a.tjres})
+            free_buf(*b);
+        if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
+        for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {
+            if (a.ev_join[q]) (void)hipEventDestroy(a.ev_join[q]);
+            if (a.sub[q]) (void)hipStreamDestroy(a.sub[q]);
+        }
     }
     if (h->alt_stream) (void)hipStreamDestroy(h->alt_stream);
+    if (h->alt2_stream) (void)hipStreamDestroy(h->alt2_stream);
     if (h->ev_prev) (void)hipEventDestroy(h->ev_prev);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

@@ -108,9 +108,10 @@ struct ptx_handle {
         hipStream_t sub[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
         hipEvent_t ev_fork = nullptr, ev_join[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
         bool init_state_valid = false, nbr_valid = false, surf_valid = false;
-    } alt;
-    bool alt_active = false;      // the members above hold the second context (stream == alt stream)
-    hipStream_t alt_stream = nullptr;  // the second context's stream (owned)
+    } alt, alt2;  // (alt2: the third context when pipe_depth() == 3; swap_frame_ctx rotates)
+    bool alt_active = false;      // the members above hold a context other than the first
+    int ctx_idx = 0;              // which context the members above hold (0: own_stream's)
+    hipStream_t alt_stream = nullptr, alt2_stream = nullptr;  // the other contexts' streams (owned)
     hipEvent_t ev_prev = nullptr;
     // multi-GPU (ptx_comm.cpp): the RCCL communicator this handle owns (ncclComm_t), its
     // rank and world; the halo exchange stream and its fork / done events
@@ -168,6 +169,8 @@ bool pipelined(const ptx_handle *h);
 int quiesce(ptx_handle *h);
 // the second frame context's G-buffer, reservoirs and stream; swap the two contexts
 int ensure_alt(ptx_handle *h);
+// frames in flight when pipelined: 2, or 3 with PTX_AB=PIPE_DEPTH=3 (A/B)
+int pipe_depth();
 void swap_frame_ctx(ptx_handle *h);
 // back to the first frame context (quiesce + swap) before the handle's stream or mode changes
 int leave_alt(ptx_handle *h);

@@ -1,7 +1,7 @@
 """Wave occupancy of one reuse frame, from the diagnostic build's per-wave timing records.
 
 usage (GPU box):  make -C pathtracerdemo_amd/csrc wgt
-                  PTX_WGT=1 PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_wgt.so python tools/wave_timeline.py [--out f.json]
+                  PTX_AB=WGT PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_wgt.so python tools/wave_timeline.py [--out f.json]
 Every instrumented kernel's waves log {start, end} on the 100 MHz real-time clock
 (PTX_WAVE_TIMER, ptx_device.h).  Prints, over the frame: the resident-wave count per
 kernel kind in 20 us bins (the chip holds 256 CUs x 4 SIMDs x the kernel's waves/SIMD), the
@@ -30,8 +30,8 @@ def main():
     ap.add_argument("--bin-us", type=float, default=20.0)
     ap.add_argument("--frames", type=int, default=1, help="frames in the measured window (pipelined frames overlap)")
     a = ap.parse_args()
-    assert os.environ.get("PTX_WGT") == "1" and "wgt" in os.environ.get("PTX_LIB_PATH", ""), \
-        "run with PTX_WGT=1 PTX_LIB_PATH=<libptx_wgt.so>"
+    assert "WGT" in os.environ.get("PTX_AB", "") and "wgt" in os.environ.get("PTX_LIB_PATH", ""), \
+        "run with PTX_AB=WGT PTX_LIB_PATH=<libptx_wgt.so>"
     from pathtracerdemo_amd import _native as N
     from pathtracerdemo_amd.renderer import Renderer
     from pathtracerdemo_amd.scene.world import compile_scene
