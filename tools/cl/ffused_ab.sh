@@ -1,0 +1,8 @@
+# PT_4 folded into the spatial combine (shading where no replay is needed) and the next frame's
+# temporal combine waiting for the spatial sequences only: GPU suite (+ debug fill), then same-box
+# A/B against PTX_AB=FINAL_FUSED=0 on the headline (3 reps) and the furnished scene
+set -o pipefail
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/ffused_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/ffused_tests.log; exit 1; }
+tail -1 gpurun_out/ffused_tests.log
+AB=$'PTX_AB=\nPTX_AB=FINAL_FUSED=0' REPS=3 TAG=ab_ffused BENCH_ARGS="--no-configs3" bash tools/ab_env.sh || exit 1
+AB=$'PTX_AB=\nPTX_AB=FINAL_FUSED=0' REPS=1 TAG=ab_ffused_f BENCH_ARGS="--no-configs3 --scene c3_furnished" bash tools/ab_env.sh || exit 1
