@@ -61,6 +61,15 @@ DEFAULT_SCENE = {"reuse": "c3_interior_32", "restir": "dummy_scene_1", "mcpt": "
                  "gi": "c3_interior_32"}
 
 
+def ab_knob(key, dflt):
+    """PTX_AB's value for `key` as the library reads it (ptx_api.cpp ab_knob): "K" -> 1, "K=v" -> v."""
+    for item in os.environ.get("PTX_AB", "").split(","):
+        k, eq, v = item.partition("=")
+        if k == key:
+            return int(v) if eq else 1
+    return dflt
+
+
 def ray_bytes(c: dict) -> int:
     return B_AABB * c["aabb_tests"] + B_TRI * c["tri_tests"] + B_INST * c["instance_xforms"] + B_HIT * c["hits"]
 
@@ -383,6 +392,10 @@ def main():
         # duration is the HIP-event average over the timed region.
         dom = "trace_queue"
         traced = [p for p in passes if p != "gbuffer"]
+        if pipeline == "reuse" and ab_knob("FINAL_ONE", 1):
+            # the reuse pipeline's PT_4 walks its replays inside its one logic kernel (wfinal_one):
+            # none of its queries reach trace_queue
+            traced = [p for p in traced if p != "final"]
         work = {k: sum(counts[p][k] for p in traced) for k in counts[traced[0]]}
         per_frame = n_trace / args.steps
         dom_bytes = (ray_bytes(work) + 64 * work["rays"]) / per_frame

@@ -608,6 +608,15 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
     }
     // the reuse pipeline's PT_4 reads the spatial output
     const uint4 *fres = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? (const uint4 *)h->d_hist.p : res;
+    // the reuse pipeline's PT_4: one launch, replays inline (PTX_AB=FINAL_ONE=0: the queued rounds)
+    static const bool final_one = ab_knob("FINAL_ONE", 1) != 0;
+    if (pass == PTX_PASS_FINAL && final_one && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && tables_fit_lds(sc)) {
+        TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
+        e = wave_final_one(sc, w, gb, fres, (float4 *)h->d_accum.p, h->stack_depth, st);
+        event_end(t, st);
+        h->init_state_valid = false;  // (its queue slots are rewritten, as by the queued form)
+        return e;
+    }
     // PT_1 fills the wave state the temporal pass may read; PT_4 / MCPT reuse those slots
     h->init_state_valid = pass == PTX_PASS_INIT && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
     const int rounds = pass == PTX_PASS_INIT ? kWaveRoundsInit : pass == PTX_PASS_FINAL ? kWaveRoundsFinal

@@ -91,6 +91,9 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mod
                       hipStream_t s, bool occ_only = false);
 hipError_t wave_init_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, uint4 *reservoir,
                            hipStream_t s);
+// PT_4 of the reuse pipeline in one launch, replays walked inline (scene tables in LDS)
+hipError_t wave_final_one(const Scene &sc, const WaveBufs &w, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
+                          uint32_t depth, hipStream_t s);
 hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const uint4 *gbuf, const uint4 *reservoir,
                             float4 *accum, hipStream_t s);
 hipError_t wave_gbuffer(const Scene &sc, const WaveBufs &w, uint4 *gbuf, uint32_t stack_depth, hipStream_t s);

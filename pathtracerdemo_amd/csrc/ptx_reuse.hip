@@ -209,7 +209,7 @@ __device__ __forceinline__ void job_finish(const Seg &g, const JobLists &JL, con
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
 void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
-    PTX_WAVE_TIMER(sc, KID_JOB_STEP);
+    PTX_WAVE_TIMER(sc, KID_JOB_STEP | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
@@ -352,7 +352,7 @@ __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBu
 // (the inlined replay needs more registers than the 4-wave budget: 160 B/lane spilled there)
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(2, 8)))
 void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
-    PTX_WAVE_TIMER(sc, KID_TEMP_START);
+    PTX_WAVE_TIMER(sc, KID_TEMP_START | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
@@ -376,7 +376,7 @@ void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
 // Temporal resampling of the pixel's PT_1 reservoir with the previous frame's output at
 // the same pixel (oracle temporal_pixel): static camera, identity shift.
 __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, ReuseArgs A) {
-    PTX_WAVE_TIMER(sc, KID_TEMP_COMBINE);
+    PTX_WAVE_TIMER(sc, KID_TEMP_COMBINE | (w.seg_base ? 0x80u : 0u));
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
     for (uint32_t k = 0; k < w.seg_px; k += WB) {
         const uint32_t q = seg_pixel(w, j, k);
@@ -490,7 +490,7 @@ constexpr uint32_t kMaxPrefetch = 3u;  // neighbours whose data wspatial_start g
 #endif
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(SPATIAL_START_WAVES, 8)))
 void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
-    PTX_WAVE_TIMER(sc, KID_SPAT_START);
+    PTX_WAVE_TIMER(sc, KID_SPAT_START | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
@@ -729,7 +729,7 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
 // the 128-byte output reservoir is written 32 bytes per lane.  Bit-identical to combine_pixel.
 constexpr uint32_t kShflLanes = 4u;  // lanes per pixel (M + 1 with M = 3)
 __global__ __launch_bounds__(WB) void wspatial_combine_shfl(Scene sc, WaveBufs w, ReuseArgs A) {
-    PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE);
+    PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE | (w.seg_base ? 0x80u : 0u));
     constexpr uint32_t M = 3u;
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
     const uint32_t lane = __lane_id(), r = lane & 3u, base = lane & ~3u;
@@ -818,7 +818,7 @@ __global__ __launch_bounds__(WB) void wspatial_combine_shfl(Scene sc, WaveBufs w
 }
 
 __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, ReuseArgs A) {
-    PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE);
+    PTX_WAVE_TIMER(sc, KID_SPAT_COMBINE | (w.seg_base ? 0x80u : 0u));
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
     for (uint32_t k = 0; k < w.seg_px; k += WB) {
         const uint32_t q = seg_pixel(w, j, k);

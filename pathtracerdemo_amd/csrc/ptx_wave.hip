@@ -141,7 +141,7 @@ __device__ __forceinline__ void dyn_prefix(const WaveBufs &w, uint32_t round, ui
 template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true, bool OCC = false, bool FLAT = false>
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
-    PTX_WAVE_TIMER(sc, KID_TRACE);
+    PTX_WAVE_TIMER(sc, KID_TRACE | (w.seg_base ? 0x80u : 0u));
     // dynamic LDS: [scene tables (LDS_TABLES)] [batch prefix (dynamic batches)] [stacks]
     extern __shared__ __attribute__((aligned(16))) uint32_t wstack[];
     const bool dyn = !COUNT && w.dyn != nullptr;
@@ -581,7 +581,7 @@ __device__ __forceinline__ void winit_finish(const WInit &s, uint4 *reservoir, u
 }
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void winit_start(Scene sc, WaveBufs w, const uint4 *gbuf, uint4 *reservoir) {
-    PTX_WAVE_TIMER(sc, KID_INIT_START);
+    PTX_WAVE_TIMER(sc, KID_INIT_START | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
@@ -624,7 +624,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
 }
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void winit_step(Scene sc, WaveBufs w, uint32_t round, uint4 *reservoir) {
-    PTX_WAVE_TIMER(sc, KID_INIT_STEP);
+    PTX_WAVE_TIMER(sc, KID_INIT_STEP | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
@@ -767,6 +767,7 @@ __device__ __forceinline__ void wfinal_store(float4 *state, uint32_t npix, uint3
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wfinal_start(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir,
                                                    float4 *accum) {
+    PTX_WAVE_TIMER(sc, KID_FINAL_START | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
@@ -814,6 +815,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
 
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wfinal_step(Scene sc, WaveBufs w, uint32_t round, const uint4 *reservoir,
                                                   float4 *accum) {
+    PTX_WAVE_TIMER(sc, KID_FINAL_STEP | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
@@ -865,6 +867,104 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
         job_keep(g, JL, emit, emit && s.phase != 0u, pix);
     }
     job_seg_end(w, g, JL);
+}
+
+// PT_4 of the reuse pipeline as ONE launch.  Its pixels almost all carry their sample's stored
+// contribution (the spatial combine's), so wfinal_start shades them and the three {trace, step}
+// rounds after it replay next to nothing -- six dependent launches of ~10 us dispatch gap each on
+// the frame's critical path.  Here the replays run inline: each wave's live pixels emit their
+// ray into their own queue slot, the whole wave walks it (trace_batch, every lane, the
+// traversal kernel's code), and the step consumes it -- the same rays, results and arithmetic as
+// wfinal_emit / trace_queue / wfinal_step, so the frame is bit-identical.
+template <bool FLAT>
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(2, 8)))
+void wfinal_one(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir, float4 *accum, PassEps eps) {
+    PTX_WAVE_TIMER(sc, KID_FINAL_START | (w.seg_base ? 0x80u : 0u));
+    extern __shared__ __attribute__((aligned(16))) uint32_t wstack[];
+    __shared__ unsigned long long c_key[WB];
+    __shared__ uint32_t c_mark[WB];
+    const LdsTables T = stage_tables(sc, wstack);
+    uint32_t *stack = wstack + tables_lds_bytes(sc) / 4u + threadIdx.x;
+    const CoopLds coop{c_key + (threadIdx.x & ~63u), c_mark + (threadIdx.x & ~63u)};
+    const uint32_t j = w.seg_base + blockIdx.x, pj = w.seg_phys + j, np = padded_pixels(sc);
+    // this thread's queue slot (the segment's first WB ray / result slots)
+    float4 *rays = w.rays + 2u * (size_t)pj * w.ray_stride, *res = w.res[0] + 2u * (size_t)pj * w.ray_stride;
+    const uint32_t slot = threadIdx.x;
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {  // (workgroup-uniform)
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y, pix = 0u;
+        bool active = false;
+        WFinal s;
+        if (q < np && tile_xy(sc, q, x, y)) {  // wfinal_start's cases
+            pix = (y - sc.row_begin) * sc.width + x;
+            const Compact x1 = gdecode(gbuf[pix]);
+            const uint4 *rv = reservoir + 8u * (size_t)pix;
+            if (!x1.valid) {
+                accum[pix] = make_float4(ENV_C, ENV_C, ENV_C, 1.0f);
+            } else {
+                const uint4 r0 = rv[0], r5 = rv[5], r7 = rv[7];
+                s.length = r5.w;
+                if (r7.y == 0u || s.length < 2u) {
+                    mix_color(sc, accum, pix, mk(0.0f, 0.0f, 0.0f));
+                } else if (r7.w == 1u) {
+                    const uint4 r6 = rv[6];
+                    mix_color(sc, accum, pix, mk(asf(r6.z), asf(r6.w), asf(r7.z)) * asf(r7.x));
+                } else {
+                    active = true;
+                    s.seed1 = r0.y;
+                    s.ucw = asf(r7.x);
+                    s.prev = x0_of(sc, x, y);
+                    s.cur = get_surface(sc, x1);
+                    s.f = mk(1.0f, 1.0f, 1.0f);
+                    s.i = 1u;
+                }
+            }
+        }
+        const uint4 *resv = reservoir + 8u * (size_t)pix;
+        // (wave-uniform) one replayed vertex per iteration, as many as the queued form's trace
+        // rounds: a path needing more is dropped there, so it is here
+        for (uint32_t it = 0u; it < (uint32_t)kWaveRoundsFinal; ++it) {
+            if (__ballot(active) == 0ull) break;
+            if (active) {  // wfinal_emit, into this thread's slot
+                const f3 V = normalize(s.prev - s.cur.pos);
+                if (s.i + 1u < s.length) {
+                    uint32_t seed = s.i == 1u ? resv[0].x : s.seed1;
+                    uint32_t lobe;
+                    const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
+                    s.phase = 0u;
+                    put_ray(rays, slot, s.cur.pos, dir, -1.0f, Q_CLOSEST);
+                } else {
+                    const LightSample XL = load_xl(resv);
+                    const f3 L = direction_to_light(s.cur, XL);
+                    s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+                    const f3 Le = l_emit<true>(XL, s.cur);
+                    s.phase = 1u;
+                    const float dist = length(XL.pos - s.cur.pos);
+                    put_ray(rays, slot, s.cur.pos, (XL.pos - s.cur.pos) / dist, dist, Q_VIS);
+                    res[2u * slot] = make_float4(0.0f, Le.x, Le.y, Le.z);
+                }
+            }
+            // the traversal kernel's walk, every lane of the wave (idle ones with a NaN bound)
+            trace_batch<false, false, false, true, FLAT>(sc, T.subs, T.insts, eps, stack, coop, rays, res, slot, active);
+            if (active) {  // wfinal_step
+                if (s.phase == 0u) {
+                    const Hit h = get_hit(res, slot);
+                    const Surface next = h.valid ? surface_at(sc, h.s, h.pos) : get_surface(sc, h.s);
+                    const f3 V = normalize(s.prev - s.cur.pos);
+                    const f3 L = normalize(next.pos - s.cur.pos);
+                    s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+                    s.prev = s.cur.pos;
+                    s.cur = next;
+                    s.i += 1u;
+                } else {
+                    const float4 a = res[2u * slot];
+                    s.f = s.f * (mk(a.y, a.z, a.w) * a.x);
+                    mix_color(sc, accum, pix, s.f * s.ucw);
+                    active = false;
+                }
+            }
+        }
+    }
 }
 
 // =========================================================================== TEST_MCPT
@@ -1164,6 +1264,18 @@ hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const
         hipLaunchKernelGGL(wfinal_start, dim3(w.seg_count), dim3(WB), 0, s, sc, w, gbuf, reservoir, accum);
     else
         hipLaunchKernelGGL(wfinal_step, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, reservoir, accum);
+    return hipGetLastError();
+}
+
+hipError_t wave_final_one(const Scene &sc, const WaveBufs &w, const uint4 *gbuf, const uint4 *reservoir, float4 *accum,
+                          uint32_t depth, hipStream_t s) {
+    const PassEps eps{1e-4f, 1e-8f};  // (wave_trace's eps_mode 1, every wavefront pass)
+    const size_t lds = tables_lds_bytes(sc) + stack_lds_bytes(depth);
+    static const uint32_t flat_min = (uint32_t)ab_knob("FLAT_MIN_INST", (int)kFlatMinInstances);
+    if (PTX_FLAT_INST && sc.n_inst >= flat_min)
+        hipLaunchKernelGGL(wfinal_one<true>, dim3(w.seg_count), dim3(WB), lds, s, sc, w, gbuf, reservoir, accum, eps);
+    else
+        hipLaunchKernelGGL(wfinal_one<false>, dim3(w.seg_count), dim3(WB), lds, s, sc, w, gbuf, reservoir, accum, eps);
     return hipGetLastError();
 }
 

@@ -54,9 +54,12 @@ def main():
     s = (rec[:, 0] - t0).astype(np.float64) / 100.0  # us
     e = (rec[:, 1] - t0).astype(np.float64) / 100.0
     kid = (rec[:, 2] >> np.uint64(32)).astype(int)
+    seq = kid >> 7  # (second launch sequence of a pipelined frame's back: kid | 0x80)
+    kid = kid & 0x7f
     span = e.max()
     nb = int(np.ceil(span / a.bin_us))
     occ = {}
+    seqocc = {}
     for k in sorted(set(kid)):
         o = np.zeros(nb)
         for si, ei in zip(s[kid == k], e[kid == k]):
@@ -68,6 +71,21 @@ def main():
                 o[b0 + 1:b1] += 1.0
                 o[b1] += ei / a.bin_us - b1
         occ[KIDS.get(k, str(k))] = o
+    for k in sorted(set(kid)):  # per launch sequence of the back (0 / 1)
+        for q in (0, 1):
+            m = (kid == k) & (seq == q)
+            if not m.any() or not (seq[kid == k] == 1).any():
+                continue
+            o = np.zeros(nb)
+            for si, ei in zip(s[m], e[m]):
+                b0, b1 = int(si // a.bin_us), int(min(ei, span - 1e-9) // a.bin_us)
+                if b0 == b1:
+                    o[b0] += (ei - si) / a.bin_us
+                else:
+                    o[b0] += (b0 + 1 - si / a.bin_us)
+                    o[b0 + 1:b1] += 1.0
+                    o[b1] += ei / a.bin_us - b1
+            seqocc[f"{KIDS.get(k, str(k))}.{q}"] = o
     total = sum(occ.values())
     print(f"{a.frames} frame(s): span {span:.1f} us, {n} waves; mean resident waves {total.mean():.0f} "
           f"(chip: 1024 SIMDs; trace kernel 4/SIMD = 4096)")
@@ -84,6 +102,7 @@ def main():
         print(f"  {b*a.bin_us:7.0f} us  T {tr[b]:6.0f}  L {lg[b]:6.0f}  " + "#" * int(tr[b] / 64) + "." * int(lg[b] / 64))
     if a.out:
         json.dump({"span_us": span, "bin_us": a.bin_us, "occupancy": {k: v.tolist() for k, v in occ.items()},
+                   "occupancy_by_sequence": {k: v.tolist() for k, v in seqocc.items()},
                    "records": rec.astype(np.int64).tolist() if n < 400000 else None}, open(a.out, "w"))
 
 
