@@ -526,6 +526,9 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.jres = (float4 *)(temporal ? h->d_tjres.p : h->d_jres.p);
     A.jpp = temporal ? 1u : 2u * h->reuse_neighbors;
     A.njobs = h->band_h * h->cfg.width * A.jpp;
+    static const bool planes = ab_knob("JOB_PLANES", 1) != 0;  // A/B: 0 = pixel-major job ids
+    A.jpx = planes ? 1u : A.jpp;
+    A.jslot = planes ? h->band_h * h->cfg.width : 1u;
     A.radius = h->reuse_radius;
     A.neighbors = h->reuse_neighbors;
     A.cap = h->temporal_cap;

@@ -110,6 +110,10 @@ struct ReuseArgs {
     float4 *jstate;     // shift-job state, 6 float4 slots x njobs (SoA)
     float4 *jres;       // per job: {f (PathContribution, rgb), q} (q = 0: invalid); p_hat = Luminance(f)
     uint32_t njobs, jpp;  // jobs of the pass (npix * jpp), jobs per pixel
+    // job id of (pixel, slot) = pix * jpx + slot * jslot: slot planes (jpx 1, jslot npix), so a
+    // wave's jobs -- one 8x8 tile, one slot -- read and write whole 128-byte lines of the SoA
+    // state (pixel-major, jpx = jpp: 16-byte pieces 16 * jpp bytes apart)
+    uint32_t jpx, jslot;
     uint32_t radius, neighbors, cap, hist_valid;
     uint32_t use_init;  // temporal: this frame's PT_1 wave state (path hits, NEE Visibility) is in w.state
     const uint4 *nbr;   // spatial: per-pixel neighbour summary (wave_reuse_summary), cur's addressing

@@ -48,6 +48,10 @@ struct Job {
     f3 rr_f;
 };
 
+// the spatial pass's job of pixel `pix`, slot `slot` (2m: forward shift from neighbour m, 2m+1: backward)
+__device__ __forceinline__ uint32_t job_id(const ReuseArgs &A, uint32_t pix, uint32_t slot) {
+    return pix * A.jpx + slot * A.jslot;
+}
 __device__ __forceinline__ const uint4 *res_at(const uint4 *base, int32_t idx) { return base + 8 * (ptrdiff_t)idx; }
 
 // A job waiting for its light segment's Visibility (phase 1) only needs HDR and F.
@@ -277,6 +281,10 @@ __device__ __forceinline__ float4 job_result(const ReuseArgs &A, const WaveBufs 
     const bool valid = qv > 0.0f && qv <= 3.402823466e38f;
     return valid ? make_float4(f.x, f.y, f.z, qv) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
+__device__ __forceinline__ float4 job_at(const ReuseArgs &A, const WaveBufs &w, uint32_t pix, uint32_t slot) {
+    const uint32_t jid = job_id(A, pix, slot);
+    return job_result(A, w, A.jres[jid], jid);
+}
 __device__ __forceinline__ SelF stored_f(const uint4 *r) {
     const uint4 r6 = r[6], r7 = r[7];
     return SelF{r7.w == 1u, mk(asf(r6.z), asf(r6.w), asf(r7.z))};
@@ -494,7 +502,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, 0u, lds);
-    const uint32_t np = padded_pixels(sc), jpp = A.jpp, M = A.neighbors;
+    const uint32_t np = padded_pixels(sc), M = A.neighbors;
     for (uint32_t base = 0; base < w.seg_px * 2u; base += WB) {  // workgroup-uniform
         const bool backward = base >= w.seg_px;
         const uint32_t q = seg_pixel(w, g.j, base % w.seg_px);
@@ -541,7 +549,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
             }
         }
         for (uint32_t m = 0; m < M; ++m) {  // uniform
-            const uint32_t jid = pix * jpp + 2u * m + (backward ? 1u : 0u);
+            const uint32_t jid = job_id(A, pix, 2u * m + (backward ? 1u : 0u));
             bool act = false;
             uint32_t s0 = 0u;
             Job s;
@@ -639,7 +647,6 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
     const float Mf = (float)M;
     const CombineCanon c{(float)c7.y, asf(c6.x), asf(c6.y), asf(c7.x), c7.y != 0u && c5.w >= 2u && asf(c6.x) > 0.0f};
     const uint32_t seed0 = reuse_seed(sc, x, y, SALT_SPATIAL);
-    const float4 *jr = A.jres + (size_t)pix * A.jpp;
     uint32_t seed = seed0, Csum = c7.y;
     float sumQ = 0.0f, w_sum = 0.0f, p_sel = c.pc, q_sel = c.qc;
     int32_t src = (int32_t)pix;
@@ -658,8 +665,8 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
 #pragma unroll
         for (uint32_t m = 0; m < MT; ++m) {  // (job results of absent neighbours are never used)
             nv[m] = A.nbr[nid[m]];
-            Fr[m] = job_result(A, w, jr[2u * m], pix * A.jpp + 2u * m);
-            B[m] = job_result(A, w, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u);
+            Fr[m] = job_at(A, w, pix, 2u * m);
+            B[m] = job_at(A, w, pix, 2u * m + 1u);
         }
         Nbr nb[MT];
 #pragma unroll
@@ -695,7 +702,7 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
                 const Nbr nb = nbr_at(A, band_index(sc, nx, ny));
                 if (nb.valid) {
                     Csum += nb.C;
-                    Q = canon_q(c, Mf, nb.C, job_result(A, w, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u));
+                    Q = canon_q(c, Mf, nb.C, job_at(A, w, pix, 2u * m + 1u));
                 }
             }
             sumQ += Q;
@@ -710,7 +717,7 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
             int32_t nidx = 0;
             if (spatial_neighbor(nseed, A.radius, x, y, sc.width, sc.height, nx, ny)) {
                 nidx = band_index(sc, nx, ny);
-                wn = neighbour_weight(c, Mf, nbr_at(A, nidx), job_result(A, w, jr[2u * m], pix * A.jpp + 2u * m), pf,
+                wn = neighbour_weight(c, Mf, nbr_at(A, nidx), job_at(A, w, pix, 2u * m), pf,
                                       qf, fj);
             }
             if (wrs_update(w_sum, wn, seed)) { src = nidx; p_sel = pf; q_sel = qf; f_sel = fj; }
@@ -757,9 +764,8 @@ __global__ __launch_bounds__(WB) void wspatial_combine_shfl(Scene sc, WaveBufs w
             pres = spatial_neighbor(seed, A.radius, x, y, sc.width, sc.height, nx, ny);
             if (pres) nid = band_index(sc, nx, ny);
             const uint4 nv = A.nbr[nid];
-            const float4 *jr = A.jres + (size_t)pix * A.jpp;
-            Fr = job_result(A, w, jr[2u * m], pix * A.jpp + 2u * m);
-            B = job_result(A, w, jr[2u * m + 1u], pix * A.jpp + 2u * m + 1u);
+            Fr = job_at(A, w, pix, 2u * m);
+            B = job_at(A, w, pix, 2u * m + 1u);
             nb = nv.w != kNbrEscape ? Nbr{(nv.w >> 31) != 0u, (nv.w >> 24) & 0x7fu, nv.w & 0xffffffu, asf(nv.x),
                                           asf(nv.y), asf(nv.z)}
                                     : nbr_at(A, nid);
