@@ -1201,11 +1201,15 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
     else {
         // Occupancy target per pipeline (WaveBufs::trace_waves), LDS-staged tables; A/B
         // switches PTX_AB=TRACE_OCC=n / TRACE_NOLDS.  Measured at 1080p with 768-pixel segments:
-        // 4 waves/SIMD (no spill) is fastest for every pipeline (with the flat node loop: reuse
-        // 369-373 vs 339-340, ReSTIR 1301 vs 1235, TEST_MCPT 1359 vs 1261, GI 720 vs 714 at 5,
-        // which spills 48-64 B/lane); 5 only for bands above 4 Mpx; 6+ spills in the node loop.
+        // 4 waves/SIMD (no spill) is fastest for the per-instance walk (with the flat node loop:
+        // reuse 369-373 vs 339-340, ReSTIR 1301 vs 1235, TEST_MCPT 1359 vs 1261 at 5); 5 for
+        // bands above 4 Mpx; 6+ spills in the node loop.  The flattened walk (>= 3 instances)
+        // runs at 5 (96 VGPRs; its 40 B/lane of spills sit at the batch boundaries, none in the
+        // walk): reuse 462.6 vs 446.6, GI 769.6 vs 757.7, furnished C3 301.6 vs 282.2 (same box,
+        // round 3) -- the launch alone is ~3 % slower, the pipelined frame faster: 96-VGPR
+        // waves leave the other frame's logic waves room on the SIMD.
         static const int env_occ = ab_knob("TRACE_OCC", 0);
-        const int occ = env_occ ? env_occ : w.trace_waves == 4u ? 4 : 5;
+        const int occ = env_occ ? env_occ : (w.trace_waves == 4u && !flat) ? 4 : 5;
         static const bool no_lds = ab_knob("TRACE_NOLDS", 0) != 0;
         const bool tables_fit = tables_fit_lds(sc) && !no_lds;
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
