@@ -211,7 +211,13 @@ __device__ __forceinline__ void job_finish(const Seg &g, const JobLists &JL, con
     job_keep(g, JL, live && !fold, live && s.phase != 0u, jid);
 }
 
-__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8)))
+#ifndef JOB_STEP_WAVES
+// 5 waves per SIMD (96 VGPRs, 80 B/lane spilled) beside the 5-wave flattened trace: reuse 464.6
+// vs 461.8 at 4 (3 reps, tools/cl/js5_ab.sh); every start / step kernel at 5 (LOGIC_WAVES):
+// reuse +1.0 %, but ReSTIR -3.2 %, TEST_MCPT -10 % (tools/cl/lw5_ab.sh)
+#define JOB_STEP_WAVES 5
+#endif
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(JOB_STEP_WAVES, 8)))
 void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
     PTX_WAVE_TIMER(sc, KID_JOB_STEP | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
