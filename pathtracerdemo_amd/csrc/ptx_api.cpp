@@ -400,10 +400,20 @@ void resolve_event(TimedLaunch &t, ptx_handle *h) {
 // loop + fresh shift jobs): the reuse pipeline +1.5 % at 1024 (768: 378.1, 1024: 383.7, 1536:
 // 372.0, 2048: 369.3 Msamples/s; 4K ±0); GI -2.5 %, TEST_MCPT -4.4 %, ReSTIR -1.7 % at 1024, so
 // they keep kWaveSegPixels.  PTX_AB=SEG_PX=n: A/B.
+// The reuse pipeline's segment grows with the band: ~1500-3000 segments per frame (the largest
+// power of two from 512 to 4096 with >= 1500 segments), measured late in round 3 with the 5-wave
+// trace (tools/cl/seg_sweep2.sh, seg_sweep3.sh): 1 Mpx bands (configs[3] over 8 GPUs, each band
+// alone) 512 px: summed band time 19.6 vs 21.3 ms at 1024; 1080p 1024 px (466.4 vs 443.7 at 512,
+// 456.7 at 1536); ~4 Mpx bands (2 GPUs) 2048: 8.15 vs 8.35 ms; the 3840x2160 frame on one GPU
+// 4096: 519.1 / 524.6 vs 505.1 / 504.9 at 1024 (2048: 513.4 / 518.5).
 static uint32_t seg_pixels(const ptx_handle *h) {
     static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);
     if (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) return env_px;
-    return h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? 1024u : kWaveSegPixels;
+    if (h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) return kWaveSegPixels;
+    const size_t npx = (size_t)h->band_h * h->cfg.width;
+    uint32_t p = 512u;
+    while (p < 4096u && (size_t)(2u * p) * 1500u <= npx) p *= 2u;
+    return p;
 }
 
 // Wavefront buffers, sized for the largest round: PT_1 emits <= 2 rays per pixel, PT_4
