@@ -562,6 +562,11 @@ static GiArgs gi_args(ptx_handle *h) {
     A.accum = (float4 *)h->d_accum.p;
     A.jray = (uint32_t *)h->d_jres.p;
     A.jpp = 2u * h->reuse_neighbors;
+    // slot planes (as the DI pass's shift jobs, reuse_args): a wave's 64 jobs of one slot write
+    // 256 contiguous bytes instead of 4-byte pieces 4 * jpp bytes apart; PTX_AB=GI_JOB_PLANES=0: A/B
+    static const bool planes = ab_knob("GI_JOB_PLANES", 1) != 0;
+    A.jpx = planes ? 1u : A.jpp;
+    A.jslot = planes ? h->band_h * h->cfg.width : 1u;
     A.radius = h->reuse_radius;
     A.neighbors = h->reuse_neighbors;
     A.cap = h->temporal_cap;

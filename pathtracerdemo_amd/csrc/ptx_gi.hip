@@ -282,6 +282,11 @@ __device__ __forceinline__ bool gi_shift_begin(const GiDomain &d, const GiSample
     return gi_q_ok(q);
 }
 
+// the spatial pass's job (pixel, slot): slot 2m forward from neighbour m, 2m + 1 backward
+__device__ __forceinline__ uint32_t gi_jid(const GiArgs &A, uint32_t pix, uint32_t slot) {
+    return pix * A.jpx + slot * A.jslot;
+}
+
 // The jobs of one pixel of one kind (workgroup-uniform): forward jobs (slot 2m: neighbour
 // m's sample -> this pixel) share this pixel's domain, backward jobs (2m+1: this pixel's
 // sample -> neighbour m) its sample; each job's contribution and q ride in its ray's
@@ -300,7 +305,7 @@ __device__ __forceinline__ void gis_pixel_jobs(const Scene &sc, const Seg &g, co
         if (own_ok) S = gi_sample(sc, rc);
     }
     for (uint32_t m = 0; m < A.neighbors; ++m) {  // uniform
-        const uint32_t jid = pix * A.jpp + 2u * m + (BACKWARD ? 1u : 0u);
+        const uint32_t jid = gi_jid(A, pix, 2u * m + (BACKWARD ? 1u : 0u));
         bool ray = false;
         f3 f{}, o{}, dir{};
         float qv = 0.0f, remain = 0.0f;
@@ -396,8 +401,8 @@ __device__ __forceinline__ void gis_combine_pixel(const Scene &sc, const GiArgs 
             const uint4 *rn = A.cur + 4 * (ptrdiff_t)nid[m];
             gv[m] = A.gbuf[nid[m]].x;
             n1[m] = rn[1]; n2[m] = rn[2]; n3[m] = rn[3];
-            jf[m] = A.jray[pix * A.jpp + 2u * m];
-            jb[m] = A.jray[pix * A.jpp + 2u * m + 1u];
+            jf[m] = A.jray[gi_jid(A, pix, 2u * m)];
+            jb[m] = A.jray[gi_jid(A, pix, 2u * m + 1u)];
         }
         bool valid[MT], hf[MT], hb[MT];
         float pn[MT];
@@ -475,7 +480,7 @@ __device__ __forceinline__ void gis_combine_pixel(const Scene &sc, const GiArgs 
                 Csum += Cn;
                 f3 B;
                 float qB;
-                if (canon_ok && gi_job(A, res, pix * A.jpp + 2u * m + 1u, B, qB)) {
+                if (canon_ok && gi_job(A, res, gi_jid(A, pix, 2u * m + 1u), B, qB)) {
                     const float pbc = luminance(B) * qc / qB;
                     const float den = cc * pc + Mf * (float)Cn * pbc;
                     Q = den > 0.0f ? (cc * pc) / den : 1.0f;
@@ -503,7 +508,7 @@ __device__ __forceinline__ void gis_combine_pixel(const Scene &sc, const GiArgs 
             const uint4 *rn = A.cur + 4 * (ptrdiff_t)nidx;
             const uint4 n1 = rn[1], n2 = rn[2], n3 = rn[3];
             const float pn = luminance(ld3(n3));
-            if (gdecode(A.gbuf[nidx]).valid && pn > 0.0f && gi_job(A, res, pix * A.jpp + 2u * m, F, qF)) {
+            if (gdecode(A.gbuf[nidx]).valid && pn > 0.0f && gi_job(A, res, gi_jid(A, pix, 2u * m), F, qF)) {
                 const float pF = luminance(F);
                 const float J = asf(n3.w) / qF;
                 const float pb = pn / J;

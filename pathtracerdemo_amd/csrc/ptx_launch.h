@@ -155,6 +155,8 @@ struct GiArgs {
     float4 *accum;      // accumulated radiance (band)
     uint32_t *jray;     // spatial: per job its occlusion ray's index, or 0xffffffff (no path)
     uint32_t jpp;       // spatial jobs per pixel (2 * neighbors)
+    uint32_t jpx, jslot;  // job (pixel, slot) at jray[pix * jpx + slot * jslot]: slot planes
+                          // (jpx 1, jslot = band pixels) or pixel-major (jpx = jpp, jslot 1)
     uint32_t radius, neighbors, cap, hist_valid;
 };
 hipError_t wave_gi_round(const Scene &sc, const WaveBufs &w, int pass, int round, const GiArgs &A, hipStream_t s);
