@@ -256,17 +256,32 @@ def main():
     Hb = row_end - row_begin
     reuse = pipeline in ("reuse", "gi")
     use_comm = reuse and world > 1 and args.halo == "rccl"
+    comm_fallback = None  # why the RCCL halo was not used, when rank 0 could not create an id
 
     def make(**kw):
+        nonlocal use_comm, comm_fallback
         r = Renderer(W, H, device=device, pipeline=pipeline, row_begin=row_begin, row_end=row_end,
                      variant=args.variant, halo_overlap=args.halo_overlap, **kw)
         r.Initialize(cs)
         drv = None
         if use_comm:  # the handle's own RCCL communicator: ptx_render exchanges the halo
-            obj = [Renderer.comm_unique_id() if rank == 0 else None]
+            # rank 0 creates the id; if it cannot (no RCCL to open), every rank learns it from
+            # the broadcast and drives the halo over torch.distributed instead -- together, so
+            # no rank waits in a communicator init its peers never join (reported in the line)
+            uid, err = None, None
+            if rank == 0:
+                try:
+                    uid = Renderer.comm_unique_id()
+                except Exception as e:  # noqa: BLE001 -- any failure selects the fallback
+                    err = f"{type(e).__name__}: {e}"
+            obj = [(uid, err)]
             dist.broadcast_object_list(obj, src=0)
-            r.comm_init(obj[0], rank, world)
-        elif reuse and world > 1:
+            uid, err = obj[0]
+            if uid is not None:
+                r.comm_init(uid, rank, world)
+            else:
+                use_comm, comm_fallback = False, err
+        if not use_comm and reuse and world > 1:
             from pathtracerdemo_amd.bands import ReuseBand
             drv = ReuseBand(r, rank, world, device=f"cuda:{device}" if backend == "nccl" else "cpu")
         return r, drv
@@ -474,6 +489,8 @@ def main():
         if calib is not None:
             line["bands"]["calibration"] = calib
         line["ranks"] = [{k: v for k, v in ri.items() if k != "digest"} for ri in ranks_info]
+        if comm_fallback is not None:
+            line["halo_fallback"] = f"torch.distributed halo: no RCCL unique id on rank 0 ({comm_fallback})"
         if parity is not None:
             line["parity_check"] = parity
     # any PTX_* switch in the environment (PTX_AB selects A/B kernel variants: unset = product)
