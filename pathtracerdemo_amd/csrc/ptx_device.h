@@ -262,6 +262,21 @@ __device__ __forceinline__ bool box_root(f3 o, f3 inv, const SubRoot &R, float v
     return (tmin <= tmax) && (vx <= tmax) && (tmin <= vy);  // (empty -> (1, 0) never overlaps: box_pair)
 }
 
+// The root pre-filter of one chunk of nc <= 32 sub-mesh roots: bit k is set when root k
+// passes at the bound vy.  (Two roots per iteration, both LDS reads in flight before either
+// test, measured +-0: DESIGN 4.1e.)
+template <bool PROF>
+__device__ __forceinline__ uint32_t root_mask(const SubRoot *rs, uint32_t nc, f3 lo, f3 inv, float vx, float vy,
+                                              Prof &pf) {
+    uint32_t mask = 0u;
+#pragma unroll 1
+    for (uint32_t k = 0; k < nc; ++k) {
+        if (PROF) pf.hit(PROF_ROOT);
+        if (box_root(lo, inv, rs[k], vx, vy)) mask |= 1u << k;
+    }
+    return mask;
+}
+
 // GetRayTriangleHitDistance (SH/PT_1_InitPass.wgsl:516-547) on the precomputed edges.
 __device__ __forceinline__ float ray_tri(f3 o, f3 d, float4 a, float4 b, float4 c, float det_eps) {
     f3 p0 = mk(a.x, a.y, a.z);
@@ -472,11 +487,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
             if (stop) {
                 // occluded (ANY): nothing more to test
             } else if (ROOTQ) {
-#pragma unroll 1
-                for (uint32_t k = 0; k < nc; ++k) {
-                    if (PROF) pf.hit(PROF_ROOT);
-                    if (box_root(lo, inv, roots[s0 + k], vx, vy)) mask |= 1u << k;
-                }
+                mask = root_mask<PROF>(roots + s0, nc, lo, inv, vx, vy, pf);
                 if (COUNT && PTX_INST_CULL && !may && mask != 0u && t_max == t_max)
                     atomicAdd(&sc.counters[CNT_CULL_MISS], 1ull);
             } else {
@@ -745,11 +756,7 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
                     // reference tests root s with the best t after roots < s, never larger; the
                     // exact test is repeated when a root is taken, below)
                     const uint32_t nc = nsub - s0 < 32u ? nsub - s0 : 32u;
-#pragma unroll 1
-                    for (uint32_t k = 0; k < nc; ++k) {
-                        if (PROF) pf.hit(PROF_ROOT);
-                        if (box_root(lo, inv, subs[sub_base + s0 + k], vx, vy)) mask |= 1u << k;
-                    }
+                    mask |= root_mask<PROF>(subs + (sub_base + s0), nc, lo, inv, vx, vy, pf);
                     vy_pf = vy;
                     if (COUNT && PTX_INST_CULL && !may && mask != 0u) atomicAdd(&sc.counters[CNT_CULL_MISS], 1ull);
                 }
