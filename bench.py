@@ -62,12 +62,29 @@ DEFAULT_SCENE = {"reuse": "c3_interior_32", "restir": "dummy_scene_1", "mcpt": "
 
 
 def ab_knob(key, dflt):
-    """PTX_AB's value for `key` as the library reads it (ptx_api.cpp ab_knob): "K" -> 1, "K=v" -> v."""
+    """PTX_AB's value for `key` as the library reads it (ptx_api.cpp ab_knob): "K" -> 1, "K=v" ->
+    atoi(v) -- the leading decimal integer of v, 0 when there is none ("K=" included)."""
+    import re
     for item in os.environ.get("PTX_AB", "").split(","):
         k, eq, v = item.partition("=")
         if k == key:
-            return int(v) if eq else 1
+            if not eq:
+                return 1
+            m = re.match(r"\s*([+-]?\d+)", v)
+            return int(m.group(1)) if m else 0
     return dflt
+
+
+def usable_cpus() -> int:
+    """CPUs this process can actually use: its affinity set, capped by the cgroup CPU quota
+    (a container's share -- the GPU box shows 256 logical CPUs but allows 16)."""
+    import math
+    h = host_cpus()
+    n = h.get("affinity") or h.get("logical") or 1
+    q = h.get("cgroup_cpus")
+    if q:
+        n = min(n, max(1, math.ceil(q)))
+    return max(1, n)
 
 
 def ray_bytes(c: dict) -> int:
@@ -102,8 +119,8 @@ def parse():
                     help="spatial pass of the interior rows while the halo is in flight")
     ap.add_argument("--scene", default=None, help="default: c3_interior_32 (reuse), dummy_scene_1 (others)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="C-oracle CPU baseline threads (default: every logical CPU of the host, os.cpu_count(); "
-                         "a 16-thread figure is reported beside it)")
+                    help="C-oracle CPU baseline threads (default: the CPUs this process may use -- affinity "
+                         "capped by the cgroup quota; a run on every logical CPU is reported beside it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs3", action="store_true", help="skip the configs3_one_gpu line (profiling runs)")
     ap.add_argument("--variant", choices=["wave", "simple"], default="wave",
@@ -407,9 +424,9 @@ def main():
         # duration is the HIP-event average over the timed region.
         dom = "trace_queue"
         traced = [p for p in passes if p != "gbuffer"]
-        if pipeline == "reuse" and ab_knob("FINAL_ONE", 1):
-            # the reuse pipeline's PT_4 walks its replays inside its one logic kernel (wfinal_one):
-            # none of its queries reach trace_queue
+        if st_k["kernel_launches"][N.PTX_STAT_FINAL_FUSED]:
+            # the library reports that the reuse pipeline's PT_4 walked its replays inside its one
+            # logic kernel (wfinal_one): none of its queries reached trace_queue
             traced = [p for p in traced if p != "final"]
         work = {k: sum(counts[p][k] for p in traced) for k in counts[traced[0]]}
         per_frame = n_trace / args.steps
@@ -426,6 +443,8 @@ def main():
         extra = {}
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
+    # (profiles/hbm_traffic.json travels to the GPU box: .gpurunignore excludes only the
+    # per-round profile directories)
     prof = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(prof):
         try:
@@ -435,8 +454,8 @@ def main():
             traffic = None
     cpu = ts_cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads or (os.cpu_count() or 1))
-        ts_cpu = ts_cpu_baseline(cs, args.scene, W, Hb, 16, rows=Hb)
+        cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads or usable_cpus(), device=device)
+        ts_cpu = ts_cpu_baseline(cs, args.scene, W, Hb, args.cpu_threads or usable_cpus(), rows=Hb)
     # configs[3]'s 3840x2160 frame on this one GPU: the single-GPU reference of the strong
     # split the N > 1 lines run (their per-GPU efficiency is value_N / (N x this value))
     one_gpu_4k = None
@@ -478,6 +497,8 @@ def main():
         "cpu_baseline": cpu,
         "ts_cpu_baseline": ts_cpu,
     }
+    if cpu is not None and "parity" in cpu:
+        line["parity"] = cpu.pop("parity")
     if world == 1:
         line["scaling_note"] = ("one GPU: configs[2]'s frame; `--gpus N` splits configs[3]'s 3840x2160 frame into N "
                                 "row bands (strong); configs3_one_gpu is that frame on this one GPU")
@@ -542,9 +563,14 @@ def one_gpu_rate(cs, W, H, pipeline, device, steps, warmup):
             "note": "configs[3]'s frame on ONE GPU: the reference for the N-GPU strong split"}
 
 
-def cpu_baseline(cs, W, H, pipeline, threads):
+def cpu_baseline(cs, W, H, pipeline, threads, device=0):
     """The C oracle (a port of the WGSL + the reuse passes) on the host cores, timed over
-    whole frames: one frame (restir / mcpt), two for reuse (the second with its history)."""
+    whole frames: one frame (restir / mcpt), two for reuse / GI (the second with its history).
+
+    The oracle's frames are then the checker of the benched configuration (N = 1): a fresh
+    handle renders the same frames of the same frame size, camera and scene on the GPU, and
+    the whole image (+ the spatial-output reservoirs for reuse) is compared with them bit for
+    bit -- the line's `parity` field (relative L2 of the radiance beside it)."""
     from oracle import oracle as O
     from pathtracerdemo_amd.scene.camera import Camera
     threads = max(1, threads)
@@ -553,44 +579,70 @@ def cpu_baseline(cs, W, H, pipeline, threads):
     u = cs.uniform(W, H, cam.view_projection_inverse(), cam.location, 1)
     nf = 2 if pipeline in ("reuse", "gi") else 1
 
-    def full_frames(nthreads):
+    def full_frames(nthreads, rect=None):
         fr = O.Frame(u, cs.scene, cs.geometry, cs.accel)
         t0 = time.perf_counter()
         for f in range(1, nf + 1):
             fr.set_frame_index(f)
             if pipeline == "reuse":
-                fr.run_reuse_frame(threads=nthreads)
+                fr.run_reuse_frame(threads=nthreads, rect=rect)
             elif pipeline == "gi":
-                fr.run_gi_frame(threads=nthreads)
+                fr.run_gi_frame(threads=nthreads, rect=rect)
             else:
-                fr.run(O.PASS_RESTIR if pipeline == "restir" else O.PASS_MCPT, threads=nthreads)
-        return time.perf_counter() - t0
+                fr.run(O.PASS_RESTIR if pipeline == "restir" else O.PASS_MCPT, threads=nthreads, rect=rect)
+        return time.perf_counter() - t0, fr
 
-    dt = full_frames(threads)
-    dt16 = full_frames(min(16, threads)) if threads != 16 else dt
+    dt, fr = full_frames(threads)
+    logical = os.cpu_count() or 1
+    dt_all = full_frames(logical)[0] if logical != threads else dt
     # one thread on a 64-row band of the same frames (the single-core rate)
-    fr1 = O.Frame(u, cs.scene, cs.geometry, cs.accel)
     rows = min(H, 64)
     y0 = (H - rows) // 2
-    t1 = time.perf_counter()
-    for f in range(1, nf + 1):
-        fr1.set_frame_index(f)
-        rect = (0, y0, W, y0 + rows)
-        if pipeline == "reuse":
-            fr1.run_reuse_frame(threads=1, rect=rect)
-        elif pipeline == "gi":
-            fr1.run_gi_frame(threads=1, rect=rect)
-        else:
-            fr1.run(O.PASS_RESTIR if pipeline == "restir" else O.PASS_MCPT, threads=1, rect=rect)
-    dt1 = time.perf_counter() - t1
-    return {"value": round(nf * W * H / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{nf} full {W}x{H} frame(s) ({pipeline}, FrameIndex 1..{nf}), C oracle, {threads} pthreads",
-            "seconds": round(dt, 2), "cpu_model": cpu_model(), "host_cpus": host_cpus(),
-            "at_16_threads": {"value": round(nf * W * H / dt16 / 1e6, 4), "unit": "Msamples/s", "cores": min(16, threads),
-                              "seconds": round(dt16, 2)},
-            "single_thread": {"value": round(nf * W * rows / dt1 / 1e6, 4), "unit": "Msamples/s",
-                              "sample": f"rows {y0}..{y0 + rows} of the same {nf} frame(s), 1 thread",
-                              "seconds": round(dt1, 2)}}
+    dt1 = full_frames(1, rect=(0, y0, W, y0 + rows))[0]
+    out = {"value": round(nf * W * H / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": f"{nf} full {W}x{H} frame(s) ({pipeline}, FrameIndex 1..{nf}), C oracle, {threads} pthreads "
+                     "(the CPUs this process may use: affinity capped by the cgroup quota)",
+           "seconds": round(dt, 2), "cpu_model": cpu_model(), "host_cpus": host_cpus(),
+           "at_all_logical_cpus": {"value": round(nf * W * H / dt_all / 1e6, 4), "unit": "Msamples/s",
+                                   "cores": logical, "seconds": round(dt_all, 2)},
+           "single_thread": {"value": round(nf * W * rows / dt1 / 1e6, 4), "unit": "Msamples/s",
+                             "sample": f"rows {y0}..{y0 + rows} of the same {nf} frame(s), 1 thread",
+                             "seconds": round(dt1, 2)}}
+    try:
+        out["parity"] = frame_parity(cs, W, H, pipeline, device, nf, fr)
+    except Exception as e:  # noqa: BLE001 -- reported, never hidden
+        out["parity"] = {"error": f"{type(e).__name__}: {e}"}
+    return out
+
+
+def frame_parity(cs, W, H, pipeline, device, nf, fr):
+    """The benched configuration's first `nf` frames on a fresh handle vs the oracle's frames
+    `fr` (same scene, size, camera, FrameIndex 1..nf): bit-exactness and relative L2."""
+    from pathtracerdemo_amd.renderer import Renderer
+    r = Renderer(W, H, device=device, pipeline=pipeline)
+    r.Initialize(cs)
+    for _ in range(nf):
+        r.Update()
+        r.Render()
+    img = r.read_image()
+    hist = r.read_history() if pipeline == "reuse" else None
+    r.close()
+    want = np.asarray(fr.accum).reshape(img.shape)
+    diff_px = int(np.any(img.view(np.uint32) != want.view(np.uint32), axis=-1).sum())
+    a, b = img[..., :3].astype(np.float64), want[..., :3].astype(np.float64)
+    den = float(np.sqrt((b * b).sum()))
+    out = {"frames": nf, "pixels": W * H, "radiance_pixels_differing": diff_px,
+           "rel_l2": float(np.sqrt(((a - b) ** 2).sum())) / den if den > 0 else 0.0}
+    bit_exact = diff_px == 0
+    if hist is not None:
+        hw = np.asarray(fr.res_hist).reshape(hist.shape)
+        nres = int(np.any(hist.view(np.uint32) != hw.view(np.uint32), axis=-1).sum())
+        out["reservoir_pixels_differing"] = nres
+        bit_exact = bit_exact and nres == 0
+    out["bit_exact"] = bit_exact
+    out["compared"] = ("the whole image" + (" + all 32 words of every spatial-output reservoir" if hist is not None
+                                             else "") + f" of frames 1..{nf} on the GPU vs the C oracle")
+    return out
 
 
 def host_cpus() -> dict:

@@ -75,6 +75,9 @@ extern "C" {
                                   overlaps its passes: slots 0..2 then only get the per-part
                                   G-buffer launches, with PTX_FLAG_TIME_LAUNCHES          */
 #define PTX_STAT_PASS_GROUP 10 /* ptx_run_passes calls of the wavefront kernels          */
+#define PTX_STAT_FINAL_FUSED 11 /* count only (no time): PT_4 passes of the reuse pipeline that
+                                   walked their replays inside their one logic launch
+                                   (wfinal_one), so none of their queries reached trace_queue */
 
 /* buffers for ptx_read_buffer / ptx_write_buffer / ptx_device_pointer */
 #define PTX_BUF_GBUFFER 0    /* band_h * W * 4 u32   */

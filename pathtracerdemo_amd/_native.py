@@ -21,6 +21,7 @@ PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_FINAL, PTX_PASS_MCPT, PTX_PASS_TRACE =
 PTX_PASS_TEMPORAL, PTX_PASS_SPATIAL = 8, 9
 PTX_STAT_WAVE_TRACE, PTX_STAT_WAVE_LOGIC, PTX_STAT_FRAME = 5, 6, 7  # stats-only slots (include/ptx.h)
 PTX_STAT_PASS_GROUP = 10
+PTX_STAT_FINAL_FUSED = 11
 PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS, PTX_BUF_RESERVOIR_HIST = 0, 1, 2, 3, 4
 PTX_BUF_DIRECT = 5
 PTX_FLAG_COUNT_WORK = 1

@@ -632,6 +632,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
         e = wave_final_one(sc, w, gb, fres, (float4 *)h->d_accum.p, h->stack_depth, st);
         event_end(t, st);
+        h->launches[PTX_STAT_FINAL_FUSED] += 1;  // (bench.py: PT_4's queries are not trace_queue's)
         h->init_state_valid = false;  // (its queue slots are rewritten, as by the queued form)
         return e;
     }

@@ -24,9 +24,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "ptx_internal.h"
@@ -45,6 +47,9 @@ struct Rccl {
     ncclResult_t (*destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*async_error)(ncclComm_t, ncclResult_t *) = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
+    // optional (non-blocking communicator init with a deadline; absent -> blocking init)
+    ncclResult_t (*init_rank_config)(ncclComm_t *, int, ncclUniqueId, int, ncclConfig_t *) = nullptr;
+    ncclResult_t (*abort)(ncclComm_t) = nullptr;
     bool ok = false;
     std::string why;
 };
@@ -79,6 +84,8 @@ const Rccl &rccl() {
         sym(r.async_error, "ncclCommGetAsyncError");
         sym(r.error_string, "ncclGetErrorString");
         r.ok = all;
+        r.init_rank_config = reinterpret_cast<decltype(r.init_rank_config)>(dlsym(lib, "ncclCommInitRankConfig"));
+        r.abort = reinterpret_cast<decltype(r.abort)>(dlsym(lib, "ncclCommAbort"));
     });
     return r;
 }
@@ -89,6 +96,37 @@ const Rccl &rccl() {
         if (r_ != ncclSuccess)                                                                               \
             return fail((h), PTX_E_HIP, "%s: %s (%s:%d)", #expr, rccl().error_string(r_), __FILE__, __LINE__); \
     } while (0)
+
+// Non-blocking communicators (ptx_comm_init): the init and every group end return at once and
+// complete in the background; their state is polled here until it leaves ncclInProgress or the
+// deadline passes.  A rank whose peers never join (one died before its ncclCommInitRank, or
+// failed inside it) thus gets an error status after `seconds` instead of hanging for ever, and
+// the communicator is aborted (PTX_AB=COMM_TIMEOUT_S=n overrides the 120 s default).
+int comm_timeout_s() {
+    static const int t = ab_knob("COMM_TIMEOUT_S", 120);
+    return t > 0 ? t : 120;
+}
+ncclResult_t comm_wait(ncclComm_t c, int seconds) {
+    const auto end = std::chrono::steady_clock::now() + std::chrono::seconds(seconds);
+    for (uint32_t spin = 0;; ++spin) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = rccl().async_error(c, &st);
+        if (r != ncclSuccess) return r;
+        if (st != ncclInProgress) return st;
+        if (std::chrono::steady_clock::now() >= end) return ncclInProgress;  // (the deadline)
+        if (spin >= 64u) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+// ncclGroupEnd on a band handle's communicator: complete (enqueued on the streams) on return.
+int group_end_wait(ptx_handle *h) {
+    ncclResult_t r = rccl().group_end();
+    if (r == ncclInProgress) r = comm_wait((ncclComm_t)h->comm, comm_timeout_s());
+    if (r == ncclInProgress)
+        return fail(h, PTX_E_HIP, "RCCL group (rank %d of %d) not enqueued within %d s", h->rank, h->world,
+                    comm_timeout_s());
+    if (r != ncclSuccess) return fail(h, PTX_E_HIP, "ncclGroupEnd: %s", rccl().error_string(r));
+    return PTX_OK;
+}
 
 // Byte ranges of the halo-extended G-buffer and reservoir allocations: rows [r0, r0 + rows)
 // (row 0 = the first top-halo row).
@@ -301,9 +339,11 @@ int check_neighbours(ptx_handle *h) {
         r = R.send(d, 6, ncclUint32, h->rank + 1, c, h->stream);
         if (r == ncclSuccess) r = R.recv(d + 12, 6, ncclUint32, h->rank + 1, c, h->stream);
     }
-    const ncclResult_t r2 = R.group_end();
-    if (r == ncclSuccess) r = r2;
-    if (r != ncclSuccess) return done(fail(h, PTX_E_HIP, "neighbour check: %s", R.error_string(r)));
+    if (r != ncclSuccess) {
+        (void)R.group_end();
+        return done(fail(h, PTX_E_HIP, "neighbour check: %s", R.error_string(r)));
+    }
+    if (int rc = group_end_wait(h)) return done(rc);
     e = hipMemcpyAsync(got, d + 6, sizeof got, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return done(fail(h, PTX_E_HIP, "neighbour check: %s", hipGetErrorString(e)));
@@ -336,8 +376,11 @@ int render_band_nccl(ptx_handle *h) {
     if (int rc = exchange_stream(h, xs)) return rc;
     NCCL_CHECK(h, rccl().group_start());
     const int rc = nccl_halo(h, xs);
-    NCCL_CHECK(h, rccl().group_end());
-    if (rc) return rc;
+    if (rc) {
+        (void)rccl().group_end();
+        return rc;
+    }
+    if (int r2 = group_end_wait(h)) return r2;
     if (h->halo_top) h->halo_bytes_sent += send_up(h).gb + send_up(h).rb;
     if (h->halo_bot) h->halo_bytes_sent += send_down(h).gb + send_down(h).rb;
     if (int r2 = halo_landed(h, xs)) return r2;
@@ -391,7 +434,26 @@ int ptx_comm_init(ptx_handle *h, const void *unique_id, size_t bytes, int rank, 
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof id);
     ncclComm_t c = nullptr;
-    NCCL_CHECK(h, R.init_rank(&c, world, id, rank));
+    if (R.init_rank_config && R.abort) {
+        // non-blocking init, polled against a deadline: every rank exits with an error status
+        // instead of hanging when a peer never joins (comm_wait)
+        ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+        config.blocking = 0;
+        ncclResult_t r = R.init_rank_config(&c, world, id, rank, &config);
+        if (r == ncclSuccess || r == ncclInProgress) r = comm_wait(c, comm_timeout_s());
+        if (r != ncclSuccess) {
+            if (c) (void)R.abort(c);
+            if (r == ncclInProgress)
+                return fail(h, PTX_E_HIP,
+                            "ptx_comm_init: rank %d of %d: the communicator was not complete after %d s (a peer "
+                            "rank never joined or failed); aborted",
+                            rank, world, comm_timeout_s());
+            return fail(h, PTX_E_HIP, "ptx_comm_init: ncclCommInitRankConfig (rank %d of %d): %s", rank, world,
+                        R.error_string(r));
+        }
+    } else {
+        NCCL_CHECK(h, R.init_rank(&c, world, id, rank));
+    }
     h->comm = c;
     h->rank = rank;
     h->world = world;

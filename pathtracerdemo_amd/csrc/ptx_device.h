@@ -118,6 +118,26 @@ struct WaveTimer {
     }
 };
 #define PTX_WAVE_TIMER(sc, k) WaveTimer wave_timer_((sc).wgt, (k))
+// one dynamic trace batch {start, end, KID_BATCH << 32 | batch, round << 32 | hw id} (lane 0)
+constexpr uint32_t KID_BATCH = 12;
+__device__ __forceinline__ void batch_record(unsigned long long *buf, unsigned long long t0, uint32_t bi, uint32_t round) {
+    if (!buf || __lane_id() != 0u) return;
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long i = atomicAdd(buf, 1ull);
+    if (i >= (1ull << 20)) return;
+    unsigned long long *r = buf + 4u + 4u * i;
+    r[0] = t0;
+    r[1] = t1;
+    r[2] = ((unsigned long long)KID_BATCH << 32) | bi;
+    r[3] = ((unsigned long long)round << 32) | (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+}
+// straggler queries (tools/stragglers.py): a trace call with >= kStragglerAabb slab tests leaves
+// two records {o.xy, o.z d.x, KID_STRAGGLER << 32 | slab tests, triangle tests | t_max << 32} and
+// {d.yz, t | inst << 32, KID_STRAGGLER2 << 32 | prim, sub-mesh}
+constexpr uint32_t KID_STRAGGLER = 13, KID_STRAGGLER2 = 14, kStragglerAabb = 256;
+__device__ __forceinline__ unsigned long long pk2(float a, float b) {
+    return (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
+}
 #else
 #define PTX_WAVE_TIMER(sc, k) ((void)0)
 #endif
@@ -877,6 +897,22 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
             if (pf.lane[r]) atomicAdd(&sc.counters[9 + 2 * r], (unsigned long long)pf.lane[r]);
         }
     }
+#ifdef PTX_WG_TIMES
+    if (sc.wgt && counted && n_aabb >= kStragglerAabb) {
+        const unsigned long long i = atomicAdd(sc.wgt, 2ull);
+        if (i + 1u < (1ull << 20)) {
+            unsigned long long *r = sc.wgt + 4u + 4u * i;
+            r[0] = pk2(ray.o.x, ray.o.y);
+            r[1] = pk2(ray.o.z, ray.d.x);
+            r[2] = ((unsigned long long)KID_STRAGGLER << 32) | n_aabb;
+            r[3] = (unsigned long long)n_tri | ((unsigned long long)__float_as_uint(t_max) << 32);
+            r[4] = pk2(ray.d.y, ray.d.z);
+            r[5] = (unsigned long long)__float_as_uint(best.valid ? vy : -1.0f) | ((unsigned long long)best.s.inst << 32);
+            r[6] = ((unsigned long long)KID_STRAGGLER2 << 32) | best.s.prim;
+            r[7] = best.s.mat;
+        }
+    }
+#endif
     if ((COUNT || PROF) && counted) {  // (PROF alone: the culled walk's executed tests)
         atomicAdd(&sc.counters[CNT_RAYS], 1ull);
         atomicAdd(&sc.counters[CNT_INST], (unsigned long long)sc.n_inst);

@@ -129,6 +129,9 @@ struct ReuseArgs {
                         // loads but does not use) never sends the fold's gather out of bounds
 };
 constexpr uint32_t kJobPending = 0xFFFFFFFFu;  // jres.w of such a job (a NaN: never a stored q)
+// The fold keeps ONE result buffer per trace round (WaveBufs::res[0..2], res_sel = round % 3):
+// a fourth round would overwrite the round-0 light results the combine still reads.
+static_assert(kWaveRoundsReuse <= 3, "fold_last: one result buffer per reuse trace round");
 // rounds of {trace, step} between a reuse pass's start and combine launches
 int reuse_rounds(int pass_temporal, const ReuseArgs &A);
 hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,

@@ -194,9 +194,15 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                 const uint32_t j = w.seg_phys + w.seg_base + lo;
                 const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
                 const uint32_t i = (bi - pref[lo]) * 64u + lane;
+#ifdef PTX_WG_TIMES
+                const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
+#endif
                 trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
                                               w.rays + 2u * (size_t)j * w.ray_stride,
                                               res_buf(w, round) + 2u * (size_t)j * w.ray_stride, i, i < n);
+#ifdef PTX_WG_TIMES
+                batch_record(sc.wgt, tb0, bi, round);
+#endif
             }
             bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
         }

@@ -71,8 +71,52 @@ function compose(t, q, s) {
     t[0], t[1], t[2], 1];
 }
 
+/** The sign-relevant 4x4 determinant (cofactor expansion along the first row). */
+function determinant(m) {
+  const a = (r, c) => m[4 * c + r];
+  const det3 = (r0, r1, r2, c0, c1, c2) => a(r0, c0) * (a(r1, c1) * a(r2, c2) - a(r1, c2) * a(r2, c1))
+    - a(r0, c1) * (a(r1, c0) * a(r2, c2) - a(r1, c2) * a(r2, c0)) + a(r0, c2) * (a(r1, c0) * a(r2, c1) - a(r1, c1) * a(r2, c0));
+  return a(0, 0) * det3(1, 2, 3, 1, 2, 3) - a(0, 1) * det3(1, 2, 3, 0, 2, 3)
+    + a(0, 2) * det3(1, 2, 3, 0, 1, 3) - a(0, 3) * det3(1, 2, 3, 0, 1, 2);
+}
+
+/** Matrix4.decompose(position, quaternion, scale) with Quaternion.setFromRotationMatrix (f64). */
+function decompose(m) {
+  let sx = Math.sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+  const sy = Math.sqrt(m[4] * m[4] + m[5] * m[5] + m[6] * m[6]);
+  const sz = Math.sqrt(m[8] * m[8] + m[9] * m[9] + m[10] * m[10]);
+  if (determinant(m) < 0) sx = -sx;
+  const ix = 1 / sx, iy = 1 / sy, iz = 1 / sz;
+  const m11 = m[0] * ix, m21 = m[1] * ix, m31 = m[2] * ix;
+  const m12 = m[4] * iy, m22 = m[5] * iy, m32 = m[6] * iy;
+  const m13 = m[8] * iz, m23 = m[9] * iz, m33 = m[10] * iz;
+  const trace = m11 + m22 + m33;
+  let q;
+  if (trace > 0) {
+    const s = 0.5 / Math.sqrt(trace + 1.0);
+    q = [(m32 - m23) * s, (m13 - m31) * s, (m21 - m12) * s, 0.25 / s];
+  } else if (m11 > m22 && m11 > m33) {
+    const s = 2.0 * Math.sqrt(1.0 + m11 - m22 - m33);
+    q = [0.25 * s, (m12 + m21) / s, (m13 + m31) / s, (m32 - m23) / s];
+  } else if (m22 > m33) {
+    const s = 2.0 * Math.sqrt(1.0 + m22 - m11 - m33);
+    q = [(m12 + m21) / s, 0.25 * s, (m23 + m32) / s, (m13 - m31) / s];
+  } else {
+    const s = 2.0 * Math.sqrt(1.0 + m33 - m11 - m22);
+    q = [(m13 + m31) / s, (m23 + m32) / s, 0.25 * s, (m21 - m12) / s];
+  }
+  return { t: [m[12], m[13], m[14]], q, s: [sx, sy, sz] };
+}
+
+/** A node's local matrix as three.js ends up composing it.  A glTF `matrix` goes through
+ * GLTFLoader's node.applyMatrix4: premultiplied onto the identity, decomposed, and recomposed by
+ * updateMatrix -- the raw matrix itself is never used (as scene/gltf.py; restated from three's
+ * published source, parity-unpinned against the library, which is not installed here). */
 function localMatrix(node) {
-  if (node.matrix) return node.matrix.slice();  // column-major, Matrix4.fromArray
+  if (node.matrix) {
+    const d = decompose(multiply(node.matrix.slice(), compose([0, 0, 0], [0, 0, 0, 1], [1, 1, 1])));
+    return compose(d.t, d.q, d.s);
+  }
   return compose(node.translation || [0, 0, 0], node.rotation || [0, 0, 0, 1], node.scale || [1, 1, 1]);
 }
 
@@ -119,7 +163,7 @@ function material(g, idx) {
 }
 
 /** geometry.applyMatrix4(matrixWorld): positions through Vector3.applyMatrix4, normals through the
- * normal matrix then normalize() (divideScalar(length() || 1)), f64 math, f32 storage. */
+ * normal matrix then normalize() (divideScalar(length() || 1) = multiplyScalar(1 / len)), f64 math, f32 storage. */
 function bake(g, prim, e) {
   const attrs = prim.attributes;
   const P = accessor(g, attrs.POSITION), nv = P.count;
@@ -140,9 +184,10 @@ function bake(g, prim, e) {
     const nx = n[0] * a + n[3] * b + n[6] * c, ny = n[1] * a + n[4] * b + n[7] * c, nz = n[2] * a + n[5] * b + n[8] * c;
     let ln = Math.sqrt(nx * nx + ny * ny + nz * nz);
     if (ln === 0) ln = 1;
-    normals[3 * v] = nx / ln;
-    normals[3 * v + 1] = ny / ln;
-    normals[3 * v + 2] = nz / ln;
+    const rl = 1 / ln;  // divideScalar(s) = multiplyScalar(1 / s)
+    normals[3 * v] = nx * rl;
+    normals[3 * v + 1] = ny * rl;
+    normals[3 * v + 2] = nz * rl;
   }
   return { positions, normals, uvs: uv, index, material: material(g, prim.material) };
 }
@@ -189,4 +234,4 @@ function loadGlbGeometry(file) {
   return { positions, normals, uvs, index, groups, materials };
 }
 
-module.exports = { readGlb, accessor, primitives, loadGlbGeometry, compose, multiply, normalMatrix };
+module.exports = { readGlb, accessor, primitives, loadGlbGeometry, compose, decompose, localMatrix, multiply, normalMatrix };

@@ -19,6 +19,7 @@ the published loader behaviour, parity with three.js is unpinned.
 from __future__ import annotations
 
 import json
+import math
 import struct
 from dataclasses import dataclass, field
 
@@ -64,9 +65,60 @@ def _compose(t, q, s) -> np.ndarray:
             float(t[0]), float(t[1]), float(t[2]), 1.0]
 
 
+def _decompose(m) -> tuple:
+    """three.js Matrix4.decompose(position, quaternion, scale) (f64, the library's order): column
+    lengths as scale (the first negated when the determinant is negative), the columns scaled by
+    1 / s, Quaternion.setFromRotationMatrix of that 3x3."""
+    sx = math.sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2])
+    sy = math.sqrt(m[4] * m[4] + m[5] * m[5] + m[6] * m[6])
+    sz = math.sqrt(m[8] * m[8] + m[9] * m[9] + m[10] * m[10])
+    if _determinant(m) < 0:
+        sx = -sx
+    ix, iy, iz = 1 / sx, 1 / sy, 1 / sz
+    m11, m21, m31 = m[0] * ix, m[1] * ix, m[2] * ix
+    m12, m22, m32 = m[4] * iy, m[5] * iy, m[6] * iy
+    m13, m23, m33 = m[8] * iz, m[9] * iz, m[10] * iz
+    trace = m11 + m22 + m33
+    if trace > 0:
+        s = 0.5 / math.sqrt(trace + 1.0)
+        q = ((m32 - m23) * s, (m13 - m31) * s, (m21 - m12) * s, 0.25 / s)
+    elif m11 > m22 and m11 > m33:
+        s = 2.0 * math.sqrt(1.0 + m11 - m22 - m33)
+        q = (0.25 * s, (m12 + m21) / s, (m13 + m31) / s, (m32 - m23) / s)
+    elif m22 > m33:
+        s = 2.0 * math.sqrt(1.0 + m22 - m11 - m33)
+        q = ((m12 + m21) / s, 0.25 * s, (m23 + m32) / s, (m13 - m31) / s)
+    else:
+        s = 2.0 * math.sqrt(1.0 + m33 - m11 - m22)
+        q = ((m13 + m31) / s, (m23 + m32) / s, 0.25 * s, (m21 - m12) / s)
+    return (m[12], m[13], m[14]), q, (sx, sy, sz)
+
+
+def _determinant(m) -> float:
+    """The 4x4 determinant by cofactors along the first row, as js/gltf.js (only its sign is
+    used: decompose's mirrored-scale test)."""
+    def a(r, c):
+        return m[4 * c + r]
+
+    def det3(r0, r1, r2, c0, c1, c2):
+        return (a(r0, c0) * (a(r1, c1) * a(r2, c2) - a(r1, c2) * a(r2, c1))
+                - a(r0, c1) * (a(r1, c0) * a(r2, c2) - a(r1, c2) * a(r2, c0))
+                + a(r0, c2) * (a(r1, c0) * a(r2, c1) - a(r1, c1) * a(r2, c0)))
+    return (a(0, 0) * det3(1, 2, 3, 1, 2, 3) - a(0, 1) * det3(1, 2, 3, 0, 2, 3)
+            + a(0, 2) * det3(1, 2, 3, 0, 1, 3) - a(0, 3) * det3(1, 2, 3, 0, 1, 2))
+
+
 def _node_local_matrix(node) -> list:
     if "matrix" in node:
-        return [float(v) for v in node["matrix"]]  # column-major in glTF, as Matrix4.fromArray
+        # GLTFLoader: node.applyMatrix4(Matrix4.fromArray(matrix)) -- premultiplied onto the
+        # node's identity matrix, then DECOMPOSED into position / quaternion / scale, and the
+        # world matrix later recomposed from them (Object3D.updateMatrix -> compose): the raw
+        # matrix itself is never used.  (Restated from three.js's published source; three is
+        # not installed here, so this path is parity-unpinned against the library itself.)
+        raw = [float(v) for v in node["matrix"]]
+        ident = _compose([0.0, 0.0, 0.0], [0.0, 0.0, 0.0, 1.0], [1.0, 1.0, 1.0])
+        t, q, sc = _decompose(_multiply(raw, ident))
+        return _compose(t, q, sc)
     return _compose(node.get("translation", [0.0, 0.0, 0.0]), node.get("rotation", [0.0, 0.0, 0.0, 1.0]),
                     node.get("scale", [1.0, 1.0, 1.0]))
 
@@ -199,7 +251,7 @@ class Glb:
         if nrm is None:
             raise ValueError("primitives without normals are not supported")
         # BufferAttribute.applyNormalMatrix(Matrix3.getNormalMatrix(m)) -> Vector3.applyMatrix3,
-        # then normalize(): divideScalar(length() || 1), f64, stored to f32
+        # then normalize(): divideScalar(length() || 1) = multiplyScalar(1 / len), f64, stored to f32
         n = _normal_matrix(world)
         x, y, z = nrm[:, 0], nrm[:, 1], nrm[:, 2]
         nx = n[0] * x + n[3] * y + n[6] * z
@@ -207,6 +259,7 @@ class Glb:
         nz = n[2] * x + n[5] * y + n[8] * z
         ln = np.sqrt(nx * nx + ny * ny + nz * nz)
         ln = np.where(ln == 0, 1.0, ln)
-        nrm_w = np.stack([nx / ln, ny / ln, nz / ln], axis=1).astype(np.float32)
+        rl = 1 / ln
+        nrm_w = np.stack([nx * rl, ny * rl, nz * rl], axis=1).astype(np.float32)
         return GltfPrimitive(positions=p_world, normals=nrm_w, uvs=uv, indices=idx,
                              material=self.material(prim.get("material")))

@@ -249,3 +249,36 @@ def test_js_mesh_load_builds_the_scene_compiler_meshes(which, tmp_path):
     for a in (cs.scene, cs.geometry, cs.accel):
         h.update(np.ascontiguousarray(a, dtype="<u4").tobytes())
     assert got["sha256"] == h.hexdigest()
+
+
+def test_matrix_nodes_are_decomposed_and_recomposed_like_three():
+    """A glTF node `matrix` goes through GLTFLoader's applyMatrix4 -> Matrix4.decompose ->
+    compose (never used raw): the Python and JS bakers agree bit for bit on rotated, scaled,
+    mirrored (negative determinant) and sheared matrices, and the recomposed matrix equals the
+    raw TRS matrix to f64 rounding.  (three.js itself is absent: parity against the library
+    is unpinned; this pins the two hosts to one restatement.)"""
+    import math
+    from pathtracerdemo_amd.scene import gltf as G
+    rng = np.random.default_rng(7)
+    cases = []
+    for k in range(6):
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        ang = rng.uniform(-math.pi, math.pi)
+        q = [*(ax * math.sin(ang / 2)), math.cos(ang / 2)]
+        sc = list(rng.uniform(0.2, 3.0, size=3))
+        if k % 2:
+            sc[k % 3] = -sc[k % 3]  # mirrored
+        cases.append(G._compose(list(rng.normal(size=3) * 4), q, sc))
+    cases.append([1.0, 0.0, 0.0, 0.0, 0.5, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 1.0, 2.0, 3.0, 1.0])  # shear
+    want = [G._node_local_matrix({"matrix": m}) for m in cases]
+    for m, w in zip(cases[:-1], want[:-1]):
+        np.testing.assert_allclose(w, m, rtol=0, atol=1e-12 * max(1.0, max(abs(v) for v in m)))
+    src = ("const G = require('./pathtracerdemo_amd/js/gltf.js');"
+           "const ms = JSON.parse(require('fs').readFileSync(0, 'utf8'));"
+           "process.stdout.write(JSON.stringify(ms.map((m) => G.localMatrix({ matrix: m }))));")
+    p = subprocess.run([NODE, "-e", src], input=json.dumps(cases), capture_output=True, text=True, cwd=ROOT, timeout=60)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)
+    for g, w in zip(got, want):  # (JSON carries -0 as 0: compared as values, which is exact here)
+        assert np.array_equal(np.array(g, dtype=np.float64), np.array(w, dtype=np.float64))
