@@ -120,16 +120,23 @@ struct WaveTimer {
 #define PTX_WAVE_TIMER(sc, k) WaveTimer wave_timer_((sc).wgt, (k))
 // one dynamic trace batch {start, end, KID_BATCH << 32 | batch, round << 32 | hw id} (lane 0)
 constexpr uint32_t KID_BATCH = 12;
-__device__ __forceinline__ void batch_record(unsigned long long *buf, unsigned long long t0, uint32_t bi, uint32_t round) {
+// + {dbg[0] | dbg[1] << 32, dbg[2] | dbg[3] << 32, KID_BATCH_DBG << 32 | dbg[4], dbg[5]} (trace_core_flat)
+constexpr uint32_t KID_BATCH_DBG = 15;
+__device__ __forceinline__ void batch_record(unsigned long long *buf, unsigned long long t0, uint32_t bi, uint32_t round,
+                                             const uint32_t *dbg) {
     if (!buf || __lane_id() != 0u) return;
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long i = atomicAdd(buf, 1ull);
-    if (i >= (1ull << 20)) return;
+    const unsigned long long i = atomicAdd(buf, 2ull);
+    if (i + 1u >= (1ull << 20)) return;
     unsigned long long *r = buf + 4u + 4u * i;
     r[0] = t0;
     r[1] = t1;
     r[2] = ((unsigned long long)KID_BATCH << 32) | bi;
     r[3] = ((unsigned long long)round << 32) | (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    r[4] = (unsigned long long)dbg[0] | ((unsigned long long)dbg[1] << 32);
+    r[5] = (unsigned long long)dbg[2] | ((unsigned long long)dbg[3] << 32);
+    r[6] = ((unsigned long long)KID_BATCH_DBG << 32) | dbg[4];
+    r[7] = dbg[5];
 }
 // straggler queries (tools/stragglers.py): a trace call with >= kStragglerAabb slab tests leaves
 // two records {o.xy, o.z d.x, KID_STRAGGLER << 32 | slab tests, triangle tests | t_max << 32} and
@@ -713,7 +720,12 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
 template <bool COUNT, bool PROF = false, bool ANY = false>
 __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *subs, const Inst *insts, Ray ray,
                                                PassEps eps, uint32_t *stack, uint32_t stride, float t_max,
-                                               CoopLds coop, bool want_pos) {
+                                               CoopLds coop, bool want_pos, uint32_t *dbg = nullptr) {
+    // dbg (diagnostic build, tools/trace_tail.py): wave-level {refill iterations, node-loop
+    // iterations, leaf phases, triangle-deal chunks, calls, max slab tests of a lane}
+#ifndef PTX_WG_TIMES
+    (void)dbg;
+#endif
     Prof pf{};
     Hit best;
     best.valid = false;
@@ -740,6 +752,9 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
         for (;;) {
             const bool need = !done && leaf == 0u && sp < 0 && mask == 0u;
             if (__ballot(need) == 0ull) break;
+#ifdef PTX_WG_TIMES
+            if (dbg) dbg[0]++;
+#endif
             if (need) {
                 bool may = true;
                 if (s0 + 32u < nsub) {
@@ -786,6 +801,9 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
         for (;;) {
             const bool want = leaf == 0u && (sp >= 0 || mask != 0u);
             if (__ballot(want) == 0ull) break;
+#ifdef PTX_WG_TIMES
+            if (dbg) dbg[1]++;
+#endif
             if (PROF && want) pf.hit(PROF_NODE);
             const bool from_root = sp < 0;
             const uint32_t k = (from_root && mask != 0u) ? (uint32_t)__builtin_ctz(mask) : 0u;
@@ -825,6 +843,12 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
         const uint32_t cnt = leaf ? (leaf >> 24) & 0x7Fu : 0u, lfirst = leaf & LEAF_FIRST_MASK;
         uint32_t total;
         const uint32_t excl = wave_excl_sum(cnt, total);
+#ifdef PTX_WG_TIMES
+        if (dbg) {
+            dbg[2]++;
+            dbg[3] += (total + 63u) / 64u;
+        }
+#endif
         __hip_atomic_store(&coop.key[lane], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         bool nan_seen = false;
@@ -898,6 +922,12 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
         }
     }
 #ifdef PTX_WG_TIMES
+    if (dbg) {
+        dbg[4]++;
+        uint32_t m = counted ? n_aabb : 0u;
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+        dbg[5] = max(dbg[5], m);
+    }
     if (sc.wgt && counted && n_aabb >= kStragglerAabb) {
         const unsigned long long i = atomicAdd(sc.wgt, 2ull);
         if (i + 1u < (1ull << 20)) {

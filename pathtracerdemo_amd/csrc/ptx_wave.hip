@@ -61,7 +61,7 @@ constexpr uint32_t kFlatMinInstances = 3u;
 template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES = false, bool FLAT = false>
 __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
                                             uint32_t *stack, CoopLds coop, const float4 *rays, float4 *res,
-                                            uint32_t i, bool active) {
+                                            uint32_t i, bool active, uint32_t *dbg = nullptr) {
     float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
     if (active) {
         a = rays[2u * i];
@@ -78,7 +78,7 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
         // a Visibility hit's position is only needed to restart through a transmissive surface:
         // it is reconstructed below for those lanes only
         Hit h = (LDS_TABLES && FLAT)
-                    ? trace_core_flat<COUNT, PROF, OCC>(sc, subs, insts, r, eps, stack, WB, t_max, coop, !vis)
+                    ? trace_core_flat<COUNT, PROF, OCC>(sc, subs, insts, r, eps, stack, WB, t_max, coop, !vis, dbg)
                     : trace_core_tab<COUNT, PROF, true, OCC, TRACE_COOP, LDS_TABLES && PTX_NODE_UNI>(
                           sc, subs, insts, r, eps, stack, WB, t_max, coop, !vis);
         if (active && !vis) {
@@ -196,12 +196,15 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                 const uint32_t i = (bi - pref[lo]) * 64u + lane;
 #ifdef PTX_WG_TIMES
                 const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
+                uint32_t dbg[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+#else
+                uint32_t *dbg = nullptr;
 #endif
                 trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
                                               w.rays + 2u * (size_t)j * w.ray_stride,
-                                              res_buf(w, round) + 2u * (size_t)j * w.ray_stride, i, i < n);
+                                              res_buf(w, round) + 2u * (size_t)j * w.ray_stride, i, i < n, dbg);
 #ifdef PTX_WG_TIMES
-                batch_record(sc.wgt, tb0, bi, round);
+                batch_record(sc.wgt, tb0, bi, round, dbg);
 #endif
             }
             bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);

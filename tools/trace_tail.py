@@ -23,7 +23,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-KID_TRACE, KID_BATCH = 1, 12
+KID_TRACE, KID_BATCH, KID_BATCH_DBG = 1, 12, 15
 
 
 def list_schedule(durs, slots):
@@ -42,7 +42,11 @@ def launches(rec):
     """Split one frame's records into trace launches (single stream: launches do not overlap)."""
     kid = (rec[:, 2] >> np.uint64(32)).astype(np.int64) & 0x7F
     tw = rec[kid == KID_TRACE]
-    tb = rec[kid == KID_BATCH]
+    ib = np.nonzero(kid == KID_BATCH)[0]
+    ib = ib[ib + 1 < len(rec)]
+    ib = ib[kid[ib + 1] == KID_BATCH_DBG]
+    # a batch record + its work breakdown as one 8-word row
+    tb = np.concatenate([rec[ib], rec[ib + 1]], axis=1)
     order = np.argsort(tw[:, 0])
     tw = tw[order]
     out, cur, end = [], [], -1
@@ -135,6 +139,26 @@ def main():
             print(f"{fi}.{li:<4d} {span:8.1f} {drain:9.1f} {tail:8.1f} {100*tail/span:5.1f} {len(w):6d} {mean_res:9.0f}"
                   f" {plateau:8d} {len(b):8d} {row['batch_p50']:6.1f} {row['batch_p99']:6.1f} {row['batch_max']:6.1f}"
                   f" {meas:11.1f} {lpt_true:9.1f} " + (f"{lpt_prev:9.1f} {corr:10.3f}" if lpt_prev is not None else ""))
+    # what the slow batches do: wave-level iterations per region vs duration (last frame)
+    allb = np.concatenate([b for _, b in frames[-1]])
+    dur = (allb[:, 1] - allb[:, 0]) / 100.0
+    refill = (allb[:, 4] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    node = (allb[:, 4] >> np.uint64(32)).astype(np.int64)
+    leafp = (allb[:, 5] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    chunks = (allb[:, 5] >> np.uint64(32)).astype(np.int64)
+    calls = (allb[:, 6] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    maxslab = allb[:, 7].astype(np.int64)
+    order = np.argsort(dur)
+    print("\nbatches by duration (last frame): us, refill it, node-loop it, leaf phases, tri chunks, calls, max slab tests/lane")
+    for q in (0.5, 0.9, 0.99, 0.999):
+        k = order[int(q * (len(order) - 1))]
+        print(f"  p{q*100:5.1f}: {dur[k]:7.1f}  {refill[k]:5d} {node[k]:6d} {leafp[k]:5d} {chunks[k]:5d} {calls[k]:3d} {maxslab[k]:6d}")
+    print("  slowest 15:")
+    for k in order[::-1][:15]:
+        print(f"          {dur[k]:7.1f}  {refill[k]:5d} {node[k]:6d} {leafp[k]:5d} {chunks[k]:5d} {calls[k]:3d} {maxslab[k]:6d}")
+    for name, v in (("node-loop it", node), ("refill it", refill), ("leaf phases", leafp), ("tri chunks", chunks),
+                    ("calls", calls), ("max slab", maxslab)):
+        print(f"  corr(duration, {name}) = {np.corrcoef(dur, v)[0, 1]:.3f}; mean {v.mean():.1f}")
     if a.out:
         json.dump(summary, open(a.out, "w"), indent=1)
 
