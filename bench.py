@@ -87,6 +87,21 @@ def usable_cpus() -> int:
     return max(1, n)
 
 
+def camera_pose(step: int):
+    """`--camera-path`: the camera of frame `step` (0-based) -- an interactive walk through the
+    room as WebGPUEngine drives it (InputController.ts:81-159: 5 units/s at 60 Hz, i.e. ~0.08
+    units per frame, with a slow mouse turn): (location, yaw in degrees)."""
+    import math
+    a = 0.166 * step
+    return (0.5 * math.sin(a), 0.0, 6.0 - 0.3 * (1.0 - math.cos(a))), 6.0 * math.sin(0.1 * step)
+
+
+def set_pose(r, step: int):
+    loc, yaw = camera_pose(step)
+    r.GetCamera().set_location(*loc)
+    r.GetCamera().set_yaw(yaw)
+
+
 def ray_bytes(c: dict) -> int:
     return B_AABB * c["aabb_tests"] + B_TRI * c["tri_tests"] + B_INST * c["instance_xforms"] + B_HIT * c["hits"]
 
@@ -123,6 +138,9 @@ def parse():
                          "capped by the cgroup quota; a run on every logical CPU is reported beside it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs3", action="store_true", help="skip the configs3_one_gpu line (profiling runs)")
+    ap.add_argument("--camera-path", action="store_true",
+                    help="move the camera every frame (camera_pose: 5 units/s at 60 Hz and a turn), so the "
+                         "temporal pass reprojects its history (the interactive case behind the UI)")
     ap.add_argument("--variant", choices=["wave", "simple"], default="wave",
                     help="kernel variant (A/B): wavefront queues, or 1 thread/pixel")
     return ap.parse_args()
@@ -305,7 +323,13 @@ def main():
 
     r, band_drv = make()
 
+    steps_done = {}
+
     def frame(rr, drv):
+        if args.camera_path:  # every handle walks the same path from its own first frame
+            k = steps_done.get(id(rr), 0)
+            steps_done[id(rr)] = k + 1
+            set_pose(rr, k)
         rr.Update()
         if drv is None:
             rr.Render()
@@ -454,7 +478,8 @@ def main():
             traffic = None
     cpu = ts_cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads or usable_cpus(), device=device)
+        cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads or usable_cpus(), device=device,
+                           camera_path=args.camera_path)
         ts_cpu = ts_cpu_baseline(cs, args.scene, W, Hb, args.cpu_threads or usable_cpus(), rows=Hb)
     # configs[3]'s 3840x2160 frame on this one GPU: the single-GPU reference of the strong
     # split the N > 1 lines run (their per-GPU efficiency is value_N / (N x this value))
@@ -467,6 +492,8 @@ def main():
     else:
         workload = f"{args.scene} {pipeline} {W}x{H}, 1 spp/frame" + (" (configs[2])" if pipeline == "reuse" and
                                                                         (W, H) == (1920, 1080) else "")
+    if args.camera_path:
+        workload += ", camera moving every frame (bench.camera_pose: 5 units/s at 60 Hz + a turn; history reprojected)"
     line = {
         "metric": "Msamples/sec at 1920x1080, 1 spp ReSTIR DI; per-pixel L2 vs WebGPU ref",
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
@@ -563,7 +590,7 @@ def one_gpu_rate(cs, W, H, pipeline, device, steps, warmup):
             "note": "configs[3]'s frame on ONE GPU: the reference for the N-GPU strong split"}
 
 
-def cpu_baseline(cs, W, H, pipeline, threads, device=0):
+def cpu_baseline(cs, W, H, pipeline, threads, device=0, camera_path=False):
     """The C oracle (a port of the WGSL + the reuse passes) on the host cores, timed over
     whole frames: one frame (restir / mcpt), two for reuse / GI (the second with its history).
 
@@ -579,10 +606,19 @@ def cpu_baseline(cs, W, H, pipeline, threads, device=0):
     u = cs.uniform(W, H, cam.view_projection_inverse(), cam.location, 1)
     nf = 2 if pipeline in ("reuse", "gi") else 1
 
+    def pose_uniform(f):
+        c = Camera(W, H)
+        loc, yaw = camera_pose(f - 1)
+        c.set_location(*loc)
+        c.set_yaw(yaw)
+        return cs.uniform(W, H, c.view_projection_inverse(), c.location, f)
+
     def full_frames(nthreads, rect=None):
-        fr = O.Frame(u, cs.scene, cs.geometry, cs.accel)
+        fr = O.Frame(pose_uniform(1) if camera_path else u, cs.scene, cs.geometry, cs.accel)
         t0 = time.perf_counter()
         for f in range(1, nf + 1):
+            if camera_path:
+                fr.set_camera(pose_uniform(f))
             fr.set_frame_index(f)
             if pipeline == "reuse":
                 fr.run_reuse_frame(threads=nthreads, rect=rect)
@@ -609,19 +645,21 @@ def cpu_baseline(cs, W, H, pipeline, threads, device=0):
                              "sample": f"rows {y0}..{y0 + rows} of the same {nf} frame(s), 1 thread",
                              "seconds": round(dt1, 2)}}
     try:
-        out["parity"] = frame_parity(cs, W, H, pipeline, device, nf, fr)
+        out["parity"] = frame_parity(cs, W, H, pipeline, device, nf, fr, camera_path)
     except Exception as e:  # noqa: BLE001 -- reported, never hidden
         out["parity"] = {"error": f"{type(e).__name__}: {e}"}
     return out
 
 
-def frame_parity(cs, W, H, pipeline, device, nf, fr):
+def frame_parity(cs, W, H, pipeline, device, nf, fr, camera_path=False):
     """The benched configuration's first `nf` frames on a fresh handle vs the oracle's frames
-    `fr` (same scene, size, camera, FrameIndex 1..nf): bit-exactness and relative L2."""
+    `fr` (same scene, size, camera (path), FrameIndex 1..nf): bit-exactness and relative L2."""
     from pathtracerdemo_amd.renderer import Renderer
     r = Renderer(W, H, device=device, pipeline=pipeline)
     r.Initialize(cs)
-    for _ in range(nf):
+    for k in range(nf):
+        if camera_path:
+            set_pose(r, k)
         r.Update()
         r.Render()
     img = r.read_image()
@@ -641,7 +679,8 @@ def frame_parity(cs, W, H, pipeline, device, nf, fr):
         bit_exact = bit_exact and nres == 0
     out["bit_exact"] = bit_exact
     out["compared"] = ("the whole image" + (" + all 32 words of every spatial-output reservoir" if hist is not None
-                                             else "") + f" of frames 1..{nf} on the GPU vs the C oracle")
+                                             else "") + f" of frames 1..{nf} on the GPU vs the C oracle"
+                       + (" (camera moving between them)" if camera_path else ""))
     return out
 
 

@@ -71,6 +71,11 @@ def lib(variant: str = ""):
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P,
                                        ctypes.POINTER(ReuseParams), ctypes.POINTER(Counters)]
         _lib.pto_run_reuse.restype = ctypes.c_int
+        _lib.pto_run_temporal_motion.argtypes = [ctypes.c_int, ctypes.POINTER(Inputs), ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int, P, P, P, P, P,
+                                                 ctypes.POINTER(ReuseParams), ctypes.POINTER(Counters)]
+        _lib.pto_run_temporal_motion.restype = ctypes.c_int
+        _lib.pto_mat4_inverse.argtypes = [P, P]
         _lib.pto_run_gi.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Inputs), ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, P, P, P, P, P, ctypes.POINTER(ReuseParams),
                                     ctypes.POINTER(Counters)]
@@ -117,6 +122,10 @@ class Frame:
         self.accum = np.zeros((self.H, self.W, 4), dtype=np.float32)
         self.res_hist = np.zeros((self.H, self.W, 32), dtype=np.uint32)  # spatial output / history
         self.hist_valid = False
+        # the frame the history was rendered with (temporal reuse under camera motion: its
+        # uniform words -- camera -- and G-buffer; pto_run_temporal_motion)
+        self.prev_uniform = self.uniform.copy()
+        self.prev_gbuffer = np.zeros_like(self.gbuffer)
         self.reuse = (REUSE_RADIUS, REUSE_NEIGHBORS, TEMPORAL_CAP)
         # ReSTIR GI buffers: candidate / temporal reservoirs, spatial output (= history), direct light
         self.gi_res = np.zeros((self.H, self.W, GI_WORDS), dtype=np.uint32)
@@ -126,6 +135,31 @@ class Frame:
 
     def set_frame_index(self, f: int):
         self.uniform[23] = f
+
+    def set_camera(self, uniform: np.ndarray):
+        """A new camera (the uniform's words 4..22: VP^-1 and position); the history stays (it
+        is reprojected: motion_moved)."""
+        self.uniform[4:23] = np.asarray(uniform, dtype=np.uint32)[4:23]
+
+    def camera_moved(self) -> bool:
+        return bool(np.any(self.uniform[4:23] != self.prev_uniform[4:23]))
+
+    def run_temporal_motion(self, threads: int = 0, rect=None) -> dict:
+        """Temporal reuse with the history at each pixel's reprojection in the previous frame
+        (prev_uniform, prev_gbuffer; pt_oracle.c temporal_motion_pixel)."""
+        threads = threads or os.cpu_count() or 1
+        x0, y0, x1, y1 = rect if rect is not None else (0, 0, self.W, self.H)
+        r, m, cap = self.reuse
+        prm = ReuseParams(r, m, cap, 1 if self.hist_valid else 0)
+        cnt = Counters()
+        rc = lib(self.variant).pto_run_temporal_motion(threads, ctypes.byref(self._inputs()), x0, y0, x1, y1,
+                                                      _ptr(self.gbuffer), _ptr(self.reservoir), _ptr(self.res_hist),
+                                                      _ptr(self.prev_uniform), _ptr(self.prev_gbuffer),
+                                                      ctypes.byref(prm), ctypes.byref(cnt))
+        if rc != 0:
+            raise RuntimeError(f"oracle motion temporal pass failed ({rc})")
+        self.counters["temporal_motion"] = cnt.as_dict()
+        return self.counters["temporal_motion"]
 
     def trace(self, rays: np.ndarray, eps_mode: int = 1, return_counters: bool = False):
         """Closest hits for (n, 8) f32 rays, same format as ptx_trace (+ the traversal work)."""
@@ -168,12 +202,21 @@ class Frame:
 
     def run_reuse_frame(self, threads: int = 0, rect=None) -> None:
         """One frame of the reuse pipeline: G-buffer -> PT_1 -> temporal -> spatial -> PT_4.
-        The caller keeps the camera fixed between frames (history stays valid) or clears
-        `hist_valid` (ptx_set_frame does the same on a camera change)."""
-        for p in (PASS_GBUFFER, PASS_INIT, PASS_TEMPORAL, PASS_SPATIAL):
+        A camera moved since the history's frame (set_camera) reprojects the history
+        (run_temporal_motion) instead of the same-pixel temporal pass; clearing `hist_valid`
+        drops it (ptx_upload_scene / ptx_reset_accumulation do)."""
+        moved = self.hist_valid and self.camera_moved()
+        for p in (PASS_GBUFFER, PASS_INIT):
             self.run(p, threads, rect)
+        if moved:
+            self.run_temporal_motion(threads, rect)
+        else:
+            self.run(PASS_TEMPORAL, threads, rect)
+        self.run(PASS_SPATIAL, threads, rect)
         self.run(PASS_FINAL, threads, rect, reservoir=self.res_hist)
         self.hist_valid = True
+        self.prev_uniform = self.uniform.copy()
+        self.prev_gbuffer[...] = self.gbuffer
 
 
     def run_reuse_frame_census(self, threads: int = 0) -> np.ndarray:

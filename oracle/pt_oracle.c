@@ -1184,6 +1184,155 @@ static void temporal_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t *cur,
     write_reused(cur, src, p_sel, q_sel, f_sel, w_sum, 1u + Cp);
 }
 
+/* ---- temporal reuse under camera motion (build-defined; ReSTIR_Pipeline.md:259-340) ----
+ * The spec's history is ReservoirBuffer_Prev[CurrentPixel - MotionVector]: the previous
+ * frame's spatial output at the pixel p' the current primary hit projected to in the previous
+ * frame, whose sample lives in the PREVIOUS frame's domain (its camera point x0' and primary
+ * hit x1' at p').  Rules (restated bit for bit by wtmotion_* in ptx_reuse.hip):
+ *  - VP' = the f32 rounding of the double-precision inverse of the previous VP^-1
+ *    (pto_mat4_inverse: cofactors along the first column, one fixed operation order);
+ *  - p' = floor(((VP' (P, 1)).xy / w + 1) * 0.5 * (W, H)), P = the current primary hit;
+ *    none when w <= 0 or p' is outside the image (a disocclusion past the border);
+ *  - the history is used iff x1' exists, n(x1') . n(x1) >= 0.9 and the depths along the
+ *    previous view agree within 5 %: | |x1' - x0'| - |P - x0'| | <= 0.05 |P - x0'| (geometry
+ *    only: the confidence never depends on a sample);
+ *  - MIS: the generalized balance heuristic with confidences (the spec's m_i) = the spatial
+ *    pass's pairwise rule with M = 1: the history sample shifted here (random replay, its
+ *    Jacobian q_h / q_c), the canonical sample shifted into the previous domain for its own
+ *    weight; c_c = 1, c_h = min(C_hist, cap); canonical draw first, then the history. */
+typedef struct pto_motion {
+    const uint32_t *prev_uniform;  /* the previous frame's 33 words (its VP^-1, camera position) */
+    const uint32_t *gbuffer_prev;  /* the previous frame's G-buffer (W*H*4)                      */
+} pto_motion;
+
+/* 4x4 inverse (column-major f32 in, f32 out) in double precision by cofactors (zeros when
+ * singular) -- the host side of the reprojection; ptx_api.cpp uses the same expression order. */
+void pto_mat4_inverse(const float *mf, float *out) {
+    double m[16], inv[16];
+    for (int i = 0; i < 16; ++i) m[i] = (double)mf[i];
+    inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    const double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+    for (int i = 0; i < 16; ++i) out[i] = det != 0.0 ? (float)(inv[i] / det) : 0.0f;
+}
+
+/* p' of world point P through the previous frame's VP (column-major f32): 0 if none */
+static int reproject(const float *vp, v3 P, uint32_t W, uint32_t H, uint32_t *px, uint32_t *py) {
+    const float cx = ((vp[0] * P.x + vp[4] * P.y) + vp[8] * P.z) + vp[12];
+    const float cy = ((vp[1] * P.x + vp[5] * P.y) + vp[9] * P.z) + vp[13];
+    const float cw = ((vp[3] * P.x + vp[7] * P.y) + vp[11] * P.z) + vp[15];
+    if (!(cw > 0.0f)) return 0;
+    const float fx = ((cx / cw + 1.0f) * 0.5f) * (float)W, fy = ((cy / cw + 1.0f) * 0.5f) * (float)H;
+    if (!(fx >= 0.0f && fx < (float)W && fy >= 0.0f && fy < (float)H)) return 0;
+    *px = (uint32_t)fx;
+    *py = (uint32_t)fy;
+    return 1;
+}
+/* the disocclusion test of the history at p' (x1' = Sp with camera point x0p) for the
+ * current primary hit P with normal Nc */
+static int motion_valid(const surface *Sp, v3 x0p, v3 P, v3 Nc) {
+    if (!(vdot(Sp->nrm, Nc) >= 0.9f)) return 0;
+    const float dp = vlength(vsub(Sp->pos, x0p)), dc = vlength(vsub(P, x0p));
+    return fabsf(dp - dc) <= 0.05f * dc;
+}
+
+static void temporal_motion_pixel(const ctx *c, const ctx *cprev, const float *vp_prev, const uint32_t *gbuffer,
+                                  uint32_t *cur, const uint32_t *hist_all, const uint32_t *gbuffer_prev,
+                                  const pto_reuse_params *prm, uint32_t x, uint32_t y) {
+    const uint32_t W = c->U[U_W], H = c->U[U_H];
+    compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
+    if (!x1.valid) return; /* PT_1 wrote the zero reservoir; PT_4 never reads it */
+    uint32_t seed = reuse_seed(c, x, y, SALT_TEMPORAL);
+    eval_out ec = eval_sample(c, x, y, x1, cur);
+    const int canon_ok = ec.valid && ec.phat > 0.0f;
+    const float cc = 1.0f, pc = ec.phat, qc = ec.q, Wc = f32_of(cur[28]);
+    /* the history pixel p' and its domain */
+    uint32_t Cp = 0u, px = 0u, py = 0u;
+    compact x1p = {0u, 0u, 0u, 0u, 0.0f, 0.0f};
+    const uint32_t *h = NULL;
+    if (prm->hist_valid) {
+        const surface S1 = get_surface(c, x1);
+        if (reproject(vp_prev, S1.pos, W, H, &px, &py)) {
+            x1p = decode_compact(gbuffer_prev + 4u * (py * W + px));
+            if (x1p.valid) {
+                const surface Sp = get_surface(c, x1p);
+                if (motion_valid(&Sp, get_x0(cprev, px, py), S1.pos, S1.nrm)) {
+                    h = hist_all + PTO_RESERVOIR_WORDS * (py * W + px);
+                    Cp = h[29] < prm->temporal_cap ? h[29] : prm->temporal_cap;
+                }
+            }
+        }
+    }
+    const float cp = (float)Cp;
+    /* forward: the history sample in this pixel's domain */
+    float wh = 0.0f, pf = 0.0f, qf = 0.0f;
+    sel_f ff = {0, {0.0f, 0.0f, 0.0f}};
+    if (Cp != 0u && h[23] >= 2u && f32_of(h[24]) > 0.0f) {
+        const float ph = f32_of(h[24]), qh = f32_of(h[25]), Wh = f32_of(h[28]);
+        eval_out F = eval_sample(c, x, y, x1, h);
+        if (F.valid) {
+            const float J = qh / F.q;
+            const float pb = ph / J;
+            const float den = cc * F.phat + cp * pb;
+            const float m = den > 0.0f ? (cp * pb) / den : 0.0f;
+            wh = m * F.phat * Wh * J;
+            pf = F.phat;
+            qf = F.q;
+            ff = eval_f(F);
+        }
+    }
+    /* backward: this pixel's sample in the previous domain (its weight) */
+    float Q = 1.0f;
+    if (canon_ok && Cp != 0u) {
+        eval_out B = eval_sample(cprev, px, py, x1p, cur);
+        if (B.valid) {
+            const float pbc = B.phat * qc / B.q;
+            const float den = cc * pc + cp * pbc;
+            Q = den > 0.0f ? (cc * pc) / den : 1.0f;
+        }
+    }
+    const float wc = canon_ok ? Q * pc * Wc : 0.0f;
+    float w_sum = 0.0f, p_sel = ec.phat, q_sel = ec.q;
+    const uint32_t *src = cur;
+    sel_f f_sel = eval_f(ec);
+    if (wrs_update(&w_sum, wc, &seed)) { src = cur; p_sel = ec.phat; q_sel = ec.q; f_sel = eval_f(ec); }
+    if (wrs_update(&w_sum, wh, &seed)) { src = h; p_sel = pf; q_sel = qf; f_sel = ff; }
+    write_reused(cur, src, p_sel, q_sel, f_sel, w_sum, 1u + Cp);
+}
+
+void pto_temporal_motion(const pto_inputs *in, const pto_motion *mot, const uint32_t *gbuffer, uint32_t *res_cur,
+                         const uint32_t *res_hist, const pto_reuse_params *prm, int x0, int y0, int x1, int y1,
+                         pto_counters *cnt) {
+    ctx c, cprev;
+    ctx_init(&c, in, EPS_FINAL, cnt);
+    pto_inputs pin = *in;
+    pin.uniform = mot->prev_uniform;
+    ctx_init(&cprev, &pin, EPS_FINAL, cnt);
+    float vp_prev[16];
+    pto_mat4_inverse((const float *)(mot->prev_uniform + U_VPINV), vp_prev);
+    const uint32_t W = c.U[U_W];
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            const uint32_t p = (uint32_t)y * W + (uint32_t)x;
+            temporal_motion_pixel(&c, &cprev, vp_prev, gbuffer, res_cur + PTO_RESERVOIR_WORDS * p, res_hist,
+                                  mot->gbuffer_prev, prm, (uint32_t)x, (uint32_t)y);
+        }
+}
+
 /* Spatial neighbour k of (x, y): two draws, offsets in [-R, R]^2. Returns 1 if inside the
  * image and not the pixel itself. */
 static int spatial_neighbor(uint32_t *seed, uint32_t R, uint32_t x, uint32_t y, uint32_t W, uint32_t H,
@@ -1441,6 +1590,7 @@ typedef struct job {
     float *accum;
     const pto_reuse_params *prm;
     pto_counters cnt;
+    const pto_motion *mot;
 } job;
 
 static void *worker(void *arg) {
@@ -1453,21 +1603,33 @@ static void *worker(void *arg) {
         case 3: pto_mcpt(j->in, j->x0, y, j->x1, y + 1, j->accum, &j->cnt); break;
         case 5: pto_temporal(j->in, j->gbuffer, j->reservoir, j->res_hist, j->prm, j->x0, y, j->x1, y + 1, &j->cnt); break;
         case 6: pto_spatial(j->in, j->gbuffer, j->reservoir, j->res_hist, j->prm, j->x0, y, j->x1, y + 1, &j->cnt); break;
+        case 7:
+            pto_temporal_motion(j->in, j->mot, j->gbuffer, j->reservoir, j->res_hist, j->prm, j->x0, y, j->x1, y + 1,
+                                &j->cnt);
+            break;
         default: break;
         }
     }
     return NULL;
 }
 
+static int run_pass_m(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                      uint32_t *gbuffer, uint32_t *reservoir, uint32_t *res_hist, const pto_reuse_params *prm,
+                      float *accum, pto_counters *cnt, const pto_motion *mot);
 static int run_pass(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
                     uint32_t *gbuffer, uint32_t *reservoir, uint32_t *res_hist, const pto_reuse_params *prm,
                     float *accum, pto_counters *cnt) {
+    return run_pass_m(pass, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, res_hist, prm, accum, cnt, NULL);
+}
+static int run_pass_m(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                      uint32_t *gbuffer, uint32_t *reservoir, uint32_t *res_hist, const pto_reuse_params *prm,
+                      float *accum, pto_counters *cnt, const pto_motion *mot) {
     if (nthreads < 1) nthreads = 1;
     job *jobs = (job *)calloc((size_t)nthreads, sizeof(job));
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     if (!jobs || !th) { free(jobs); free(th); return -1; }
     for (int t = 0; t < nthreads; ++t) {
-        job j = {pass, t, nthreads, x0, y0, x1, y1, in, gbuffer, reservoir, res_hist, accum, prm, {0, 0, 0, 0, 0}};
+        job j = {pass, t, nthreads, x0, y0, x1, y1, in, gbuffer, reservoir, res_hist, accum, prm, {0, 0, 0, 0, 0}, mot};
         jobs[t] = j;
         if (nthreads > 1) pthread_create(&th[t], NULL, worker, &jobs[t]);
     }
@@ -1504,5 +1666,15 @@ int pto_run_reuse(int pass, int nthreads, const pto_inputs *in, int x0, int y0, 
                   pto_counters *cnt) {
     if ((pass != 5 && pass != 6) || !prm || prm->neighbors > 16u) return -2;
     return run_pass(pass, nthreads, in, x0, y0, x1, y1, (uint32_t *)gbuffer, res_cur, res_hist, prm, NULL, cnt);
+}
+/* pass 7: temporal reuse under camera motion (temporal_motion_pixel) */
+int pto_run_temporal_motion(int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                            const uint32_t *gbuffer, uint32_t *res_cur, const uint32_t *res_hist,
+                            const uint32_t *prev_uniform, const uint32_t *gbuffer_prev, const pto_reuse_params *prm,
+                            pto_counters *cnt) {
+    if (!prm || !prev_uniform || !gbuffer_prev) return -2;
+    pto_motion mot = {prev_uniform, gbuffer_prev};
+    return run_pass_m(7, nthreads, in, x0, y0, x1, y1, (uint32_t *)gbuffer, res_cur, (uint32_t *)res_hist, prm, NULL,
+                      cnt, &mot);
 }
 #include "pt_oracle_gi.c"

@@ -78,6 +78,14 @@ typedef struct pto_reuse_params {
 /* temporal: res_cur (PT_1 output) updated in place from res_hist (previous spatial output) */
 void pto_temporal(const pto_inputs *in, const uint32_t *gbuffer, uint32_t *res_cur, const uint32_t *res_hist,
                   const pto_reuse_params *prm, int x0, int y0, int x1, int y1, pto_counters *cnt);
+/* temporal under camera motion: res_cur (PT_1 output) updated in place from the previous
+ * frame's spatial output res_hist at each pixel's reprojection, in the previous frame's domain
+ * (prev_uniform: its 33 words; gbuffer_prev: its G-buffer).  pt_oracle.c temporal_motion_pixel. */
+int pto_run_temporal_motion(int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                            const uint32_t *gbuffer, uint32_t *res_cur, const uint32_t *res_hist,
+                            const uint32_t *prev_uniform, const uint32_t *gbuffer_prev, const pto_reuse_params *prm,
+                            pto_counters *cnt);
+void pto_mat4_inverse(const float *m /* 16, column-major */, float *out /* 16 */);
 /* spatial: reads res_cur of the pixel and its neighbours, writes res_out (PT_4's input) */
 void pto_spatial(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *res_cur, uint32_t *res_out,
                  const pto_reuse_params *prm, int x0, int y0, int x1, int y1, pto_counters *cnt);

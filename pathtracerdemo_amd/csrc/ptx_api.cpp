@@ -416,12 +416,16 @@ static uint32_t seg_pixels(const ptx_handle *h) {
     return p;
 }
 
+// shift jobs per pixel the DI reuse passes may hold at once: the spatial pass's 2M, the motion
+// temporal pass's kMotionJobs
+static size_t reuse_jobs_per_px(const ptx_handle *h) { return std::max<size_t>(2u * h->reuse_neighbors, kMotionJobs); }
 // Wavefront buffers, sized for the largest round: PT_1 emits <= 2 rays per pixel, PT_4
 // <= 1, TEST_MCPT <= LightCount + 1 (all shadow rays of a vertex + the next path ray).
 int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t npix = (size_t)h->band_h * h->cfg.width;
     const uint32_t nl = h->uniform[U_LIGHT_COUNT];
-    const size_t jpp = has_reuse(h) ? 2u * h->reuse_neighbors : 1u;
+    const size_t jpp = !has_reuse(h) ? 1u : h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI ? 2u * h->reuse_neighbors
+                                                                                         : reuse_jobs_per_px(h);
     const size_t per_px = std::max<size_t>(std::max<size_t>(2u, (size_t)nl + 1u), jpp);
     const size_t padded = (size_t)((h->cfg.width + 7u) / 8u) * ((h->band_h + 7u) / 8u) * 64u;
     const uint32_t seg_px = seg_pixels(h);
@@ -517,7 +521,8 @@ static size_t px_with_halo(const ptx_handle *h) {
     return (size_t)(h->halo_top + h->band_h + h->halo_bot) * h->cfg.width;
 }
 int reuse_buffers(ptx_handle *h) {
-    const size_t njobs = (size_t)h->band_h * h->cfg.width * 2u * h->reuse_neighbors;
+    const size_t njobs = (size_t)h->band_h * h->cfg.width *
+                         (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI ? 2u * h->reuse_neighbors : reuse_jobs_per_px(h));
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) return alloc_buf(h, h->d_jres, njobs * 4u);  // ray index per job
     if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
     if (int rc = alloc_buf(h, h->d_nbr, px_with_halo(h) * 16u)) return rc;
@@ -542,7 +547,8 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     A.radius = h->reuse_radius;
     A.neighbors = h->reuse_neighbors;
     A.cap = h->temporal_cap;
-    A.hist_valid = h->hist_valid ? 1u : 0u;
+    // (a moved camera's history is only usable through the motion pass: motion_args)
+    A.hist_valid = h->hist_valid && !h->hist_moved ? 1u : 0u;
     A.use_init = (pass == PTX_PASS_TEMPORAL && h->init_state_valid) ? 1u : 0u;
     A.nbr_out = (uint4 *)h->d_nbr.p + (size_t)h->halo_top * h->cfg.width;
     A.nbr = A.nbr_out;
@@ -550,6 +556,26 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     static const bool fold_off = ab_knob("FOLD_LAST_STEP", 1) == 0;  // A/B
     A.fold_last = ((pass == PTX_PASS_SPATIAL || pass == PTX_PASS_TEMPORAL) && !fold_off) ? 1u : 0u;
     A.ray_cap = (uint32_t)std::min<size_t>(h->wave_ray_cap, 0xffffffffu);
+    return A;
+}
+
+// The motion temporal pass (wtmotion_*): the spatial pass's shift-job buffers (free again once
+// the previous frame's spatial pass is done, which this pass waits for like the still one), the
+// history reprojected through the previous frame's camera.
+void mat4_inverse(const float *mf, float *out);
+static ReuseArgs motion_args(ptx_handle *h) {
+    ReuseArgs A = reuse_args(h, PTX_PASS_SPATIAL);
+    A.jpp = (uint32_t)reuse_jobs_per_px(h);
+    A.njobs = h->band_h * h->cfg.width * A.jpp;
+    static const bool planes = ab_knob("JOB_PLANES", 1) != 0;
+    A.jpx = planes ? 1u : A.jpp;
+    A.hist_valid = h->hist_valid ? 1u : 0u;
+    A.use_init = h->init_state_valid ? 1u : 0u;
+    A.fold_last = 0u;
+    A.motion = 1u;
+    std::memcpy(A.vpinv_prev, h->hist_camera, sizeof A.vpinv_prev);  // (words 4..19 of that frame)
+    mat4_inverse(A.vpinv_prev, A.vp_prev);
+    A.psurf = (const uint4 *)h->d_psurf.p;
     return A;
 }
 
@@ -600,9 +626,10 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         return e;
     }
     if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL || pass == kPassTemporalJobs ||
-        pass == kPassTemporalCombine) {
+        pass == kPassTemporalCombine || pass == kPassTemporalMotion) {
         const bool temporal = pass != PTX_PASS_SPATIAL;
-        ReuseArgs A = reuse_args(h, temporal ? PTX_PASS_TEMPORAL : PTX_PASS_SPATIAL);
+        ReuseArgs A = pass == kPassTemporalMotion ? motion_args(h)
+                                                  : reuse_args(h, temporal ? PTX_PASS_TEMPORAL : PTX_PASS_SPATIAL);
         WaveBufs wj = w;
         if (A.fold_last && wj.res[2]) wj.nres = 3;  // light segments finished by the combine
         else A.fold_last = 0u;
@@ -712,7 +739,7 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
         if (passes[i] == PTX_PASS_SPATIAL) {
             if (summaries && (e = spatial_summaries(h, h->stream)) != hipSuccess) return e;
         } else if (passes[i] != PTX_PASS_FINAL && passes[i] != PTX_PASS_TEMPORAL && passes[i] != kPassTemporalJobs &&
-                   passes[i] != kPassTemporalCombine) {
+                   passes[i] != kPassTemporalCombine && passes[i] != kPassTemporalMotion) {
             h->nbr_valid = false;  // G-buffer / PT_1 / MCPT rewrite what the summaries describe
         }
     }
@@ -723,7 +750,8 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     for (int i = 0; i < npasses && i < 8; ++i) {
         if (passes[i] == PTX_PASS_GBUFFER) surf_ok = false;
         else if (passes[i] == PTX_PASS_INIT && w.surf) surf_ok = true;
-        else if ((passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalJobs || passes[i] == PTX_PASS_SPATIAL) &&
+        else if ((passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalJobs || passes[i] == PTX_PASS_SPATIAL ||
+                  passes[i] == kPassTemporalMotion) &&
                  w.surf) {
             need_surf[i] = !surf_ok;
             surf_ok = true;
@@ -760,6 +788,18 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
             part.dyn = !use_dyn ? nullptr
                                : (uint32_t *)h->d_wctr.p + 2u * kWaveMaxRounds * ws.cnt_stride +
                                      (uint32_t)((set * ptx_handle::kMaxSplit + q) * kWaveMaxRounds) * kDynRoundWords;
+            // the launch sequence's restart pools (its dynamic-batch trace launches: <= kDynMaxGroups
+            // workgroups of WB / 64 waves; sequences run concurrently, so each has its own).
+            // PTX_AB=RESTART_POOL=0: every restart in place (A/B)
+            static const bool pool_on = ab_knob("RESTART_POOL", 1) != 0;
+            part.pool = nullptr;
+            if (use_dyn && pool_on) {
+                const size_t per_set = (size_t)kDynMaxGroups * (kBlock / 64) * 2u * kRestartCap;  // float4s
+                if (!h->d_wpool.p && (e = hipMalloc(&h->d_wpool.p, kRestartPoolSets * per_set * 16u)) != hipSuccess)
+                    return e;
+                h->d_wpool.bytes = kRestartPoolSets * per_set * 16u;
+                part.pool = (float4 *)h->d_wpool.p + (size_t)(set * ptx_handle::kMaxSplit + q) * per_set;
+            }
             part.seg_base = (uint32_t)((uint64_t)ws.nseg * q / k);
             part.seg_count = (uint32_t)((uint64_t)ws.nseg * (q + 1) / k) - part.seg_base;
             if (!part.seg_count) continue;
@@ -788,7 +828,7 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     }
     // the temporal pass rewrote the reservoirs PT_1's state describes, and summarised them
     for (int i = 0; i < npasses; ++i)
-        if (passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalCombine) {
+        if (passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalCombine || passes[i] == kPassTemporalMotion) {
             h->init_state_valid = false;
             h->nbr_valid = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
         }
@@ -803,6 +843,48 @@ static hipError_t launch_wave_pass(ptx_handle *h, const Scene &sc, const WaveBuf
 void mark_history(ptx_handle *h) {
     std::memcpy(h->hist_camera, h->uniform + 4, sizeof h->hist_camera);
     h->hist_valid = true;
+    h->hist_moved = false;
+}
+
+// 4x4 inverse of a column-major f32 matrix in double by cofactors, rounded to f32 (zeros when
+// singular): the previous frame's VP for the motion pass's reprojection.  The same expressions
+// in the same order as the oracle's pto_mat4_inverse (both built without FMA contraction), so
+// the kernels and the oracle reproject through the same f32 matrix.
+void mat4_inverse(const float *mf, float *out) {
+    double m[16], inv[16];
+    for (int i = 0; i < 16; ++i) m[i] = (double)mf[i];
+    inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    const double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+    for (int i = 0; i < 16; ++i) out[i] = det != 0.0 ? (float)(inv[i] / det) : 0.0f;
+}
+
+// Before a moved-camera frame's passes: the previous frame's surface records -> d_psurf, on the
+// stream of that frame (`st`, ordered after its PT_1; a pipelined frame's next G-buffer on that
+// stream comes after the copy).  Whole-image DI reuse handles only (ptx_set_frame).
+static int motion_prepare(ptx_handle *h, hipStream_t st) {
+    if (!h->d_surf.p) {  // (no surface records yet: nothing to reproject)
+        h->hist_valid = false;
+        h->hist_moved = false;
+        return PTX_OK;
+    }
+    if (int rc = alloc_buf(h, h->d_psurf, h->d_surf.bytes)) return rc;
+    HIP_CHECK(h, hipMemcpyAsync(h->d_psurf.p, h->d_surf.p, h->d_surf.bytes, hipMemcpyDeviceToDevice, st));
+    return PTX_OK;
 }
 
 // ---------------------------------------------------------------- frame pipelining
@@ -874,6 +956,7 @@ static void swap_two(ptx_handle *h) {
     std::swap(h->d_wact0, a.wact0);
     std::swap(h->d_wact1, a.wact1);
     std::swap(h->d_wctr, a.wctr);
+    std::swap(h->d_wpool, a.wpool);
     std::swap(h->wave_ray_cap, a.wave_ray_cap);
     std::swap(h->wave_slots, a.wave_slots);
     std::swap(h->stream, a.stream);
@@ -938,6 +1021,13 @@ static int timed_wave_frame(ptx_handle *h) {
     Scene sc = make_scene(h);
     if (!tables_fit_lds(sc)) return 1;
     const bool pipe = pipelined(h);
+    // a moved camera (whole-image DI reuse): the history is reprojected, from the previous
+    // frame's surface records, copied first on that frame's stream (the current one here)
+    bool moved = h->hist_valid && h->hist_moved && has_reuse(h) && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
+    if (moved) {
+        if (int rc = motion_prepare(h, h->stream)) return rc;
+        moved = h->hist_moved;
+    }
     if (pipe) {
         // frame N goes to the other context; ev_prev marks everything enqueued before it
         // (frame N-1 and any host operation since) on the current context's stream
@@ -958,13 +1048,16 @@ static int timed_wave_frame(ptx_handle *h) {
         if (int rc = reuse_buffers(h)) return rc;
         // (the temporal pass's shift jobs read only this frame's PT_1 output: they run before the
         // wait, its combine after; PTX_AB=TEMPORAL_SPLIT=0: the whole pass after the wait)
+        // (a moved camera: the whole motion temporal pass after the wait -- its history jobs read
+        // the previous frame's spatial output)
         static const bool split = ab_knob("TEMPORAL_SPLIT", 1) != 0;
         static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, kPassTemporalJobs};
         static const int temporal[1] = {PTX_PASS_TEMPORAL}, temporal_b[1] = {kPassTemporalCombine};
+        static const int temporal_m[1] = {kPassTemporalMotion};
         static const int back[2] = {PTX_PASS_SPATIAL, PTX_PASS_FINAL};
-        e = launch_wave_parts(h, sc, w, front, split ? 3 : 2);
+        e = launch_wave_parts(h, sc, w, front, split && !moved ? 3 : 2);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
-        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, split ? temporal_b : temporal, 1);
+        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, moved ? temporal_m : split ? temporal_b : temporal, 1);
         if (e == hipSuccess) e = launch_wave_parts(h, sc, w, back, 2);
         if (e == hipSuccess) mark_history(h);
     } else if (has_reuse(h)) {
@@ -972,8 +1065,9 @@ static int timed_wave_frame(ptx_handle *h) {
         // the spatial pass reads neighbours) spatial + PT_4
         if (int rc = reuse_buffers(h)) return rc;
         static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_TEMPORAL};
+        static const int front_m[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, kPassTemporalMotion};
         static const int back[2] = {PTX_PASS_SPATIAL, PTX_PASS_FINAL};
-        e = launch_wave_parts(h, sc, w, front, 3);
+        e = launch_wave_parts(h, sc, w, moved ? front_m : front, 3);
         if (e == hipSuccess) e = launch_wave_parts(h, sc, w, back, 2);
         if (e == hipSuccess) mark_history(h);
     } else {
@@ -1194,8 +1288,12 @@ int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]) {
     }
     std::memcpy(h->uniform, uniform, sizeof h->uniform);
     h->frame_set = true;
-    // temporal history is reusable only for the camera (and scene) that produced it
-    if (std::memcmp(h->hist_camera, uniform + 4, sizeof h->hist_camera) != 0) h->hist_valid = false;
+    // temporal history: a whole-image DI reuse handle reprojects it when the camera moved (the
+    // motion temporal pass); elsewhere it is reusable only for the camera that produced it
+    // (GI's temporal pass and band handles: dropped)
+    h->hist_moved = std::memcmp(h->hist_camera, uniform + 4, sizeof h->hist_camera) != 0;
+    const bool whole = h->band_h == h->cfg.height && !h->halo_top && !h->halo_bot && !h->comm;
+    if (h->hist_moved && !(whole && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE)) h->hist_valid = false;
     if (h->scene_loaded && !h->layout_valid) return build_layout(h);
     return PTX_OK;
 }
@@ -1365,7 +1463,7 @@ int ptx_get_stats(ptx_handle *h, ptx_stats *out) {
     out->max_bvh_depth = h->max_depth;
     out->device_bytes = h->d_scene.bytes + h->d_geometry.bytes + h->d_tris.bytes + h->d_nodes.bytes +
                         h->d_subs.bytes + h->d_insts.bytes + h->d_mats.bytes + h->d_tverts.bytes + h->d_gbuf.bytes + h->d_res.bytes + h->d_accum.bytes +
-                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_tjstate.bytes + h->d_tjres.bytes + h->d_nbr.bytes + h->d_surf.bytes + h->d_direct.bytes;
+                        h->d_hist.bytes + h->d_jstate.bytes + h->d_jres.bytes + h->d_tjstate.bytes + h->d_tjres.bytes + h->d_nbr.bytes + h->d_surf.bytes + h->d_psurf.bytes + h->d_direct.bytes;
     return PTX_OK;
 }
 
@@ -1533,13 +1631,13 @@ int ptx_destroy(ptx_handle *h) {
     if (h->host_stage) (void)hipHostFree(h->host_stage);
     for (DevBuf *b : {&h->d_canvas, &h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
-                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wres2, &h->d_wact0, &h->d_wact1, &h->d_wctr,
-                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_tjstate, &h->d_tjres, &h->d_nbr, &h->d_surf, &h->d_direct, &h->d_census})
+                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wres2, &h->d_wact0, &h->d_wact1, &h->d_wctr, &h->d_wpool,
+                      &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_tjstate, &h->d_tjres, &h->d_nbr, &h->d_surf, &h->d_psurf, &h->d_direct, &h->d_census})
         free_buf(*b);
     for (ptx_handle::FrameCtx *ap : {&h->alt, &h->alt2}) {
         ptx_handle::FrameCtx &a = *ap;
         for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wres2, &a.wact0, &a.wact1,
-                          &a.wctr, &a.tjstate, &a.tjres})
+                          &a.wctr, &a.wpool, &a.tjstate, &a.tjres})
             free_buf(*b);
         if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
         for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

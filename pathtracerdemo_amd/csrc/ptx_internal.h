@@ -30,6 +30,8 @@ using namespace ptx;
 // previous frame's spatial output) -- so a pipelined frame runs the jobs before waiting for
 // the previous frame.
 constexpr int kPassTemporalJobs = 0x100, kPassTemporalCombine = 0x101;
+// the temporal pass of a frame whose camera moved since the history's (wtmotion_*)
+constexpr int kPassTemporalMotion = 0x102;
 
 struct ptx_handle {
     ptx_config cfg{};
@@ -77,9 +79,15 @@ struct ptx_handle {
     uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
     bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
     uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
+    // the camera moved since d_hist's frame (whole-image DI reuse handles): ptx_render reprojects
+    // the history (the motion temporal pass) with d_psurf = that frame's primary-hit surface
+    // records, copied on its stream before the next frame's G-buffer may overwrite them
+    bool hist_moved = false;
+    DevBuf d_psurf;
     DevBuf d_qrays, d_qhits;  // staging for ptx_trace (host arrays)
     // wavefront variant: pixel state, ray queue + ping-pong results / active lists, counters
     DevBuf d_wstate, d_wrays, d_wres0, d_wres1, d_wres2, d_wact0, d_wact1, d_wctr;
+    DevBuf d_wpool;  // Visibility restart pools of the dynamic-batch trace launches (WaveBufs::pool)
     size_t wave_ray_cap = 0;
     // second stream: the two halves of the segments run as independent launch sequences so
     // one half's latency-bound traces overlap the other's ALU-bound shading
@@ -101,7 +109,7 @@ struct ptx_handle {
     // ptx_render swaps the members above with `alt` per frame, so everything else always sees
     // the latest frame's buffers; the shared ones (accumulation, history, jobs, scene) never move.
     struct FrameCtx {
-        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wres2, wact0, wact1, wctr, tjstate, tjres;
+        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wres2, wact0, wact1, wctr, wpool, tjstate, tjres;
         size_t wave_ray_cap = 0;
         uint32_t wave_slots = 0;
         hipStream_t stream = nullptr;

@@ -85,7 +85,20 @@ struct WaveBufs {
     // DI reuse pipeline: primary-hit surface records (2 uint4 per pixel, first band row; halo
     // rows at negative / >= npix indices), written by winit_start; nullptr otherwise
     uint4 *surf;
+    // Visibility restart pools of a dynamic-batch trace launch (trace_lanes): per wave of the
+    // launch, kRestartCap entries of 2 float4; nullptr = every restart continues in place
+    float4 *pool;
 };
+// A Visibility query whose closest hit is transmissive restarts from the hit (up to 5
+// segments, SH/PT_1_InitPass.wgsl:774-802).  When fewer than kRestartInPlace lanes of a wave's
+// batch restart, their continuations go to the wave's pool instead (origin, remaining distance,
+// transmittance, segment, query slot) and the wave walks them later as one batch of >=
+// kRestartRun restarts (or at the end): the same per-query walks, without 60+ idle lanes each.
+constexpr uint32_t kRestartCap = 64u, kRestartInPlace = 32u, kRestartRun = 32u;
+constexpr size_t kRestartPoolSets = 8u;  // (tile set, launch sequence) pairs of a frame context
+// dynamic trace batches: one workgroup per slot, at most kDynMaxGroups (the chip holds ~1024 trace
+// workgroups; later ones find the list drained and leave)
+constexpr uint32_t kDynMaxGroups = 1024u, kDynMaxSlots = 4096u;
 // occ_only: every query of the round is Q_OCC (any-hit kernel instance)
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w, int round, int eps_mode, uint32_t stack_depth,
                       hipStream_t s, bool occ_only = false);
@@ -127,7 +140,16 @@ struct ReuseArgs {
     uint32_t fold_last;
     uint32_t ray_cap;   // ray slots of the wave buffers: a stale jres word (a slot the combine
                         // loads but does not use) never sends the fold's gather out of bounds
+    // temporal reuse under camera motion (wtmotion_*, ptx_reuse.hip): the previous frame's
+    // VP^-1 (its camera points) and VP (the reprojection), its primary-hit surface records
+    // (the whole image, cur's addressing); motion = 1 selects the pass
+    uint32_t motion;
+    float vpinv_prev[16], vp_prev[16];
+    const uint4 *psurf;
 };
+// the motion temporal pass's jobs per pixel: the canonical sample at home, the reprojected
+// history sample here, the canonical sample in the previous frame's domain
+constexpr uint32_t kMotionJobs = 3u;
 constexpr uint32_t kJobPending = 0xFFFFFFFFu;  // jres.w of such a job (a NaN: never a stored q)
 // The fold keeps ONE result buffer per trace round (WaveBufs::res[0..2], res_sel = round % 3):
 // a fourth round would overwrite the round-0 light results the combine still reads.

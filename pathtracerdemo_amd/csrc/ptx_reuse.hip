@@ -53,12 +53,22 @@ __device__ __forceinline__ uint32_t job_id(const ReuseArgs &A, uint32_t pix, uin
     return pix * A.jpx + slot * A.jslot;
 }
 __device__ __forceinline__ const uint4 *res_at(const uint4 *base, int32_t idx) { return base + 8 * (ptrdiff_t)idx; }
+// A job's sample reservoir: a band index into cur (the pass's reservoirs, halo rows < 0 or
+// >= npix), or kHistRef + index into hist -- the motion temporal pass's reprojected history
+// sample, which lives in the previous frame's spatial output.
+constexpr int32_t kHistRef = 1 << 29;
+__device__ __forceinline__ const uint4 *res_of(const ReuseArgs &A, int32_t ref) {
+    return ref >= kHistRef ? A.hist + 8 * (ptrdiff_t)(ref - kHistRef) : A.cur + 8 * (ptrdiff_t)ref;
+}
+// a job whose domain is not a pixel of this frame (the previous frame's, motion temporal pass):
+// stored in the full layout, as the fresh one re-derives the domain from this frame's records
+constexpr int32_t kDomPrev = INT32_MIN;
 
 // A job waiting for its light segment's Visibility (phase 1) only needs HDR and F.
 __device__ __forceinline__ void job_store(const ReuseArgs &A, uint32_t jid, const Job &s) {
     const size_t n = A.njobs;
     float4 *st = A.jstate;
-    if (PTX_JOB_FRESH && s.i == 1u && s.phase == 0u) {  // fresh: 48 B (see above)
+    if (PTX_JOB_FRESH && s.i == 1u && s.phase == 0u && s.dom != kDomPrev) {  // fresh: 48 B (see above)
         st[JS_HDR * n + jid] = make_float4(asf(1u | (s.length << 8) | kJobFresh), asf((uint32_t)s.dom), asf(s.idx),
                                            asf((uint32_t)s.ref));
         st[JS_F * n + jid] = make_float4(s.rr_f.x, s.rr_f.y, s.rr_f.z, s.prod);
@@ -84,7 +94,7 @@ __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, ui
     if (hw & kJobFresh) {  // the fresh layout: gather what it leaves out (same bits)
         const float4 rf = st[JS_RRF * n + jid];
         s.dom = (int32_t)asu(hd.y);
-        s.seed1 = res_at(A.cur, s.ref)[0].y;
+        s.seed1 = res_of(A, s.ref)[0].y;
         s.f = mk(1.0f, 1.0f, 1.0f); s.prod = fv.w;
         s.rr_f = mk(fv.x, fv.y, fv.z);
         s.beta = rf.x; s.rr_p = rf.y;
@@ -153,7 +163,7 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
     f3 o = mk(0.0f, 0.0f, 0.0f), d = o, Le = o;
     float remain = -1.0f;
     if (emit) {
-        const uint4 *rv = res_at(A.cur, s.ref);
+        const uint4 *rv = res_of(A, s.ref);
         const f3 V = normalize(s.prev - s.cur.pos);
         bool ok = true;
         if (s.i + 1u < s.length) {
@@ -320,7 +330,7 @@ __device__ __forceinline__ uint4 nbr_pack(bool valid, uint4 r5, uint4 r6, uint4 
 // trace results read instead of recomputed (identical bits: same rays, deterministic
 // traversal).  Returns true when the job still needs its light ray (an env candidate).
 __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBufs &w, const ReuseArgs &A, Job &s,
-                                                   uint32_t pix) {
+                                                   uint32_t pix, uint32_t jid) {
     const uint4 *rv = res_at(A.cur, s.ref);
     while (s.i + 1u < s.length) {
         f3 V = normalize(s.prev - s.cur.pos);
@@ -330,7 +340,7 @@ __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBu
         const f3 fv = bsdf_pdf(s.cur, V, dir, pdf);
         s.prod *= pdf;
         if (!rr_step(s, s.cur, dir, fv, pdf)) {
-            A.jres[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             return false;
         }
         const float4 c = w.state[(s.i == 1u ? kStateCs2 : kStateCs3) * w.npix + pix];
@@ -359,7 +369,7 @@ __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBu
     s.f = s.f * (Le * T);
     const float qv = s.prod;
     const bool valid = qv > 0.0f && qv <= 3.402823466e38f;
-    A.jres[pix] = valid ? make_float4(s.f.x, s.f.y, s.f.z, qv) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    A.jres[jid] = valid ? make_float4(s.f.x, s.f.y, s.f.z, qv) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     return false;
 }
 
@@ -379,7 +389,7 @@ void wtemporal_start(Scene sc, WaveBufs w, ReuseArgs A) {
         if (q < np && tile_xy(sc, q, x, y)) {
             pix = (y - sc.row_begin) * sc.width + x;
             active = job_begin(sc, A, s, x, y, (int32_t)pix, (int32_t)pix);
-            if (active && A.use_init) active = temporal_from_init(sc, w, A, s, pix);
+            if (active && A.use_init) active = temporal_from_init(sc, w, A, s, pix, pix);
         }
         const bool live = job_emit(sc, g, A, active, s, pix, active ? A.cur[8u * (size_t)pix].x : 0u);
         job_finish(g, JL, A, live, s, pix);
@@ -424,6 +434,190 @@ __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, Re
         const float W = p_sel > 0.0f ? w_sum / p_sel : 0.0f;
         A.nbr_out[pix] = nbr_pack(true, make_uint4(0u, 0u, 0u, from_hist ? h5.w : r5.w),
                                   make_uint4(asu(p_sel), asu(q_sel), 0u, 0u), make_uint4(asu(W), 1u + Cp, 0u, 0u));
+    }
+}
+
+// ---------------------------------------------------------------- temporal, moved camera
+// The history of pixel p lives at its reprojection p' in the previous frame, in that frame's
+// domain (oracle temporal_motion_pixel, the rules and their constants are stated there): three
+// shift jobs per pixel -- slot 0 the canonical PT_1 sample at home (from PT_1's state, as the
+// still-camera pass), slot 1 the history sample at p' replayed here, slot 2 the canonical sample
+// replayed from the previous frame's camera point and primary hit at p' -- then a combine with
+// the generalized balance heuristic (the spatial pass's pairwise rule with M = 1).
+__device__ __forceinline__ f3 x0_prev(const ReuseArgs &A, const Scene &sc, uint32_t x, uint32_t y) {
+    float u = ((float)x + 0.5f) / (float)sc.U[U_W];  // (x0_of with the previous frame's VP^-1)
+    float v = ((float)y + 0.5f) / (float)sc.U[U_H];
+    return xform_point(A.vpinv_prev, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
+}
+struct MotionHist { bool ok; int32_t pp; uint32_t px, py, C; };
+// p' of pixel pix's primary hit X1 and the disocclusion test (oracle reproject / motion_valid):
+// C = min(C_hist, cap) when the history at p' is usable, else 0
+__device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseArgs &A, const Surface &X1) {
+    MotionHist m{false, 0, 0u, 0u, 0u};
+    if (!A.hist_valid) return m;
+    const float *vp = A.vp_prev;
+    const f3 P = X1.pos;
+    const float cx = ((vp[0] * P.x + vp[4] * P.y) + vp[8] * P.z) + vp[12];
+    const float cy = ((vp[1] * P.x + vp[5] * P.y) + vp[9] * P.z) + vp[13];
+    const float cw = ((vp[3] * P.x + vp[7] * P.y) + vp[11] * P.z) + vp[15];
+    if (!(cw > 0.0f)) return m;
+    const float W = (float)sc.width, H = (float)sc.height;
+    const float fx = ((cx / cw + 1.0f) * 0.5f) * W, fy = ((cy / cw + 1.0f) * 0.5f) * H;
+    if (!(fx >= 0.0f && fx < W && fy >= 0.0f && fy < H)) return m;
+    m.px = (uint32_t)fx;
+    m.py = (uint32_t)fy;
+    m.pp = (int32_t)(m.py * sc.width + m.px);  // (whole-image handles only)
+    const uint4 a = A.psurf[2 * (ptrdiff_t)m.pp];
+    if (a.w == kNoSurface) return m;
+    const uint4 b = A.psurf[2 * (ptrdiff_t)m.pp + 1];
+    const f3 pp = mk(asf(a.x), asf(a.y), asf(a.z)), pn = mk(asf(b.x), asf(b.y), asf(b.z));
+    if (!(dot(pn, X1.nrm) >= 0.9f)) return m;
+    const f3 x0p = x0_prev(A, sc, m.px, m.py);
+    const float dp = length(pp - x0p), dc = length(P - x0p);
+    if (!(fabsf(dp - dc) <= 0.05f * dc)) return m;
+    m.C = min(A.hist[8 * (ptrdiff_t)m.pp + 7].y, A.cap);
+    m.ok = m.C != 0u;
+    return m;
+}
+
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(2, 8)))
+void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_TEMP_START | (w.seg_base ? 0x80u : 0u));
+    __shared__ uint32_t lds[3];
+    const JobLists JL = job_lists(w, lds);
+    const Seg g = seg_begin(w, 0u, lds);
+    const uint32_t np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, g.j, k);
+        uint32_t x = 0u, y = 0u, pix = 0u;
+        bool valid = false;
+        Surface X1{};
+        uint32_t mref = 0u;
+        if (q < np && tile_xy(sc, q, x, y)) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            valid = surf_load(sc, A.surf, pix, X1, mref);
+        }
+        const uint4 *rv = A.cur + 8u * (size_t)pix;
+        const uint32_t cC = valid ? rv[7].y : 0u, clen = valid ? rv[5].w : 0u;
+        const bool canon = valid && cC != 0u && clen >= 2u;
+        // slot 0: the canonical sample at home (PT_1's state when it still describes it)
+        {
+            const uint32_t jid = job_id(A, pix, 0u);
+            Job s;
+            bool act = canon && job_begin(sc, A, s, x, y, (int32_t)pix, (int32_t)pix);
+            if (act && A.use_init) act = temporal_from_init(sc, w, A, s, pix, jid);
+            const bool live = job_emit(sc, g, A, act, s, jid, act ? rv[0].x : 0u);
+            job_finish(g, JL, A, live, s, jid);
+        }
+        const MotionHist mh = valid ? motion_hist(sc, A, X1) : MotionHist{false, 0, 0u, 0u, 0u};
+        // slot 1: the history sample at p' in this pixel's domain
+        {
+            const uint32_t jid = job_id(A, pix, 1u);
+            Job s;
+            bool act = false;
+            uint32_t s0 = 0u;
+            if (mh.ok) {
+                const uint4 *hv = A.hist + 8 * (ptrdiff_t)mh.pp;
+                const uint4 h0 = hv[0], h5 = hv[5], h6 = hv[6];
+                act = h5.w >= 2u && asf(h6.x) > 0.0f;
+                if (act) {
+                    job_init(s, x0_of(sc, x, y), X1, mref, kHistRef + mh.pp, h5.w, h0.y, (int32_t)pix);
+                    s0 = h0.x;
+                }
+            }
+            const bool live = job_emit(sc, g, A, act, s, jid, s0);
+            job_finish(g, JL, A, live, s, jid);
+        }
+        // slot 2: the canonical sample in the previous frame's domain at p' (used only when the
+        // canonical evaluation is valid; created whenever it may be)
+        {
+            const uint32_t jid = job_id(A, pix, 2u);
+            Job s;
+            bool act = false;
+            uint32_t s0 = 0u;
+            if (mh.ok && canon) {
+                Surface Xp;
+                uint32_t pref;
+                act = surf_load(sc, A.psurf, mh.pp, Xp, pref);
+                if (act) {
+                    job_init(s, x0_prev(A, sc, mh.px, mh.py), Xp, pref, (int32_t)pix, clen, rv[0].y, kDomPrev);
+                    s0 = rv[0].x;
+                }
+            }
+            const bool live = job_emit(sc, g, A, act, s, jid, s0);
+            job_finish(g, JL, A, live, s, jid);
+        }
+    }
+    job_seg_end(w, g, JL);
+}
+
+__global__ __launch_bounds__(WB) void wtmotion_combine(Scene sc, WaveBufs w, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_TEMP_COMBINE | (w.seg_base ? 0x80u : 0u));
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        Surface X1;
+        uint32_t mref;
+        if (!surf_load(sc, A.surf, pix, X1, mref)) {  // PT_1 wrote the zero reservoir
+            A.nbr_out[pix] = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
+        uint4 *rv = A.cur + 8u * (size_t)pix;
+        uint32_t seed = reuse_seed(sc, x, y, SALT_TEMPORAL);
+        const uint4 r5 = rv[5], r7 = rv[7];
+        const float4 er = (r7.y != 0u && r5.w >= 2u) ? A.jres[job_id(A, pix, 0u)] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float ecp = er.w > 0.0f ? luminance(mk(er.x, er.y, er.z)) : 0.0f, ecq = er.w;
+        const bool canon_ok = ecq > 0.0f && ecp > 0.0f;
+        const float cc = 1.0f, pc = ecp, qc = ecq, Wc = asf(r7.x);
+        const MotionHist mh = motion_hist(sc, A, X1);
+        const uint32_t Cp = mh.ok ? mh.C : 0u;
+        const float cp = (float)Cp;
+        const uint4 *hv = A.hist + 8 * (ptrdiff_t)mh.pp;
+        // forward: the history sample shifted here
+        float wh = 0.0f, pf = 0.0f, qf = 0.0f;
+        SelF ff{false, mk(0.0f, 0.0f, 0.0f)};
+        uint32_t hlen = 0u;
+        if (Cp != 0u) {
+            const uint4 h5 = hv[5], h6 = hv[6], h7 = hv[7];
+            hlen = h5.w;
+            const float ph = asf(h6.x), qh = asf(h6.y), Wh = asf(h7.x);
+            if (h5.w >= 2u && ph > 0.0f) {
+                const float4 Fr = A.jres[job_id(A, pix, 1u)];
+                if (Fr.w > 0.0f) {
+                    const float Fp = luminance(mk(Fr.x, Fr.y, Fr.z)), Fq = Fr.w;
+                    const float J = qh / Fq;
+                    const float pb = ph / J;
+                    const float den = cc * Fp + cp * pb;
+                    const float m = den > 0.0f ? (cp * pb) / den : 0.0f;
+                    wh = m * Fp * Wh * J;
+                    pf = Fp;
+                    qf = Fq;
+                    ff = job_f(Fr);
+                }
+            }
+        }
+        // backward: the canonical sample's weight from its shift into the previous domain
+        float Q = 1.0f;
+        if (canon_ok && Cp != 0u) {
+            const float4 B = A.jres[job_id(A, pix, 2u)];
+            if (B.w > 0.0f) {
+                const float pbc = luminance(mk(B.x, B.y, B.z)) * qc / B.w;
+                const float den = cc * pc + cp * pbc;
+                Q = den > 0.0f ? (cc * pc) / den : 1.0f;
+            }
+        }
+        const float wc = canon_ok ? Q * pc * Wc : 0.0f;
+        float w_sum = 0.0f, p_sel = ecp, q_sel = ecq;
+        bool from_hist = false;
+        if (wrs_update(w_sum, wc, seed)) { from_hist = false; p_sel = ecp; q_sel = ecq; }
+        if (wrs_update(w_sum, wh, seed)) { from_hist = true; p_sel = pf; q_sel = qf; }
+        write_reused(rv, from_hist ? hv : rv, p_sel, q_sel, from_hist ? ff : job_f(er), w_sum, 1u + Cp);
+        const float Wo = p_sel > 0.0f ? w_sum / p_sel : 0.0f;
+        A.nbr_out[pix] = nbr_pack(true, make_uint4(0u, 0u, 0u, from_hist ? hlen : r5.w),
+                                  make_uint4(asu(p_sel), asu(q_sel), 0u, 0u), make_uint4(asu(Wo), 1u + Cp, 0u, 0u));
     }
 }
 
@@ -851,18 +1045,22 @@ __global__ __launch_bounds__(WB) void wspatial_combine(Scene sc, WaveBufs w, Reu
 // Logic round 0 creates the jobs, rounds 1..kWaveRoundsReuse step them, the last round
 // combines (so round r > 0 consumes trace round r-1).
 // temporal from PT_1's state: only env candidates trace (one light ray each)
-int reuse_rounds(int pass_temporal, const ReuseArgs &A) { return pass_temporal && A.use_init ? 1 : kWaveRoundsReuse; }
+int reuse_rounds(int pass_temporal, const ReuseArgs &A) {
+    return pass_temporal && A.use_init && !A.motion ? 1 : kWaveRoundsReuse;
+}
 
 hipError_t wave_reuse_round(const Scene &sc, const WaveBufs &w, int pass_temporal, int round, const ReuseArgs &A,
                             hipStream_t s) {
     const dim3 grid(w.seg_count), blk(WB);
     if (round == 0) {
-        if (pass_temporal) hipLaunchKernelGGL(wtemporal_start, grid, blk, 0, s, sc, w, A);
+        if (pass_temporal && A.motion) hipLaunchKernelGGL(wtmotion_start, grid, blk, 0, s, sc, w, A);
+        else if (pass_temporal) hipLaunchKernelGGL(wtemporal_start, grid, blk, 0, s, sc, w, A);
         else hipLaunchKernelGGL(wspatial_start, grid, blk, 0, s, sc, w, A);
     } else if (round <= reuse_rounds(pass_temporal, A)) {
         hipLaunchKernelGGL(wjob_step, grid, blk, 0, s, sc, w, (uint32_t)round, A);
     } else {
-        if (pass_temporal) hipLaunchKernelGGL(wtemporal_combine, grid, blk, 0, s, sc, w, A);
+        if (pass_temporal && A.motion) hipLaunchKernelGGL(wtmotion_combine, grid, blk, 0, s, sc, w, A);
+        else if (pass_temporal) hipLaunchKernelGGL(wtemporal_combine, grid, blk, 0, s, sc, w, A);
         else if (A.neighbors == 3u && !ab_knob("COMBINE_SCALAR", 0))  // (A/B switch)
             hipLaunchKernelGGL(wspatial_combine_shfl, dim3(w.seg_count), blk, 0, s, sc, w, A);
         else hipLaunchKernelGGL(wspatial_combine, grid, blk, 0, s, sc, w, A);

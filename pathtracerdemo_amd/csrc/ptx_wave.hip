@@ -58,22 +58,18 @@ namespace ptx {
 // Measured same box (1080p): furnished C3 (13 instances) +9.7 %, GI on C3 (3) +3.2 %, reuse on
 // C3 +0.6 %, TEST_MCPT on C1 (2 instances) -3.2 %: flattened from 3 instances up.
 constexpr uint32_t kFlatMinInstances = 3u;
-template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES = false, bool FLAT = false>
-__device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
-                                            uint32_t *stack, CoopLds coop, const float4 *rays, float4 *res,
-                                            uint32_t i, bool active, uint32_t *dbg = nullptr) {
-    float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
-    if (active) {
-        a = rays[2u * i];
-        b = rays[2u * i + 1u];
-    }
-    Ray r{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)};
-    const uint32_t kind = asu(b.w);
+// The queries of one wave: lane state {ray, kind, transmittance T, remaining distance, segment}
+// for query slot gi (its result at res[2 gi]).  Visibility (SH/PT_1_InitPass.wgsl:774-802) walks
+// through transmissive hits: one trace site, looped, so the traversal code is emitted once.
+// pool (dynamic batches): after the first segment, a few restarting lanes leave their
+// continuation in the wave's pool (kRestartInPlace, trace_restarts) instead of walking again here.
+template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES, bool FLAT>
+__device__ __forceinline__ void trace_lanes(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
+                                            uint32_t *stack, CoopLds coop, Ray r, uint32_t kind, float T, float remain,
+                                            uint32_t seg, bool active, float4 *res, uint32_t gi, float4 *pool,
+                                            uint32_t &pool_n, uint32_t *dbg) {
     const bool vis = kind != Q_CLOSEST;
-    // Visibility (SH/PT_1_InitPass.wgsl:774-802) walks through transmissive hits:
-    // one trace site, looped, so the traversal code is emitted once
-    float T = 1.0f, remain = a.w;
-    for (uint32_t it = 0u;; ++it) {
+    for (;;) {
         const float t_max = !active ? __builtin_nanf("") : vis ? fminf(remain, 1e10f) : 1e10f;
         // a Visibility hit's position is only needed to restart through a transmissive surface:
         // it is reconstructed below for those lanes only
@@ -83,8 +79,8 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
                           sc, subs, insts, r, eps, stack, WB, t_max, coop, !vis);
         if (active && !vis) {
             const uint32_t enc = ((h.valid ? 1u : 0u) << 31) | (h.s.inst << 16) | h.s.mat;
-            res[2u * i] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
-            res[2u * i + 1u] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
+            res[2u * gi] = make_float4(h.t, asf(enc), asf(h.s.prim), h.s.bu);
+            res[2u * gi + 1u] = make_float4(h.s.bv, h.pos.x, h.pos.y, h.pos.z);
             active = false;
         } else if (active) {
             float out = -1.0f;
@@ -97,18 +93,48 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
                     remain -= h.t;
                     complete_hit(sc, r, eps, h, insts);
                     r.o = h.pos;
-                    if (it == 4u) out = 0.0f;  // Visibility gives up after 5 segments
+                    if (seg == 4u) out = 0.0f;  // Visibility gives up after 5 segments
+                    ++seg;
                 }
             }
             if (out >= 0.0f) {  // only res.x is written: .yzw and res[2i+1] carry the payload
-                res[2u * i].x = out;
+                res[2u * gi].x = out;
                 active = false;
+            }
+        }
+        if (pool) {  // (wave-uniform) lanes that just finished their first segment
+            const unsigned long long rs = __ballot(active && seg == 1u);
+            const uint32_t nr = (uint32_t)__popcll(rs);
+            if (nr != 0u && nr < kRestartInPlace && pool_n + nr <= kRestartCap) {
+                if (active && seg == 1u) {
+                    const uint32_t slot =
+                        pool_n + __builtin_amdgcn_mbcnt_hi((uint32_t)(rs >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rs, 0u));
+                    pool[2u * slot] = make_float4(r.o.x, r.o.y, r.o.z, remain);
+                    pool[2u * slot + 1u] = make_float4(T, asf(seg), asf(gi), 0.0f);
+                    active = false;
+                }
+                pool_n += nr;
             }
         }
         if (__ballot(active) == 0ull) break;
     }
 }
-
+// Lane i of the wave traces query i of a batch (`rays` / `res` = the segment's, slot
+// gbase + i of the launch's buffers rays_all / res_all).
+template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES = false, bool FLAT = false>
+__device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
+                                            uint32_t *stack, CoopLds coop, float4 *res_all, const float4 *rays_all,
+                                            uint32_t gbase, uint32_t i, bool active, float4 *pool, uint32_t &pool_n,
+                                            uint32_t *dbg = nullptr) {
+    const uint32_t gi = gbase + i;
+    float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+    if (active) {
+        a = rays_all[2u * gi];
+        b = rays_all[2u * gi + 1u];
+    }
+    trace_lanes<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop, Ray{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)},
+                                                    asu(b.w), 1.0f, a.w, 0u, active, res_all, gi, pool, pool_n, dbg);
+}
 // Dynamic batches (WaveBufs::dyn): the launch's rays -- every slot of the launch's segment
 // range -- are one list of 64-query batches (a slot's batch k = its queries 64k .. 64k+63,
 // consecutive entries of one tile, coherent), and every wave takes the next batch from a
@@ -163,6 +189,12 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         // a wave whose chunk is drained moves on to the next one
         uint32_t *heads = w.dyn + round * kDynRoundWords;
         const uint32_t lane = __lane_id();
+        float4 *res_all = res_buf(w, round);
+        // this wave's restart pool (none in the counting / profiling builds: same work, in place)
+        float4 *pool = (!COUNT && !PROF && w.pool)
+                           ? w.pool + ((size_t)blockIdx.x * (WB / 64u) + (threadIdx.x >> 6)) * (2u * kRestartCap)
+                           : nullptr;
+        uint32_t pool_n = 0u;
         uint32_t x = blockIdx.x % kDynHeads, visited = 0u;
         uint32_t c0 = (uint32_t)((uint64_t)total * x / kDynHeads), c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
         // each dequeue takes G consecutive batches (WaveBufs::trace_split in this mode): one
@@ -170,21 +202,54 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         const uint32_t G = w.trace_split;
         uint32_t bnext = 0u;
         if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
-        uint32_t bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
-        for (;;) {  // wave-uniform
-            if (bi >= c1) {  // this chunk is drained: the next head
-                if (++visited == kDynHeads) break;
-                x = (x + 1u) % kDynHeads;
-                c0 = (uint32_t)((uint64_t)total * x / kDynHeads);
-                c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
-                if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
-                bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
-                continue;
+        uint32_t bi = 0u, bend = 0u, lo = 0u;
+        bool drained = false;
+        // One unit of work per iteration -- the next batch, or (once kRestartRun restarts are
+        // pooled, and at the end) the pooled restarts -- through ONE trace site (wave-uniform).
+        for (;;) {
+            bool restart = pool_n >= kRestartRun;
+            while (!restart && !drained && bi >= bend) {  // the next dequeue (its successor fetched ahead)
+                const uint32_t nb = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
+                if (nb < c1) {
+                    bi = nb;
+                    bend = min(nb + G, c1);
+                    lo = 0u;
+                    if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
+                } else if (++visited == kDynHeads) {
+                    drained = true;
+                } else {  // this chunk is drained: the next head
+                    x = (x + 1u) % kDynHeads;
+                    c0 = (uint32_t)((uint64_t)total * x / kDynHeads);
+                    c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
+                    if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
+                }
             }
-            if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);  // the next dequeue, fetched ahead
-            const uint32_t bend = min(bi + G, c1);
-            uint32_t lo = 0u;
-            for (; bi < bend; ++bi) {
+            if (drained && !restart) {
+                if (pool_n == 0u) break;
+                restart = true;  // the wave's last restarts
+            }
+#ifdef PTX_WG_TIMES
+            const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t dbg[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+            const uint32_t rec_bi = restart ? 0xFFFFFFFFu : bi;
+#else
+            uint32_t *dbg = nullptr;
+#endif
+            float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c = a;
+            bool active;
+            uint32_t gi = 0u;
+            if (restart) {  // pooled restart `lane`: {origin, remain}, {T, segment, query slot}
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (the wave's own pool stores)
+                active = lane < pool_n;
+                c = make_float4(1.0f, 0.0f, 0.0f, 0.0f);
+                if (active) {
+                    a = pool[2u * lane];
+                    c = pool[2u * lane + 1u];
+                    gi = asu(c.z);
+                    b = w.rays[2u * gi + 1u];  // the query's direction and kind
+                }
+                pool_n = 0u;
+            } else {
                 uint32_t hi = w.seg_count;  // last slot with pref <= bi (batches ascend: search from lo)
                 while (hi - lo > 1u) {
                     const uint32_t mid = (lo + hi) >> 1;
@@ -194,20 +259,22 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                 const uint32_t j = w.seg_phys + w.seg_base + lo;
                 const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
                 const uint32_t i = (bi - pref[lo]) * 64u + lane;
-#ifdef PTX_WG_TIMES
-                const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
-                uint32_t dbg[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-#else
-                uint32_t *dbg = nullptr;
-#endif
-                trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
-                                              w.rays + 2u * (size_t)j * w.ray_stride,
-                                              res_buf(w, round) + 2u * (size_t)j * w.ray_stride, i, i < n, dbg);
-#ifdef PTX_WG_TIMES
-                batch_record(sc.wgt, tb0, bi, round, dbg);
-#endif
+                active = i < n;
+                gi = j * w.ray_stride + i;
+                c = make_float4(1.0f, 0.0f, 0.0f, 0.0f);  // T = 1, segment 0
+                if (active) {
+                    a = w.rays[2u * gi];
+                    b = w.rays[2u * gi + 1u];
+                }
+                ++bi;
             }
-            bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
+            trace_lanes<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
+                                                            Ray{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)}, asu(b.w), c.x, a.w,
+                                                            asu(c.y), active, res_all, gi, restart ? nullptr : pool, pool_n,
+                                                            dbg);
+#ifdef PTX_WG_TIMES
+            batch_record(sc.wgt, tb0, rec_bi, round, dbg);
+#endif
         }
         return;
     }
@@ -227,11 +294,11 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     const Inst *insts = T.insts;
     if (COUNT && sc.census)  // row census: this slot's queries count into its own block
         sc.counters = sc.census + (size_t)kCensusWords * ((sc.row_end - sc.row_begin + 7u) / 8u + j);
-    const float4 *rays = w.rays + 2u * (size_t)j * w.ray_stride;
-    float4 *res = res_buf(w, round) + 2u * (size_t)j * w.ray_stride;
+    uint32_t no_pool = 0u;
     for (uint32_t i0 = share * WB; i0 < n; i0 += K * WB) {  // workgroup-uniform
         const uint32_t i = i0 + threadIdx.x;
-        trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop, rays, res, i, i < n);
+        trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop, res_buf(w, round), w.rays,
+                                                         j * w.ray_stride, i, i < n, nullptr, no_pool);
     }
 }
 
@@ -954,7 +1021,9 @@ void wfinal_one(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir,
                 }
             }
             // the traversal kernel's walk, every lane of the wave (idle ones with a NaN bound)
-            trace_batch<false, false, false, true, FLAT>(sc, T.subs, T.insts, eps, stack, coop, rays, res, slot, active);
+            uint32_t no_pool = 0u;
+            trace_batch<false, false, false, true, FLAT>(sc, T.subs, T.insts, eps, stack, coop, res, rays, 0u, slot, active,
+                                                         nullptr, no_pool);
             if (active) {  // wfinal_step
                 if (s.phase == 0u) {
                     const Hit h = get_hit(res, slot);
@@ -1148,9 +1217,6 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
 
 // =========================================================================== host side
 // trace_queue's grid: trace_split workgroups per segment
-// dynamic batches: one workgroup per slot, at most kDynMaxGroups (the chip holds ~1024 trace
-// workgroups; later ones find the list drained and leave)
-constexpr uint32_t kDynMaxGroups = 1024u, kDynMaxSlots = 4096u;
 static inline bool trace_dyn(const WaveBufs &w) { return w.dyn != nullptr && w.seg_count <= kDynMaxSlots; }
 static inline uint32_t trace_grid(const WaveBufs &w) {
     return trace_dyn(w) ? std::min(w.seg_count, kDynMaxGroups) : w.seg_count * w.trace_split;

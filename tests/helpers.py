@@ -4,9 +4,13 @@ import numpy as np
 from pathtracerdemo_amd.scene.camera import Camera
 
 
-def uniform_for(cs, W, H, frame=1, location=(0.0, 0.0, 6.0)):
+def uniform_for(cs, W, H, frame=1, location=(0.0, 0.0, 6.0), yaw=0.0, pitch=0.0):
     cam = Camera(W, H)
     cam.set_location(*location)
+    if yaw:
+        cam.set_yaw(yaw)
+    if pitch:
+        cam.set_pitch(pitch)
     return cs.uniform(W, H, cam.view_projection_inverse(), cam.location, frame)
 
 

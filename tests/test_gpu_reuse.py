@@ -3,7 +3,7 @@ through the C ABI.  Every reservoir and radiance value is compared BIT FOR BIT.
 
 Each pass is first fed the oracle's inputs (so a mismatch is pinned to one kernel), then
 whole frames run end to end (history included), on odd sizes, C3's 32 lights, a band pair
-with the halo exchange, a camera move (history dropped) and a full 1080p frame checked on
+with the halo exchange, camera moves (history reprojected) and a full 1080p frame checked on
 a row window the oracle can afford.
 """
 import numpy as np
@@ -148,9 +148,9 @@ def test_pass_by_pass_equals_render(scene1, native):
     assert_same(a.read_image(), b.read_image(), "radiance")
 
 
-def test_camera_move_drops_history(scene1, oracle_mod):
-    """A new camera invalidates the temporal history (ptx_set_frame): frame 3 after the move
-    equals the oracle's with hist_valid cleared."""
+def test_camera_move_reprojects_history(scene1, oracle_mod):
+    """A new camera keeps the temporal history and reprojects it (the motion temporal pass,
+    oracle temporal_motion_pixel): frame 3 after the move is bit-identical to the oracle's."""
     O, W, H = oracle_mod, 48, 32
     fr = oracle_frame(O, scene1, W, H)
     r = reuse_renderer(scene1, W, H)
@@ -161,15 +161,52 @@ def test_camera_move_drops_history(scene1, oracle_mod):
         r.Render()
     r.GetCamera().set_location(0.3, 0.1, 5.5)
     r.Update()
-    moved = r.uniform.copy()
     r.Render()
-    fr2 = O.Frame(moved, scene1.scene, scene1.geometry, scene1.accel)
-    fr2.accum[:] = fr.accum
-    fr2.res_hist[:] = fr.res_hist
-    fr2.hist_valid = False
-    fr2.run_reuse_frame(threads=8)
-    assert_same(r.read_history(), fr2.res_hist, "spatial output after the move")
-    assert_same(r.read_image(), fr2.accum, "radiance after the move")
+    fr.set_camera(r.uniform)
+    fr.set_frame_index(3)
+    fr.run_reuse_frame(threads=8)
+    assert_same(r.read_reservoir(), fr.reservoir, "temporal output after the move")
+    assert_same(r.read_history(), fr.res_hist, "spatial output after the move")
+    assert_same(r.read_image(), fr.accum, "radiance after the move")
+    assert (fr.reservoir[..., 29][(fr.gbuffer[..., 0] >> 31) == 1] > 1).mean() > 0.5  # reprojected history used
+
+
+# an interactive camera path: WebGPUEngine moves the camera by speed * dt per frame (5 units/s at
+# 60 Hz, InputController.ts:81-159) and turns it with the mouse
+CAMERA_PATH = [((0.0, 0.0, 6.0), 0.0), ((0.083, 0.0, 6.0), 0.0), ((0.166, 0.0, 5.95), 0.0),
+               ((0.25, 0.02, 5.9), 1.5), ((0.25, 0.02, 5.9), 3.0), ((0.2, 0.02, 5.85), 4.5),
+               ((0.2, 0.02, 5.85), 4.5), ((0.12, 0.0, 5.8), 3.0)]
+
+
+@pytest.mark.parametrize("scene,W,H,single", [("scene1", 64, 48, False), ("scene3", 96, 64, False),
+                                               ("scene3", 96, 64, True)])
+def test_moving_camera_path_bit_exact(request, oracle_mod, scene, W, H, single):
+    """Eight frames along CAMERA_PATH (translations of 5 units/s at 60 Hz, a yaw turn, two still
+    frames) through the reuse pipeline, pipelined (two frames in flight) or one launch sequence:
+    every frame's temporal output (motion pass on the moved frames), spatial output and the
+    accumulated radiance are bit-identical to the oracle's; the reprojected history is used."""
+    O = oracle_mod
+    cs = request.getfixturevalue(scene)
+    fr = oracle_frame(O, cs, W, H)
+    r = reuse_renderer(cs, W, H, single_stream=single, time_launches=single)
+    used = 0
+    for f, (loc, yaw) in enumerate(CAMERA_PATH, start=1):
+        r.GetCamera().set_location(*loc)
+        r.GetCamera().set_yaw(yaw)
+        r.Update()
+        r.Render()
+        fr.set_camera(r.uniform)
+        fr.set_frame_index(f)
+        moved = fr.hist_valid and fr.camera_moved()
+        fr.run_reuse_frame(threads=16)
+        if moved:
+            used += int((fr.reservoir[..., 29] > 1).sum())
+        if f in (2, 5, 8):
+            assert_same(r.read_reservoir(), fr.reservoir, f"temporal output, frame {f}")
+            assert_same(r.read_history(), fr.res_hist, f"spatial output, frame {f}")
+            assert_same(r.read_image(), fr.accum, f"radiance, frame {f}")
+    assert used > 0
+    r.close()
 
 
 def test_band_pair_with_halo_exchange_bit_exact(scene1, oracle_mod):
@@ -282,13 +319,11 @@ def test_pipelined_frames_interleaved_with_host_ops(scene3, oracle_mod, native):
     fr = oracle_frame(O, scene3, W, H)
     r = reuse_renderer(scene3, W, H)
     for f in range(1, 8):
-        if f == 5:  # camera move: the handle drops the history itself
+        if f == 5:  # camera move: the handle reprojects the history itself
             r.GetCamera().set_location(0.25, 0.1, 5.5)
         r.Update()
         if f == 5:
-            fr = oracle_frame(O, scene3, W, H)
-            fr.uniform[:] = r.uniform
-            fr.accum[:] = np.frombuffer(r.read_image().tobytes(), np.float32).reshape(fr.accum.shape)
+            fr.set_camera(r.uniform)
         fr.set_frame_index(r.uniform[23])
         fr.run_reuse_frame(threads=8)
         r.Render()

@@ -156,6 +156,13 @@ def main():
     print("  slowest 15:")
     for k in order[::-1][:15]:
         print(f"          {dur[k]:7.1f}  {refill[k]:5d} {node[k]:6d} {leafp[k]:5d} {chunks[k]:5d} {calls[k]:3d} {maxslab[k]:6d}")
+    for c in sorted(set(calls.tolist())):
+        m = calls == c
+        print(f"  calls {c}: {m.sum():6d} batches, mean {dur[m].mean():6.1f} us, p99 {np.percentile(dur[m], 99):6.1f} us, "
+              f"node-loop it mean {node[m].mean():6.1f}, share of batch time {dur[m].sum() / dur.sum():.3f}")
+    if a.out:
+        np.savez(a.out.replace(".json", "_batches.npz"), dur=dur, refill=refill, node=node, leaf=leafp, chunks=chunks,
+                 calls=calls, maxslab=maxslab)
     for name, v in (("node-loop it", node), ("refill it", refill), ("leaf phases", leafp), ("tri chunks", chunks),
                     ("calls", calls), ("max slab", maxslab)):
         print(f"  corr(duration, {name}) = {np.corrcoef(dur, v)[0, 1]:.3f}; mean {v.mean():.1f}")
