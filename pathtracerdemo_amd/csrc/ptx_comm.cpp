@@ -387,6 +387,34 @@ int render_band_nccl(ptx_handle *h) {
     return band_back(h, sc, w, ft);
 }
 
+// The exchange's proxy on one GPU (PTX_AB=HALO_PROXY_US=n, with PTX_FLAG_HALO_SKIP: timing
+// only): the band's edge rows copied into its own halo rows on the exchange stream (the same
+// bytes an exchange moves, device to device), then a one-workgroup wait of n microseconds
+// standing for the xGMI transfer (2 x 16.6 MB per direction at 153 GB/s: ~110 us), so the
+// band's frame time shows where the exchange sits on its critical chain.
+__global__ void halo_proxy_wait(uint32_t us) {
+    const unsigned long long end = __builtin_amdgcn_s_memrealtime() + 100ull * us;  // (100 MHz)
+    for (uint32_t i = 0; i < (1u << 24); ++i) {  // (bounded: every wave leaves)
+        if (__builtin_amdgcn_s_memrealtime() >= end) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+static int halo_proxy(ptx_handle *h, hipStream_t xs, uint32_t us) {
+    if (h->halo_top) {
+        const Rows s = send_up(h), r = recv_top(h);
+        HIP_CHECK(h, hipMemcpyAsync(r.g, s.g, s.gb, hipMemcpyDeviceToDevice, xs));
+        HIP_CHECK(h, hipMemcpyAsync(r.r, s.r, s.rb, hipMemcpyDeviceToDevice, xs));
+    }
+    if (h->halo_bot) {
+        const Rows s = send_down(h), r = recv_bottom(h);
+        HIP_CHECK(h, hipMemcpyAsync(r.g, s.g, s.gb, hipMemcpyDeviceToDevice, xs));
+        HIP_CHECK(h, hipMemcpyAsync(r.r, s.r, s.rb, hipMemcpyDeviceToDevice, xs));
+    }
+    hipLaunchKernelGGL(halo_proxy_wait, dim3(1), dim3(64), 0, xs, us);
+    HIP_CHECK(h, hipGetLastError());
+    return PTX_OK;
+}
+
 // PTX_FLAG_HALO_SKIP: the same band frame without the exchange (the halo rows keep what they
 // hold) -- a rank's band timed alone on one GPU (bench.py's band calibration, tools/band_alone.py).
 int render_band_solo(ptx_handle *h) {
@@ -398,6 +426,9 @@ int render_band_solo(ptx_handle *h) {
     if (int rc = band_front(h, sc, w, ft, pipe)) return rc;
     hipStream_t xs;
     if (int rc = exchange_stream(h, xs)) return rc;
+    static const int proxy_us = ab_knob("HALO_PROXY_US", 0);
+    if (proxy_us > 0 && proxy_us <= 100000)
+        if (int rc = halo_proxy(h, xs, (uint32_t)proxy_us)) return rc;
     if (int rc = halo_landed(h, xs)) return rc;
     return band_back(h, sc, w, ft);
 }

@@ -242,6 +242,11 @@ struct Prof {
     }
 };
 
+// A lane mask of a boolean: the ballot builtin on the i1 itself.  (HIP's __ballot takes an
+// int, so a bool predicate went through a VGPR -- v_cndmask + v_cmp -- before the mask; in the
+// traversal's per-iteration loop tests that is two VALU instructions each.)
+__device__ __forceinline__ unsigned long long wballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
 // ------------------------------------------------------------------ ray / hit
 struct Ray { f3 o, d; };
 struct Compact { uint32_t valid, inst, mat, prim; float bu, bv; };
@@ -464,6 +469,23 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t &total) {
     total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     return incl - v;
 }
+// A deal over the wave: lane l holds work items [excl, excl + cnt) of `total` (excl =
+// wave_excl_sum(cnt)), dealt out 64 at a time.  The owner of item c0 + lane = the last lane
+// with cnt != 0 whose excl <= c0 + lane: each such lane whose range starts inside the chunk
+// marks its start position (lane + 1; starts are distinct and ascend with the lane), position
+// 0 also takes the last owner that started before the chunk, and a prefix maximum over the
+// positions carries every mark forward.  Called by every lane; -1 past the last item.
+__device__ __forceinline__ int deal_owner(CoopLds coop, uint32_t lane, uint32_t cnt, uint32_t excl, uint32_t c0) {
+    __hip_atomic_store(&coop.mark[lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (cnt != 0u && excl >= c0 && excl - c0 < 64u)
+        __hip_atomic_store(&coop.mark[excl - c0], lane + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    uint32_t m = __hip_atomic_load(&coop.mark[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const unsigned long long before = wballot(cnt != 0u && excl < c0);
+    if (lane == 0u && before != 0ull) m = max(m, 64u - (uint32_t)__builtin_clzll(before));
+    return (int)wave_incl_max(m) - 1;
+}
 // UNI: `subs` is the workgroup's LDS copy of the root table (like `stack`): pops and root takes
 // share one code path (fewer exec-mask branches per node-loop iteration; same per-lane sequence).
 template <bool COUNT, bool PROF = false, bool ROOTQ = true, bool ANY = false, bool COOP = false, bool UNI = false>
@@ -489,7 +511,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
     for (uint32_t ii = 0; ii < sc.n_inst && (COOP || !stop); ++ii) {
         const Inst &I = insts[ii];
         const bool may = !PTX_INST_CULL || !rfin || inst_may_hit(I, ray.o, winv, omax, vy);
-        if (PTX_INST_CULL && !COUNT && __ballot(may) == 0ull) continue;  // (wave-uniform)
+        if (PTX_INST_CULL && !COUNT && wballot(may) == 0ull) continue;  // (wave-uniform)
         if (PROF) pf.hit(PROF_INST);
         // TransformRayWithMat4x4(InRay, M^-1, false), SH/PT_1_InitPass.wgsl:486-496
         // (the identity shortcut of inst_point is not used here: at the trace kernel's 128-VGPR
@@ -538,7 +560,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                 // lane the root tests, pops, tests and pushes are the reference's sequence.
                 for (;;) {
                     const bool want = leaf == 0u && (sp >= 0 || mask != 0u);
-                    if (__ballot(want) == 0ull) break;
+                    if (wballot(want) == 0ull) break;
                     if (PROF && want) pf.hit(PROF_NODE);
                     uint32_t ref = 0u;
                     bool node = false;
@@ -596,7 +618,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                 }
                 // (the whole wave must be here: after a NaN fallback lanes leave one by one)
                 if (wave_coop && __ballot(1) == ~0ull) {  // a wave-uniform leaf phase
-                    if (__ballot(leaf != 0u) == 0ull) break;
+                    if (wballot(leaf != 0u) == 0ull) break;
                     if (PROF) pf.hit(PROF_LEAF);
                     const uint32_t lane = __lane_id();
                     const uint32_t cnt = leaf ? (leaf >> 24) & 0x7Fu : 0u, lfirst = leaf & LEAF_FIRST_MASK;
@@ -620,7 +642,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                                                __HIP_MEMORY_SCOPE_WAVEFRONT);
                         __atomic_signal_fence(__ATOMIC_SEQ_CST);
                         uint32_t m = __hip_atomic_load(&coop.mark[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                        const unsigned long long before = __ballot(cnt != 0u && excl < c0);
+                        const unsigned long long before = wballot(cnt != 0u && excl < c0);
                         if (lane == 0u && before != 0ull) m = max(m, 64u - (uint32_t)__builtin_clzll(before));
                         const int owner = (int)wave_incl_max(m) - 1;
                         // triangle u of the deal is the owner's leaf triangle lfirst + (u - excl)
@@ -639,7 +661,7 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                         }
                     }
                     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    if (__ballot(nan_seen) == 0ull) {
+                    if (wballot(nan_seen) == 0ull) {
                         if (leaf) {
                             const unsigned long long key =
                                 __hip_atomic_load(&coop.key[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -751,7 +773,7 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
         // chunk of 32 roots or its next instance (transform + root pre-filter)
         for (;;) {
             const bool need = !done && leaf == 0u && sp < 0 && mask == 0u;
-            if (__ballot(need) == 0ull) break;
+            if (wballot(need) == 0ull) break;
 #ifdef PTX_WG_TIMES
             if (dbg) dbg[0]++;
 #endif
@@ -800,7 +822,7 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
         // node loop: pops and root takes through one LDS read (as trace_core_tab UNI)
         for (;;) {
             const bool want = leaf == 0u && (sp >= 0 || mask != 0u);
-            if (__ballot(want) == 0ull) break;
+            if (wballot(want) == 0ull) break;
 #ifdef PTX_WG_TIMES
             if (dbg) dbg[1]++;
 #endif
@@ -832,9 +854,9 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
             stack[(uint32_t)(sp + 2) * stride] = near;
             sp += both ? 2 : ((hl || hr) ? 1 : 0);
         }
-        const unsigned long long holders = __ballot(leaf != 0u);
+        const unsigned long long holders = wballot(leaf != 0u);
         if (holders == 0ull) {
-            if (__ballot(!done) == 0ull) break;  // every lane has walked every instance
+            if (wballot(!done) == 0ull) break;  // every lane has walked every instance
             continue;
         }
         // cooperative leaf phase (trace_core_tab COOP), the owner's triangle base included
@@ -854,15 +876,7 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
         bool nan_seen = false;
         for (uint32_t c0 = 0; c0 < total; c0 += 64u) {
             const uint32_t u = c0 + lane;
-            __hip_atomic_store(&coop.mark[lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            if (cnt != 0u && excl >= c0 && excl - c0 < 64u)
-                __hip_atomic_store(&coop.mark[excl - c0], lane + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            uint32_t m = __hip_atomic_load(&coop.mark[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            const unsigned long long before = __ballot(cnt != 0u && excl < c0);
-            if (lane == 0u && before != 0ull) m = max(m, 64u - (uint32_t)__builtin_clzll(before));
-            const int owner = (int)wave_incl_max(m) - 1;
+            const int owner = deal_owner(coop, lane, cnt, excl, c0);
             // triangle u of the deal: the owner's leaf triangle lfirst + (u - excl), in its instance
             const uint32_t tri = u + __shfl(lfirst - excl, owner);
             const uint32_t tb = __shfl(tri_base, owner);
@@ -880,7 +894,7 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
             }
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (__ballot(nan_seen) == 0ull) {
+        if (wballot(nan_seen) == 0ull) {
             if (leaf) {
                 const unsigned long long key = __hip_atomic_load(&coop.key[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                 n_tri += cnt;

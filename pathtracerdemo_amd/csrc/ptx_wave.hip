@@ -103,7 +103,7 @@ __device__ __forceinline__ void trace_lanes(const Scene &sc, const SubRoot *subs
             }
         }
         if (pool) {  // (wave-uniform) lanes that just finished their first segment
-            const unsigned long long rs = __ballot(active && seg == 1u);
+            const unsigned long long rs = wballot(active && seg == 1u);
             const uint32_t nr = (uint32_t)__popcll(rs);
             if (nr != 0u && nr < kRestartInPlace && pool_n + nr <= kRestartCap) {
                 if (active && seg == 1u) {
@@ -116,7 +116,7 @@ __device__ __forceinline__ void trace_lanes(const Scene &sc, const SubRoot *subs
                 pool_n += nr;
             }
         }
-        if (__ballot(active) == 0ull) break;
+        if (wballot(active) == 0ull) break;
     }
 }
 // Lane i of the wave traces query i of a batch (`rays` / `res` = the segment's, slot
@@ -1000,7 +1000,7 @@ void wfinal_one(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir,
         // (wave-uniform) one replayed vertex per iteration, as many as the queued form's trace
         // rounds: a path needing more is dropped there, so it is here
         for (uint32_t it = 0u; it < (uint32_t)kWaveRoundsFinal; ++it) {
-            if (__ballot(active) == 0ull) break;
+            if (wballot(active) == 0ull) break;
             if (active) {  // wfinal_emit, into this thread's slot
                 const f3 V = normalize(s.prev - s.cur.pos);
                 if (s.i + 1u < s.length) {
