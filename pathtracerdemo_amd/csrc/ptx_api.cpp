@@ -793,7 +793,7 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
             // PTX_AB=RESTART_POOL=0: every restart in place (A/B)
             static const bool pool_on = ab_knob("RESTART_POOL", 1) != 0;
             part.pool = nullptr;
-            if (use_dyn && pool_on) {
+            if (PTX_RESTART_POOL && use_dyn && pool_on) {
                 const size_t per_set = (size_t)kDynMaxGroups * (kBlock / 64) * 2u * kRestartCap;  // float4s
                 if (!h->d_wpool.p && (e = hipMalloc(&h->d_wpool.p, kRestartPoolSets * per_set * 16u)) != hipSuccess)
                     return e;

@@ -94,6 +94,10 @@ struct WaveBufs {
 // batch restart, their continuations go to the wave's pool instead (origin, remaining distance,
 // transmittance, segment, query slot) and the wave walks them later as one batch of >=
 // kRestartRun restarts (or at the end): the same per-query walks, without 60+ idle lanes each.
+// PTX_RESTART_POOL=1 builds this form (A/B: -7.5 % on the headline; default off).
+#ifndef PTX_RESTART_POOL
+#define PTX_RESTART_POOL 0
+#endif
 constexpr uint32_t kRestartCap = 64u, kRestartInPlace = 32u, kRestartRun = 32u;
 constexpr size_t kRestartPoolSets = 8u;  // (tile set, launch sequence) pairs of a frame context
 // dynamic trace batches: one workgroup per slot, at most kDynMaxGroups (the chip holds ~1024 trace

@@ -202,6 +202,54 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         const uint32_t G = w.trace_split;
         uint32_t bnext = 0u;
         if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
+        if constexpr (!PTX_RESTART_POOL) {
+            // One trace_batch per dequeued batch, every restart in place.  (The pooled loop
+            // below, one trace site fed by batches and pooled restarts, measured -7.5 % on the
+            // headline against this form: 442 vs 477 Msamples/s, tools/cl/r4_libs_ab.sh,
+            // r4_bis_ab.sh.)
+            uint32_t no_pool = 0u;
+            uint32_t bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
+            for (;;) {  // wave-uniform
+                if (bi >= c1) {  // this chunk is drained: the next head
+                    if (++visited == kDynHeads) break;
+                    x = (x + 1u) % kDynHeads;
+                    c0 = (uint32_t)((uint64_t)total * x / kDynHeads);
+                    c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
+                    if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
+                    bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
+                    continue;
+                }
+                if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);  // the next dequeue, fetched ahead
+                const uint32_t bend = min(bi + G, c1);
+                uint32_t lo = 0u;
+                for (; bi < bend; ++bi) {
+                    uint32_t hi = w.seg_count;  // last slot with pref <= bi (batches ascend: search from lo)
+                    while (hi - lo > 1u) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (pref[mid] <= bi) lo = mid;
+                        else hi = mid;
+                    }
+                    const uint32_t j = w.seg_phys + w.seg_base + lo;
+                    const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
+                    const uint32_t i = (bi - pref[lo]) * 64u + lane;
+#ifdef PTX_WG_TIMES
+                    const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
+                    uint32_t dbg[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+#else
+                    uint32_t *dbg = nullptr;
+#endif
+                    trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
+                                                                     res_all + 2u * (size_t)j * w.ray_stride,
+                                                                     w.rays + 2u * (size_t)j * w.ray_stride, 0u, i,
+                                                                     i < n, nullptr, no_pool, dbg);
+#ifdef PTX_WG_TIMES
+                    batch_record(sc.wgt, tb0, bi, round, dbg);
+#endif
+                }
+                bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
+            }
+            return;
+        }
         uint32_t bi = 0u, bend = 0u, lo = 0u;
         bool drained = false;
         // One unit of work per iteration -- the next batch, or (once kRestartRun restarts are
