@@ -342,6 +342,10 @@ int build_layout(ptx_handle *h) {
     if (nodes.empty()) nodes.resize(1);
     if (subs.empty()) subs.resize(1);
     if (mats.empty()) mats.resize(8, 0.0f);
+    // each root record carries its sub-mesh's transmission (the Visibility restart test reads
+    // it from the trace kernel's LDS root table: subs_transmission)
+    if (mats.size() != 8u * subs.size()) return fail(h, PTX_E_SCENE, "material / sub-mesh tables disagree");
+    for (size_t k = 0; k < subs.size(); ++k) std::memcpy(&subs[k].pad, &mats[8u * k + 5u], 4);
     if (int rc = upload(h, h->d_tris, tris.data(), tris.size() * sizeof(float))) return rc;
     if (int rc = upload(h, h->d_nodes, nodes.data(), nodes.size() * sizeof(NodePair))) return rc;
     if (int rc = upload(h, h->d_subs, subs.data(), subs.size() * sizeof(SubRoot))) return rc;

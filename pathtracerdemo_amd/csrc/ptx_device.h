@@ -56,7 +56,8 @@ struct alignas(16) NodePair {   // 64 B
 };
 struct alignas(16) SubRoot {    // 32 B: the root box by axis, {min, max} pairs (box_root)
     float x[2], y[2], z[2];
-    uint32_t ref, pad;
+    uint32_t ref;
+    uint32_t pad;  // the sub-mesh's transmission (f32 bits, Scene::mats word 5): subs_transmission
 };
 struct alignas(16) Inst {       // 176 B
     float m[16];

@@ -28,6 +28,12 @@ __device__ __forceinline__ Material material_at(const Scene &sc, uint32_t flat) 
 __device__ __forceinline__ float get_transmission(const Scene &sc, uint32_t inst, uint32_t mid) {
     return sc.mats[2u * mat_index(sc, inst, mid) + 1u].y;
 }
+// The same value from the root and instance tables (the trace kernels' LDS copies): each root
+// record carries its sub-mesh's transmission (SubRoot::pad, ptx_api.cpp build_layout), so a
+// Visibility restart test costs two LDS reads instead of two dependent global loads.
+__device__ __forceinline__ float subs_transmission(const SubRoot *subs, const Inst *insts, uint32_t inst, uint32_t mid) {
+    return asf(subs[insts[inst].sub_base + mid].pad);
+}
 
 // GetSurface (SH/PT_1_InitPass.wgsl:438-467) with GetTriangleWorldSpace (:390-407)
 __device__ __forceinline__ Surface get_surface(const Scene &sc, Compact x) {

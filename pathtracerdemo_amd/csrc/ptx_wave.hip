@@ -58,6 +58,9 @@ namespace ptx {
 // Measured same box (1080p): furnished C3 (13 instances) +9.7 %, GI on C3 (3) +3.2 %, reuse on
 // C3 +0.6 %, TEST_MCPT on C1 (2 instances) -3.2 %: flattened from 3 instances up.
 constexpr uint32_t kFlatMinInstances = 3u;
+#ifndef PTX_LDS_TRANS
+#define PTX_LDS_TRANS 1  // the restart test's transmission from the LDS root table (A/B: 0 = Scene::mats)
+#endif
 // The queries of one wave: lane state {ray, kind, transmittance T, remaining distance, segment}
 // for query slot gi (its result at res[2 gi]).  Visibility (SH/PT_1_InitPass.wgsl:774-802) walks
 // through transmissive hits: one trace site, looped, so the traversal code is emitted once.
@@ -86,7 +89,9 @@ __device__ __forceinline__ void trace_lanes(const Scene &sc, const SubRoot *subs
             float out = -1.0f;
             if (!h.valid || h.t > remain) out = T;
             else {
-                const float tr = kind == Q_OCC ? 0.0f : get_transmission(sc, h.s.inst, h.s.mat);
+                const float tr = kind == Q_OCC              ? 0.0f
+                                 : PTX_LDS_TRANS ? subs_transmission(subs, insts, h.s.inst, h.s.mat)
+                                                 : get_transmission(sc, h.s.inst, h.s.mat);
                 if (tr == 0.0f) out = 0.0f;
                 else {
                     T *= tr;
