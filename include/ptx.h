@@ -84,6 +84,9 @@ extern "C" {
 #define PTX_BUF_RESERVOIR 1  /* band_h * W * 32 u32 (GI pipeline: 16 u32) */
 #define PTX_BUF_ACCUM 2      /* band_h * W * 4 f32 (Scene texture: accumulated radiance) */
 #define PTX_BUF_COUNTERS 3   /* 32 u64: work counters [0..4] (PTX_FLAG_COUNT builds), diagnostics [8..) */
+/* PTX_BUF_COUNTERS word 6, every build: pixels whose history a band could not reproject (past its
+ * motion halo of reuse_radius rows; such a pixel has no temporal history); zeroed by ptx_reset_stats */
+#define PTX_COUNTER_MOTION_CLIP 6
 #define PTX_BUF_RESERVOIR_HIST 4 /* band_h * W * 32 u32: spatial output = Final's input and the
                                     next frame's temporal history (reuse pipeline)           */
 #define PTX_BUF_DIRECT 5     /* band_h * W * 4 f32: direct light of the GI init pass (GI pipeline) */

@@ -24,6 +24,7 @@ PTX_STAT_PASS_GROUP = 10
 PTX_STAT_FINAL_FUSED = 11
 PTX_BUF_GBUFFER, PTX_BUF_RESERVOIR, PTX_BUF_ACCUM, PTX_BUF_COUNTERS, PTX_BUF_RESERVOIR_HIST = 0, 1, 2, 3, 4
 PTX_BUF_DIRECT = 5
+PTX_COUNTER_MOTION_CLIP = 6  # word of PTX_BUF_COUNTERS: pixels a band could not reproject (ptx.h)
 PTX_FLAG_COUNT_WORK = 1
 PTX_FLAG_SIMPLE_KERNELS = 2
 PTX_FLAGS_RETIRED = 12  # the removed persistent-lane / tiled A/B variants: ptx_create rejects them

@@ -114,6 +114,9 @@ static int upload(ptx_handle *h, DevBuf &b, const void *src, size_t bytes) {
 // first band row of the halo-extended G-buffer / reservoir allocations
 uint4 *gbuf_band(ptx_handle *h) { return (uint4 *)h->d_gbuf.p + (size_t)h->halo_top * h->cfg.width; }
 uint4 *res_band(ptx_handle *h) { return (uint4 *)h->d_res.p + h->res_u4 * (size_t)h->halo_top * h->cfg.width; }
+// the history (spatial output) carries the same halo rows: a band's motion halo, received from
+// the neighbours before a moved camera's temporal pass (ptx_comm.cpp)
+uint4 *hist_band(ptx_handle *h) { return (uint4 *)h->d_hist.p + h->res_u4 * (size_t)h->halo_top * h->cfg.width; }
 // pipelines with the build-defined temporal / spatial passes (DI reuse, GI)
 bool has_reuse(const ptx_handle *h) {
     return h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE || h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI;
@@ -539,7 +542,7 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     ReuseArgs A{};
     A.gbuf = gbuf_band(h);
     A.cur = res_band(h);
-    A.hist = (uint4 *)h->d_hist.p;
+    A.hist = hist_band(h);
     const bool temporal = pass == PTX_PASS_TEMPORAL;
     A.jstate = (float4 *)(temporal ? h->d_tjstate.p : h->d_jstate.p);
     A.jres = (float4 *)(temporal ? h->d_tjres.p : h->d_jres.p);
@@ -579,7 +582,13 @@ static ReuseArgs motion_args(ptx_handle *h) {
     A.motion = 1u;
     std::memcpy(A.vpinv_prev, h->hist_camera, sizeof A.vpinv_prev);  // (words 4..19 of that frame)
     mat4_inverse(A.vpinv_prev, A.vp_prev);
-    A.psurf = (const uint4 *)h->d_psurf.p;
+    const size_t W = h->cfg.width;
+    A.psurf = (const uint4 *)h->d_psurf.p + 2u * (size_t)h->halo_top * W;
+    // the previous frame's rows held here: the band and its halo rows (the neighbours' surface
+    // records from that frame's exchange, their spatial output from this frame's motion halo)
+    A.prev_row_lo = -(int32_t)h->halo_top;
+    A.prev_row_hi = (int32_t)(h->band_h + h->halo_bot);
+    A.clip = (unsigned long long *)h->d_counters.p + CNT_MOTION_CLIP;
     return A;
 }
 
@@ -587,7 +596,7 @@ static GiArgs gi_args(ptx_handle *h) {
     GiArgs A{};
     A.gbuf = gbuf_band(h);
     A.cur = res_band(h);
-    A.hist = (uint4 *)h->d_hist.p;
+    A.hist = hist_band(h);
     A.direct = (float4 *)h->d_direct.p;
     A.accum = (float4 *)h->d_accum.p;
     A.jray = (uint32_t *)h->d_jres.p;
@@ -656,7 +665,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         return e;
     }
     // the reuse pipeline's PT_4 reads the spatial output
-    const uint4 *fres = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? (const uint4 *)h->d_hist.p : res;
+    const uint4 *fres = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ? (const uint4 *)hist_band(h) : res;
     // the reuse pipeline's PT_4: one launch, replays inline (PTX_AB=FINAL_ONE=0: the queued rounds)
     static const bool final_one = ab_knob("FINAL_ONE", 1) != 0;
     if (pass == PTX_PASS_FINAL && final_one && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && tables_fit_lds(sc)) {
@@ -879,8 +888,9 @@ void mat4_inverse(const float *mf, float *out) {
 
 // Before a moved-camera frame's passes: the previous frame's surface records -> d_psurf, on the
 // stream of that frame (`st`, ordered after its PT_1; a pipelined frame's next G-buffer on that
-// stream comes after the copy).  Whole-image DI reuse handles only (ptx_set_frame).
-static int motion_prepare(ptx_handle *h, hipStream_t st) {
+// stream comes after the copy).  DI reuse handles (a band's halo rows included: that frame's
+// summaries wrote them from the exchanged G-buffer rows).
+int motion_prepare(ptx_handle *h, hipStream_t st) {
     if (!h->d_surf.p) {  // (no surface records yet: nothing to reproject)
         h->hist_valid = false;
         h->hist_moved = false;
@@ -1159,7 +1169,7 @@ static bool buffer_view(ptx_handle *h, int which, DevBuf &v) {
     case PTX_BUF_DIRECT: v = h->d_direct; return v.p != nullptr;
     case PTX_BUF_ACCUM: v = h->d_accum; return true;
     case PTX_BUF_COUNTERS: v = h->d_counters; return true;
-    case PTX_BUF_RESERVOIR_HIST: v = h->d_hist; return v.p != nullptr;
+    case PTX_BUF_RESERVOIR_HIST: v.p = h->d_hist.p ? hist_band(h) : nullptr; v.bytes = px * 16u * h->res_u4; return v.p != nullptr;
     default: return false;
     }
 }
@@ -1222,7 +1232,7 @@ int ptx_create(const ptx_config *cfg, ptx_handle **out) {
     if (!rc) rc = alloc_buf(h, h->d_gbuf, px_halo * 16u);
     if (!rc) rc = alloc_buf(h, h->d_res, px_halo * 16u * h->res_u4);
     if (!rc && has_reuse(h)) {
-        rc = alloc_buf(h, h->d_hist, px * 16u * h->res_u4);
+        rc = alloc_buf(h, h->d_hist, px_halo * 16u * h->res_u4);
         if (!rc && memset_sync(h, h->d_hist.p, 0, h->d_hist.bytes) != hipSuccess) rc = PTX_E_HIP;
     }
     if (!rc && h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {
@@ -1292,12 +1302,12 @@ int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]) {
     }
     std::memcpy(h->uniform, uniform, sizeof h->uniform);
     h->frame_set = true;
-    // temporal history: a whole-image DI reuse handle reprojects it when the camera moved (the
-    // motion temporal pass); elsewhere it is reusable only for the camera that produced it
-    // (GI's temporal pass and band handles: dropped)
+    // temporal history: a DI reuse handle reprojects it when the camera moved (the motion
+    // temporal pass; a band through ptx_render with a communicator or ptx_render_bands, which
+    // bring the neighbours' rows of it); elsewhere it is reusable only for the camera that
+    // produced it (GI's temporal pass, and pass by pass: dropped)
     h->hist_moved = std::memcmp(h->hist_camera, uniform + 4, sizeof h->hist_camera) != 0;
-    const bool whole = h->band_h == h->cfg.height && !h->halo_top && !h->halo_bot && !h->comm;
-    if (h->hist_moved && !(whole && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE)) h->hist_valid = false;
+    if (h->hist_moved && h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) h->hist_valid = false;
     if (h->scene_loaded && !h->layout_valid) return build_layout(h);
     return PTX_OK;
 }

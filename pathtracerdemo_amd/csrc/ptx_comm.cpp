@@ -145,6 +145,20 @@ Rows send_up(ptx_handle *h) { return rows_of(h, h->halo_top, h->halo_top); }
 Rows send_down(ptx_handle *h) { return rows_of(h, h->halo_top + h->band_h - h->halo_bot, h->halo_bot); }
 Rows recv_top(ptx_handle *h) { return rows_of(h, 0u, h->halo_top); }
 Rows recv_bottom(ptx_handle *h) { return rows_of(h, h->halo_top + h->band_h, h->halo_bot); }
+// The motion halo: the same rows of the history (the previous frame's spatial output), which a
+// moved camera's temporal pass reprojects into (ReuseArgs::prev_row_lo / hi).
+struct HistRows {
+    char *p;
+    size_t bytes;
+};
+HistRows hist_rows_of(ptx_handle *h, uint32_t r0, uint32_t rows) {
+    const size_t W = h->cfg.width, rpx = 16u * h->res_u4;
+    return HistRows{(char *)h->d_hist.p + (size_t)r0 * W * rpx, rows * W * rpx};
+}
+HistRows hist_send_up(ptx_handle *h) { return hist_rows_of(h, h->halo_top, h->halo_top); }
+HistRows hist_send_down(ptx_handle *h) { return hist_rows_of(h, h->halo_top + h->band_h - h->halo_bot, h->halo_bot); }
+HistRows hist_recv_top(ptx_handle *h) { return hist_rows_of(h, 0u, h->halo_top); }
+HistRows hist_recv_bottom(ptx_handle *h) { return hist_rows_of(h, h->halo_top + h->band_h, h->halo_bot); }
 
 bool overlap(const ptx_handle *h) { return (h->cfg.flags & PTX_FLAG_HALO_OVERLAP) != 0; }
 
@@ -187,8 +201,12 @@ BandSets band_sets(const ptx_handle *h, const WaveBufs &w) {
 // surface records, queues; shared: history, shift jobs, accumulation.  The previous frame's
 // sends read the other context's rows, and a context's next frame starts on its stream after
 // its back passes, which wait for that frame's exchange (ev_halo): nothing is overwritten in
-// flight.
-int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w, bool &pipe) {
+// flight.  A moved camera (DI reuse, history valid: `moved`) reprojects the history: the previous
+// frame's surface records are copied first (motion_prepare, before the context swap), and the
+// neighbours' rows of its spatial output arrive as the motion halo before the temporal pass.
+// ev_prev marks everything enqueued before this frame on the previous frame's stream (pipelined
+// or not: a neighbour's motion-halo copy waits for it).
+int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w, bool &pipe, bool &moved) {
     if (!has_reuse(h)) return fail(h, PTX_E_INVALID, "band frames need the reuse or GI pipeline");
     if (h->cfg.flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK))
         return fail(h, PTX_E_INVALID, "band frames run the wavefront kernels (no counting / A-B variants)");
@@ -197,12 +215,17 @@ int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w, bool &pipe) {
         if (int rc = build_layout(h)) return rc;
     sc = make_scene(h);
     if (!tables_fit_lds(sc)) return fail(h, PTX_E_SCENE, "band frames need the LDS root / instance tables");
-    pipe = pipelined(h);
-    if (pipe) {
-        if (int rc = ensure_alt(h)) return rc;
-        HIP_CHECK(h, hipEventRecord(h->ev_prev, h->stream));
-        swap_frame_ctx(h);
+    moved = h->hist_valid && h->hist_moved && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
+    if (moved) {
+        if (int rc = motion_prepare(h, h->stream)) return rc;
+        moved = h->hist_moved;
     }
+    pipe = pipelined(h);
+    if (pipe)
+        if (int rc = ensure_alt(h)) return rc;
+    if (!h->ev_prev) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_prev, hipEventDisableTiming));
+    HIP_CHECK(h, hipEventRecord(h->ev_prev, h->stream));
+    if (pipe) swap_frame_ctx(h);
     if (int rc = wave_buffers(h, w)) return rc;
     if (int rc = reuse_buffers(h)) return rc;
     hipError_t e = hipSuccess;
@@ -215,25 +238,30 @@ int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w, bool &pipe) {
     return PTX_OK;
 }
 
-// G-buffer -> PT_1 -> temporal over the whole band, then ev_front on h->stream.  Pipelined:
-// the temporal pass (it reads the previous frame's spatial output and shares its job buffers)
-// waits for ev_prev.
-int band_front(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *&frame_t, bool pipe) {
+// G-buffer -> PT_1 -> temporal over the whole band, then ev_front on h->stream, in two calls:
+// band_front (everything before the wait for the previous frame: G-buffer, PT_1 and, pipelined,
+// the still camera's temporal jobs; unpipelined and still, the whole temporal pass) and
+// band_temporal (after it: the temporal combine, or a moved camera's whole motion pass, once the
+// motion halo has landed -- the caller exchanges it in between).
+int band_front(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *&frame_t, bool pipe, bool moved) {
     frame_t = &h->ring[h->ring_pos];
     h->ring_pos = (h->ring_pos + 1) % kEventRing;
     resolve_event(*frame_t, h);
     HIP_CHECK(h, hipEventRecord(frame_t->start, h->stream));
     static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_TEMPORAL};
-    static const int front_split[4] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, kPassTemporalJobs, kPassTemporalCombine};
-    hipError_t e;
-    if (pipe) {  // (the temporal jobs before the wait, the temporal combine after: timed_wave_frame)
-        e = launch_wave_parts(h, sc, w, front_split, 3);
-        if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
-        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, front_split + 3, 1);
-    } else {
-        e = launch_wave_parts(h, sc, w, front, 3);
-    }
+    static const int front_split[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, kPassTemporalJobs};
+    // (the temporal jobs before the wait, the temporal combine after: timed_wave_frame)
+    const hipError_t e = launch_wave_parts(h, sc, w, pipe ? front_split : front, moved ? 2 : 3);
     if (e != hipSuccess) return fail(h, PTX_E_HIP, "band front passes: %s", hipGetErrorString(e));
+    if (pipe) HIP_CHECK(h, hipStreamWaitEvent(h->stream, h->ev_prev, 0));
+    return PTX_OK;
+}
+int band_temporal(ptx_handle *h, const Scene &sc, const WaveBufs &w, bool pipe, bool moved) {
+    static const int combine[1] = {kPassTemporalCombine}, motion[1] = {kPassTemporalMotion};
+    if (moved || pipe) {
+        const hipError_t e = launch_wave_parts(h, sc, w, moved ? motion : combine, 1);
+        if (e != hipSuccess) return fail(h, PTX_E_HIP, "band temporal pass: %s", hipGetErrorString(e));
+    }
     HIP_CHECK(h, hipEventRecord(h->ev_front, h->stream));
     return PTX_OK;
 }
@@ -266,6 +294,28 @@ int nccl_halo(ptx_handle *h, hipStream_t xs) {
         NCCL_CHECK(h, R.send(s.r, s.rb, ncclUint8, h->rank + 1, c, xs));
         NCCL_CHECK(h, R.recv(r.g, r.gb, ncclUint8, h->rank + 1, c, xs));
         NCCL_CHECK(h, R.recv(r.r, r.rb, ncclUint8, h->rank + 1, c, xs));
+    }
+    return PTX_OK;
+}
+
+// A moved camera's motion halo over the communicator, on h->stream after the wait for the previous
+// frame (its spatial output is complete there, and this frame's spatial pass comes after):
+// this band's first / last rows of the history to the neighbours, theirs into its halo rows.
+// Every rank of a frame moves or none (the same camera): the groups stay matched.
+int nccl_motion_halo(ptx_handle *h) {
+    const Rccl &R = rccl();
+    ncclComm_t c = (ncclComm_t)h->comm;
+    if (h->halo_top) {
+        const HistRows s = hist_send_up(h), r = hist_recv_top(h);
+        NCCL_CHECK(h, R.send(s.p, s.bytes, ncclUint8, h->rank - 1, c, h->stream));
+        NCCL_CHECK(h, R.recv(r.p, r.bytes, ncclUint8, h->rank - 1, c, h->stream));
+        h->halo_bytes_sent += s.bytes;
+    }
+    if (h->halo_bot) {
+        const HistRows s = hist_send_down(h), r = hist_recv_bottom(h);
+        NCCL_CHECK(h, R.send(s.p, s.bytes, ncclUint8, h->rank + 1, c, h->stream));
+        NCCL_CHECK(h, R.recv(r.p, r.bytes, ncclUint8, h->rank + 1, c, h->stream));
+        h->halo_bytes_sent += s.bytes;
     }
     return PTX_OK;
 }
@@ -368,10 +418,20 @@ int render_band_nccl(ptx_handle *h) {
     if (int rc = comm_health(h)) return rc;
     Scene sc{};
     WaveBufs w{};
-    bool pipe = false;
-    if (int rc = band_prepare(h, sc, w, pipe)) return rc;
+    bool pipe = false, moved = false;
+    if (int rc = band_prepare(h, sc, w, pipe, moved)) return rc;
     TimedLaunch *ft = nullptr;
-    if (int rc = band_front(h, sc, w, ft, pipe)) return rc;
+    if (int rc = band_front(h, sc, w, ft, pipe, moved)) return rc;
+    if (moved) {
+        NCCL_CHECK(h, rccl().group_start());
+        const int rc = nccl_motion_halo(h);
+        if (rc) {
+            (void)rccl().group_end();
+            return rc;
+        }
+        if (int r2 = group_end_wait(h)) return r2;
+    }
+    if (int rc = band_temporal(h, sc, w, pipe, moved)) return rc;
     hipStream_t xs;
     if (int rc = exchange_stream(h, xs)) return rc;
     NCCL_CHECK(h, rccl().group_start());
@@ -420,10 +480,11 @@ static int halo_proxy(ptx_handle *h, hipStream_t xs, uint32_t us) {
 int render_band_solo(ptx_handle *h) {
     Scene sc{};
     WaveBufs w{};
-    bool pipe = false;
-    if (int rc = band_prepare(h, sc, w, pipe)) return rc;
+    bool pipe = false, moved = false;
+    if (int rc = band_prepare(h, sc, w, pipe, moved)) return rc;
     TimedLaunch *ft = nullptr;
-    if (int rc = band_front(h, sc, w, ft, pipe)) return rc;
+    if (int rc = band_front(h, sc, w, ft, pipe, moved)) return rc;
+    if (int rc = band_temporal(h, sc, w, pipe, moved)) return rc;  // (a motion halo keeps what it holds)
     hipStream_t xs;
     if (int rc = exchange_stream(h, xs)) return rc;
     static const int proxy_us = ab_knob("HALO_PROXY_US", 0);
@@ -556,11 +617,54 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
     std::vector<WaveBufs> w(n);
     std::vector<TimedLaunch *> ft(n);
     std::vector<hipStream_t> xs(n);
+    std::vector<char> pipe(n), moved(n);
     for (int i = 0; i < n; ++i) {
         HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
-        bool pipe = false;
-        if (int rc = band_prepare(hs[i], sc[i], w[i], pipe)) return rc;
-        if (int rc = band_front(hs[i], sc[i], w[i], ft[i], pipe)) return rc;
+        bool p = false, m = false;
+        if (int rc = band_prepare(hs[i], sc[i], w[i], p, m)) return rc;
+        pipe[i] = p;
+        moved[i] = m;
+        if (int rc = band_front(hs[i], sc[i], w[i], ft[i], p, m)) return rc;
+    }
+    for (int i = 1; i < n; ++i)
+        if (moved[i] != moved[0])
+            return fail(hs[i], PTX_E_INVALID, "ptx_render_bands: band %d %s the history and band 0 %s", i,
+                        moved[i] ? "reprojects" : "does not reproject", moved[0] ? "does" : "does not");
+    if (moved[0]) {  // the motion halo: the neighbours' rows of the previous frame's spatial output
+        if (nccl) {
+            NCCL_CHECK(h0, rccl().group_start());
+            int rc = PTX_OK;
+            for (int i = 0; i < n && !rc; ++i) rc = nccl_motion_halo(hs[i]);
+            NCCL_CHECK(h0, rccl().group_end());
+            if (rc) return rc;
+        } else {
+            // peer copies once the neighbour's previous frame is complete (its ev_prev); the
+            // neighbours' spatial passes, which rewrite those rows, wait for ev_mhalo (below)
+            for (int i = 0; i < n; ++i) {
+                ptx_handle *h = hs[i];
+                HIP_CHECK(h, hipSetDevice(h->device));
+                if (i > 0 && h->halo_top) {
+                    ptx_handle *a = hs[i - 1];
+                    const HistRows s = hist_send_down(a), r = hist_recv_top(h);
+                    if (s.bytes != r.bytes) return fail(h, PTX_E_INVALID, "motion halo of band %d does not match band %d", i, i - 1);
+                    HIP_CHECK(h, hipStreamWaitEvent(h->stream, a->ev_prev, 0));
+                    HIP_CHECK(h, hipMemcpyPeerAsync(r.p, h->device, s.p, a->device, r.bytes, h->stream));
+                }
+                if (i + 1 < n && h->halo_bot) {
+                    ptx_handle *b = hs[i + 1];
+                    const HistRows s = hist_send_up(b), r = hist_recv_bottom(h);
+                    if (s.bytes != r.bytes) return fail(h, PTX_E_INVALID, "motion halo of band %d does not match band %d", i, i + 1);
+                    HIP_CHECK(h, hipStreamWaitEvent(h->stream, b->ev_prev, 0));
+                    HIP_CHECK(h, hipMemcpyPeerAsync(r.p, h->device, s.p, b->device, r.bytes, h->stream));
+                }
+                if (!h->ev_mhalo) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_mhalo, hipEventDisableTiming));
+                HIP_CHECK(h, hipEventRecord(h->ev_mhalo, h->stream));
+            }
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
+        if (int rc = band_temporal(hs[i], sc[i], w[i], pipe[i], moved[i])) return rc;
     }
     for (int i = 0; i < n; ++i)
         if (int rc = exchange_stream(hs[i], xs[i])) return rc;
@@ -602,6 +706,10 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
     }
     for (int i = 0; i < n; ++i) {
         HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
+        if (moved[0] && !nccl) {  // (the neighbours have copied this band's history rows)
+            if (i > 0) HIP_CHECK(hs[i], hipStreamWaitEvent(hs[i]->stream, hs[i - 1]->ev_mhalo, 0));
+            if (i + 1 < n) HIP_CHECK(hs[i], hipStreamWaitEvent(hs[i]->stream, hs[i + 1]->ev_mhalo, 0));
+        }
         if (int rc = band_back(hs[i], sc[i], w[i], ft[i])) return rc;
     }
     if (!nccl) {  // the next frame's front passes must not overwrite rows a neighbour still copies
@@ -636,6 +744,7 @@ void comm_destroy(ptx_handle *h) {
     h->xstream = nullptr;
     if (h->ev_front) (void)hipEventDestroy(h->ev_front);
     if (h->ev_halo) (void)hipEventDestroy(h->ev_halo);
-    h->ev_front = h->ev_halo = nullptr;
+    if (h->ev_mhalo) (void)hipEventDestroy(h->ev_mhalo);
+    h->ev_front = h->ev_halo = h->ev_mhalo = nullptr;
 }
 }  // namespace ptx

@@ -402,6 +402,10 @@ __device__ __forceinline__ void complete_hit(const Scene &sc, const Ray &ray, Pa
 // every query it traces (CNT_CULL_MISS: a culled lane whose root pre-filter passed) without
 // culling; the other builds skip an instance when no lane of the wave may reach it.
 constexpr int CNT_CULL_MISS = 5;
+// every build: pixels of a moved camera's temporal pass whose reprojection fell past the rows of
+// the previous frame the band holds (its motion halo; ReuseArgs::prev_row_lo / hi) -- such a
+// pixel gets no history, where the whole image would have had it (0 keeps bands bit-identical)
+constexpr int CNT_MOTION_CLIP = 6;
 __device__ __forceinline__ bool inst_may_hit(const Inst &I, f3 o, f3 winv, float omax, float vy) {
     if (!(I.wpad >= 0.0f)) return true;
     const float p = I.wpad + I.wscale * omax;

@@ -127,6 +127,9 @@ struct ptx_handle {
     int rank = 0, world = 1;
     hipStream_t xstream = nullptr;
     hipEvent_t ev_front = nullptr, ev_halo = nullptr;
+    // ptx_render_bands without communicators, moved camera: this band has copied its motion halo
+    // (the neighbours' previous spatial output) -- their spatial passes overwrite it after this
+    hipEvent_t ev_mhalo = nullptr;
     uint64_t halo_bytes_sent = 0;  // halo bytes this handle's communicator has sent (ptx_comm_info)
     // ptx_present's canvas on the device; the pinned staging buffer of read_to_host
     DevBuf d_canvas;
@@ -171,6 +174,8 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
 // the neighbour summaries of the halo rows (or of everything when the band's are stale)
 hipError_t spatial_summaries(ptx_handle *h, hipStream_t st);
 void mark_history(ptx_handle *h);
+int motion_prepare(ptx_handle *h, hipStream_t st);
+uint4 *hist_band(ptx_handle *h);
 // frame pipelining: whether ptx_render runs this handle's frames two in flight; wait for both
 // frames' streams (before anything that replaces shared buffers or the stream)
 bool pipelined(const ptx_handle *h);

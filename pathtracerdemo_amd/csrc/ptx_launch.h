@@ -123,7 +123,8 @@ constexpr int kWaveRoundsReuse = 3;
 struct ReuseArgs {
     const uint4 *gbuf;  // G-buffer of the band's first row; halo rows at negative / >= npix indices
     uint4 *cur;         // PT_1 reservoirs (temporal output in place), same addressing
-    uint4 *hist;        // spatial output = PT_4 input = next frame's history (band only)
+    uint4 *hist;        // spatial output = PT_4 input = next frame's history, cur's addressing
+                        // (a band's halo rows: the neighbours' previous spatial output, motion pass)
     float4 *jstate;     // shift-job state, 6 float4 slots x njobs (SoA)
     float4 *jres;       // per job: {f (PathContribution, rgb), q} (q = 0: invalid); p_hat = Luminance(f)
     uint32_t njobs, jpp;  // jobs of the pass (npix * jpp), jobs per pixel
@@ -146,10 +147,14 @@ struct ReuseArgs {
                         // loads but does not use) never sends the fold's gather out of bounds
     // temporal reuse under camera motion (wtmotion_*, ptx_reuse.hip): the previous frame's
     // VP^-1 (its camera points) and VP (the reprojection), its primary-hit surface records
-    // (the whole image, cur's addressing); motion = 1 selects the pass
+    // (cur's addressing); motion = 1 selects the pass.  hist / psurf hold the previous frame's
+    // band rows [prev_row_lo, prev_row_hi) (band-relative: a band's motion halo, the whole image
+    // [0, H)); a pixel reprojected outside them has no history (and counts in *clip)
     uint32_t motion;
     float vpinv_prev[16], vp_prev[16];
     const uint4 *psurf;
+    int32_t prev_row_lo, prev_row_hi;
+    unsigned long long *clip;  // nullptr: not counted
 };
 // the motion temporal pass's jobs per pixel: the canonical sample at home, the reprojected
 // history sample here, the canonical sample in the previous frame's domain

@@ -56,9 +56,11 @@ __device__ __forceinline__ const uint4 *res_at(const uint4 *base, int32_t idx) {
 // A job's sample reservoir: a band index into cur (the pass's reservoirs, halo rows < 0 or
 // >= npix), or kHistRef + index into hist -- the motion temporal pass's reprojected history
 // sample, which lives in the previous frame's spatial output.
-constexpr int32_t kHistRef = 1 << 29;
+// (hist indices may be negative too -- a band's motion halo rows above it: every index of either
+// buffer lies within 2^28 of 0, so refs at or above 2^29 are history refs)
+constexpr int32_t kHistRef = 1 << 30;
 __device__ __forceinline__ const uint4 *res_of(const ReuseArgs &A, int32_t ref) {
-    return ref >= kHistRef ? A.hist + 8 * (ptrdiff_t)(ref - kHistRef) : A.cur + 8 * (ptrdiff_t)ref;
+    return ref >= (kHistRef >> 1) ? A.hist + 8 * (ptrdiff_t)(ref - kHistRef) : A.cur + 8 * (ptrdiff_t)ref;
 }
 // a job whose domain is not a pixel of this frame (the previous frame's, motion temporal pass):
 // stored in the full layout, as the fresh one re-derives the domain from this frame's records
@@ -452,7 +454,9 @@ __device__ __forceinline__ f3 x0_prev(const ReuseArgs &A, const Scene &sc, uint3
 struct MotionHist { bool ok; int32_t pp; uint32_t px, py, C; };
 // p' of pixel pix's primary hit X1 and the disocclusion test (oracle reproject / motion_valid):
 // C = min(C_hist, cap) when the history at p' is usable, else 0
-__device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseArgs &A, const Surface &X1) {
+// (count: this call counts a reprojection past the band's motion halo in A.clip)
+__device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseArgs &A, const Surface &X1,
+                                                  bool count = false) {
     MotionHist m{false, 0, 0u, 0u, 0u};
     if (!A.hist_valid) return m;
     const float *vp = A.vp_prev;
@@ -466,7 +470,14 @@ __device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseAr
     if (!(fx >= 0.0f && fx < W && fy >= 0.0f && fy < H)) return m;
     m.px = (uint32_t)fx;
     m.py = (uint32_t)fy;
-    m.pp = (int32_t)(m.py * sc.width + m.px);  // (whole-image handles only)
+    // p' in the band's addressing: the previous frame's rows this handle holds are its band and
+    // the motion halo received from the neighbours (the whole image: every row)
+    const int32_t ry = (int32_t)m.py - (int32_t)sc.row_begin;
+    if (ry < A.prev_row_lo || ry >= A.prev_row_hi) {
+        if (count && A.clip) atomicAdd(A.clip, 1ull);
+        return m;
+    }
+    m.pp = ry * (int32_t)sc.width + (int32_t)m.px;
     const uint4 a = A.psurf[2 * (ptrdiff_t)m.pp];
     if (a.w == kNoSurface) return m;
     const uint4 b = A.psurf[2 * (ptrdiff_t)m.pp + 1];
@@ -509,7 +520,7 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
             const bool live = job_emit(sc, g, A, act, s, jid, act ? rv[0].x : 0u);
             job_finish(g, JL, A, live, s, jid);
         }
-        const MotionHist mh = valid ? motion_hist(sc, A, X1) : MotionHist{false, 0, 0u, 0u, 0u};
+        const MotionHist mh = valid ? motion_hist(sc, A, X1, true) : MotionHist{false, 0, 0u, 0u, 0u};
         // slot 1: the history sample at p' in this pixel's domain
         {
             const uint32_t jid = job_id(A, pix, 1u);

@@ -205,7 +205,10 @@ class Renderer:
         # cull_misses: queries of the counting build whose instance cull would have skipped an
         # instance with a root its pre-filter passes (the cull's conservativeness check: always 0)
         return {"rays": int(c[0]), "instance_xforms": int(c[1]), "aabb_tests": int(c[2]), "tri_tests": int(c[3]),
-                "hits": int(c[4]), "cull_misses": int(c[5])}
+                "hits": int(c[4]), "cull_misses": int(c[5]),
+                # motion_clips (every build): pixels of a moved camera's frames whose reprojection
+                # fell past a band's motion halo (no history there; 0 keeps bands bit-identical)
+                "motion_clips": int(c[N.PTX_COUNTER_MOTION_CLIP])}
 
     def stats(self) -> dict:
         s = N.PtxStats()

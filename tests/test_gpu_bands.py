@@ -192,3 +192,79 @@ def test_pipelined_band_frames_with_host_reads(scene3):
         assert_same(np.concatenate([b.read_image() for b in bands]), one.read_image(), f"radiance, frame {f + 1}")
     for r in [one] + bands:
         r.close()
+
+
+# tests/test_gpu_reuse.py's interactive camera path (5 units/s at 60 Hz, a yaw turn, still frames)
+MOTION_PATH = [((0.0, 0.0, 6.0), 0.0), ((0.083, 0.0, 6.0), 0.0), ((0.166, 0.0, 5.95), 0.0),
+               ((0.25, 0.02, 5.9), 1.5), ((0.25, 0.02, 5.9), 3.0), ((0.2, 0.02, 5.85), 4.5),
+               ((0.2, 0.02, 5.85), 4.5), ((0.12, 0.0, 5.8), 3.0)]
+
+
+def pose(r, loc, yaw, pitch=0.0):
+    r.GetCamera().set_location(*loc)
+    r.GetCamera().set_yaw(yaw)
+    r.GetCamera().set_pitch(pitch)
+    r.Update()
+
+
+@pytest.mark.parametrize("cuts,overlap", [([32, 64], False), ([30, 63], True)])
+def test_moving_camera_bands_bit_identical(scene3, cuts, overlap):
+    """A moving camera through band handles (ptx_render_bands, peer copies): each band reprojects
+    its history, the previous frame's spatial output of the rows above / below it arriving first
+    as the motion halo (reuse_radius rows, the neighbours' band rows); after every frame of the
+    path the split equals the single handle bit for bit, no reprojection left a band's motion
+    halo, and the reprojected history was used."""
+    from pathtracerdemo_amd.renderer import Renderer
+    W, H = 96, 96
+    one = make(scene3, W, H)
+    bounds = [0] + cuts + [H]
+    bands = [make(scene3, W, H, row_begin=a, row_end=b, halo_overlap=overlap) for a, b in zip(bounds, bounds[1:])]
+    for f, (loc, yaw) in enumerate(MOTION_PATH, start=1):
+        pose(one, loc, yaw)
+        one.Render()
+        for b in bands:
+            pose(b, loc, yaw)
+        Renderer.render_bands(bands)
+        hist = np.concatenate([b.read_history() for b in bands])
+        assert_same(hist, one.read_history(), f"spatial output, frame {f}")
+        assert_same(np.concatenate([b.read_reservoir() for b in bands]), one.read_reservoir(), f"temporal output, frame {f}")
+        assert_same(np.concatenate([b.read_image() for b in bands]), one.read_image(), f"radiance, frame {f}")
+    assert sum(b.read_counters()["motion_clips"] for b in bands) == 0
+    assert (one.read_reservoir()[..., 29] > 1).mean() > 0.3  # the history survived the moves
+    for r in [one] + bands:
+        r.close()
+
+
+def test_band_motion_past_the_halo_is_counted(scene3):
+    """A pitch jump that moves rows by more than the motion halo (R = 6 rows): the pixels whose
+    history lies past it get none, and are counted (PTX_COUNTER_MOTION_CLIP); the frames still
+    render, finite."""
+    from pathtracerdemo_amd.renderer import Renderer
+    W, H, R = 64, 96, 6
+    bands = [make(scene3, W, H, radius=R, row_begin=a, row_end=b) for a, b in ((0, 48), (48, 96))]
+    for f, pitch in enumerate((0.0, 0.0, 12.0, 12.0), start=1):
+        for b in bands:
+            pose(b, (0.0, 0.0, 6.0), 0.0, pitch)
+        img = np.zeros((H, W, 4), np.float32)
+        Renderer.render_bands(bands, img)
+        assert np.isfinite(img).all()
+    assert sum(b.read_counters()["motion_clips"] for b in bands) > 0
+    for b in bands:
+        b.close()
+
+
+def test_communicator_band_moving_camera(scene3):
+    """The RCCL band path (ptx_comm_init, world 1: no neighbours) along the moving-camera path:
+    its motion temporal pass matches the plain handle's frame by frame."""
+    from pathtracerdemo_amd.renderer import Renderer
+    W, H = 96, 64
+    a, b = make(scene3, W, H), make(scene3, W, H)
+    b.comm_init(Renderer.comm_unique_id(), 0, 1)
+    for f, (loc, yaw) in enumerate(MOTION_PATH[:5], start=1):
+        for r in (a, b):
+            pose(r, loc, yaw)
+            r.Render()
+        assert_same(b.read_history(), a.read_history(), f"spatial output, frame {f}")
+        assert_same(b.read_image(), a.read_image(), f"radiance, frame {f}")
+    for r in (a, b):
+        r.close()
