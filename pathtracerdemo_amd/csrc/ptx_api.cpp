@@ -533,9 +533,10 @@ int reuse_buffers(ptx_handle *h) {
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) return alloc_buf(h, h->d_jres, njobs * 4u);  // ray index per job
     if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
     if (int rc = alloc_buf(h, h->d_nbr, px_with_halo(h) * 16u)) return rc;
+    // per frame context: the temporal pass's jobs (one per pixel; the motion pass's kMotionJobs)
     const size_t npix = (size_t)h->band_h * h->cfg.width;
-    if (int rc = alloc_buf(h, h->d_tjstate, npix * 6u * 16u)) return rc;
-    if (int rc = alloc_buf(h, h->d_tjres, npix * 16u)) return rc;
+    if (int rc = alloc_buf(h, h->d_tjstate, npix * kMotionJobs * 6u * 16u)) return rc;
+    if (int rc = alloc_buf(h, h->d_tjres, npix * kMotionJobs * 16u)) return rc;
     return alloc_buf(h, h->d_jres, njobs * 16u);
 }
 static ReuseArgs reuse_args(ptx_handle *h, int pass) {
@@ -566,16 +567,23 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
     return A;
 }
 
-// The motion temporal pass (wtmotion_*): the spatial pass's shift-job buffers (free again once
-// the previous frame's spatial pass is done, which this pass waits for like the still one), the
-// history reprojected through the previous frame's camera.
+// The motion temporal pass (wtmotion_*): the frame context's temporal job buffers (three job
+// planes; so its first part may run before the previous frame's spatial pass, which owns the
+// spatial job buffers, is done), the history reprojected through the previous frame's camera.
+// `pass`: the whole pass, its jobs before the wait (slots 0 and 2, the reprojection test on
+// geometry only) or the rest after it (slot 1 and the combine).
 void mat4_inverse(const float *mf, float *out);
-static ReuseArgs motion_args(ptx_handle *h) {
+static ReuseArgs motion_args(ptx_handle *h, int pass) {
     ReuseArgs A = reuse_args(h, PTX_PASS_SPATIAL);
-    A.jpp = (uint32_t)reuse_jobs_per_px(h);
+    A.jstate = (float4 *)h->d_tjstate.p;
+    A.jres = (float4 *)h->d_tjres.p;
+    A.jpp = kMotionJobs;
     A.njobs = h->band_h * h->cfg.width * A.jpp;
     static const bool planes = ab_knob("JOB_PLANES", 1) != 0;
     A.jpx = planes ? 1u : A.jpp;
+    A.jslot = planes ? h->band_h * h->cfg.width : 1u;
+    A.motion_slots = pass == kPassTemporalMotionJobs ? 5u : pass == kPassTemporalMotionCombine ? 2u : 7u;
+    A.motion_geom = pass == kPassTemporalMotionJobs ? 1u : 0u;
     A.hist_valid = h->hist_valid ? 1u : 0u;
     A.use_init = h->init_state_valid ? 1u : 0u;
     A.fold_last = 0u;
@@ -639,17 +647,17 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         return e;
     }
     if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL || pass == kPassTemporalJobs ||
-        pass == kPassTemporalCombine || pass == kPassTemporalMotion) {
+        pass == kPassTemporalCombine || is_motion_pass(pass)) {
         const bool temporal = pass != PTX_PASS_SPATIAL;
-        ReuseArgs A = pass == kPassTemporalMotion ? motion_args(h)
-                                                  : reuse_args(h, temporal ? PTX_PASS_TEMPORAL : PTX_PASS_SPATIAL);
+        ReuseArgs A = is_motion_pass(pass) ? motion_args(h, pass)
+                                           : reuse_args(h, temporal ? PTX_PASS_TEMPORAL : PTX_PASS_SPATIAL);
         WaveBufs wj = w;
         if (A.fold_last && wj.res[2]) wj.nres = 3;  // light segments finished by the combine
         else A.fold_last = 0u;
         const int nr = reuse_rounds(temporal, A);
         // (the temporal pass in parts: its jobs = rounds 0..nr, its combine = round nr + 1)
         const int r_first = pass == kPassTemporalCombine ? nr + 1 : 0;
-        const int r_last = pass == kPassTemporalJobs ? nr : nr + 1;
+        const int r_last = pass == kPassTemporalJobs || pass == kPassTemporalMotionJobs ? nr : nr + 1;
         for (int r = r_first; e == hipSuccess && r <= r_last; ++r) {
             if (r > 0 && r <= nr) {
                 TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
@@ -752,7 +760,7 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
         if (passes[i] == PTX_PASS_SPATIAL) {
             if (summaries && (e = spatial_summaries(h, h->stream)) != hipSuccess) return e;
         } else if (passes[i] != PTX_PASS_FINAL && passes[i] != PTX_PASS_TEMPORAL && passes[i] != kPassTemporalJobs &&
-                   passes[i] != kPassTemporalCombine && passes[i] != kPassTemporalMotion) {
+                   passes[i] != kPassTemporalCombine && !is_motion_pass(passes[i])) {
             h->nbr_valid = false;  // G-buffer / PT_1 / MCPT rewrite what the summaries describe
         }
     }
@@ -762,11 +770,12 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     bool surf_ok = h->surf_valid;
     for (int i = 0; i < npasses && i < 8; ++i) {
         if (passes[i] == PTX_PASS_GBUFFER) surf_ok = false;
-        else if (passes[i] == PTX_PASS_INIT && w.surf) surf_ok = true;
+        else if (passes[i] == PTX_PASS_INIT && w.surf) surf_ok = true, h->ev_surf_ok = false;
         else if ((passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalJobs || passes[i] == PTX_PASS_SPATIAL ||
-                  passes[i] == kPassTemporalMotion) &&
+                  is_motion_pass(passes[i])) &&
                  w.surf) {
             need_surf[i] = !surf_ok;
+            if (need_surf[i]) h->ev_surf_ok = false;
             surf_ok = true;
         }
     }
@@ -841,7 +850,8 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     }
     // the temporal pass rewrote the reservoirs PT_1's state describes, and summarised them
     for (int i = 0; i < npasses; ++i)
-        if (passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalCombine || passes[i] == kPassTemporalMotion) {
+        if (passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalCombine || passes[i] == kPassTemporalMotion ||
+            passes[i] == kPassTemporalMotionCombine) {
             h->init_state_valid = false;
             h->nbr_valid = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
         }
@@ -949,6 +959,7 @@ static void swap_two(ptx_handle *h);
 // The next context (round robin over pipe_depth() contexts): the members become the next
 // context's, `alt` (and `alt2`) the ones after it.
 void swap_frame_ctx(ptx_handle *h) {
+    h->ev_surf_ok = false;  // (ev_surf describes the surface records of the context it was recorded on)
     swap_two(h);
     if (pipe_depth() == 3) std::swap(h->alt, h->alt2);
     h->ctx_idx = (h->ctx_idx + 1) % pipe_depth();
@@ -1022,6 +1033,12 @@ int leave_alt(ptx_handle *h) {
     return PTX_OK;
 }
 
+static int ensure_motion_events(ptx_handle *h) {
+    for (hipEvent_t *ev : {&h->ev_surf, &h->ev_psurf, &h->ev_motion})
+        if (!*ev) HIP_CHECK(h, hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    return PTX_OK;
+}
+
 // A whole ReSTIR frame in wavefront form (G-buffer -> init -> final per segment group), timed
 // as one unit in stats slot PTX_STAT_FRAME.  Returns 1 if this path does not apply.
 static int timed_wave_frame(ptx_handle *h) {
@@ -1036,9 +1053,17 @@ static int timed_wave_frame(ptx_handle *h) {
     if (!tables_fit_lds(sc)) return 1;
     const bool pipe = pipelined(h);
     // a moved camera (whole-image DI reuse): the history is reprojected, from the previous
-    // frame's surface records, copied first on that frame's stream (the current one here)
+    // frame's surface records.  Pipelined (two contexts), the motion pass runs in two parts
+    // like the still temporal pass (msplit): the previous frame's records are copied on THIS
+    // frame's stream once that frame's PT_1 is done (ev_surf) and its slot-0 / slot-2 jobs run
+    // before the wait for the previous frame; otherwise they are copied first on the previous
+    // frame's stream (the current one here) and the whole pass runs after the wait.
+    // PTX_AB=MOTION_SPLIT=0: the latter always.
+    static const bool msplit_on = ab_knob("MOTION_SPLIT", 1) != 0;
     bool moved = h->hist_valid && h->hist_moved && has_reuse(h) && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
-    if (moved) {
+    const bool msplit = moved && pipe && msplit_on && pipe_depth() == 2 && h->ev_surf_ok && h->d_surf.p;
+    const DevBuf prev_surf = h->d_surf;  // (the previous frame's context, before the swap)
+    if (moved && !msplit) {
         if (int rc = motion_prepare(h, h->stream)) return rc;
         moved = h->hist_moved;
     }
@@ -1065,13 +1090,37 @@ static int timed_wave_frame(ptx_handle *h) {
         // (a moved camera: the whole motion temporal pass after the wait -- its history jobs read
         // the previous frame's spatial output)
         static const bool split = ab_knob("TEMPORAL_SPLIT", 1) != 0;
-        static const int front[3] = {PTX_PASS_GBUFFER, PTX_PASS_INIT, kPassTemporalJobs};
+        static const int front[2] = {PTX_PASS_GBUFFER, PTX_PASS_INIT};
+        static const int jobs[1] = {kPassTemporalJobs}, jobs_m[1] = {kPassTemporalMotionJobs};
         static const int temporal[1] = {PTX_PASS_TEMPORAL}, temporal_b[1] = {kPassTemporalCombine};
-        static const int temporal_m[1] = {kPassTemporalMotion};
+        static const int temporal_m[1] = {kPassTemporalMotion}, temporal_mb[1] = {kPassTemporalMotionCombine};
         static const int back[2] = {PTX_PASS_SPATIAL, PTX_PASS_FINAL};
-        e = launch_wave_parts(h, sc, w, front, split && !moved ? 3 : 2);
+        if (int rc = ensure_motion_events(h)) return rc;
+        // (the frame after a split motion pass rewrites the surface records it copied)
+        if (h->psurf_wait) HIP_CHECK(h, hipStreamWaitEvent(h->stream, h->ev_psurf, 0));
+        h->psurf_wait = false;
+        e = launch_wave_parts(h, sc, w, front, 2);
+        if (e == hipSuccess && msplit) {
+            // the previous frame's surface records, once its PT_1 is done and the motion combine
+            // before (which reads d_psurf) has finished
+            if (h->motion_wait) e = hipStreamWaitEvent(h->stream, h->ev_motion, 0);
+            if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_surf, 0);
+            if (e == hipSuccess && alloc_buf(h, h->d_psurf, prev_surf.bytes) != PTX_OK) e = hipErrorOutOfMemory;
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(h->d_psurf.p, prev_surf.p, prev_surf.bytes, hipMemcpyDeviceToDevice, h->stream);
+            if (e == hipSuccess) e = hipEventRecord(h->ev_psurf, h->stream);
+            h->psurf_wait = true;
+        }
+        // this frame's surface records are complete here (a moved next frame copies them)
+        if (e == hipSuccess) e = hipEventRecord(h->ev_surf, h->stream);
+        h->ev_surf_ok = e == hipSuccess;
+        if (e == hipSuccess && (msplit || (split && !moved)))
+            e = launch_wave_parts(h, sc, w, msplit ? jobs_m : jobs, 1);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
-        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, moved ? temporal_m : split ? temporal_b : temporal, 1);
+        if (e == hipSuccess)
+            e = launch_wave_parts(h, sc, w, msplit ? temporal_mb : moved ? temporal_m : split ? temporal_b : temporal, 1);
+        if (e == hipSuccess && msplit) e = hipEventRecord(h->ev_motion, h->stream);
+        h->motion_wait = msplit;
         if (e == hipSuccess) e = launch_wave_parts(h, sc, w, back, 2);
         if (e == hipSuccess) mark_history(h);
     } else if (has_reuse(h)) {
@@ -1662,6 +1711,8 @@ int ptx_destroy(ptx_handle *h) {
     if (h->alt_stream) (void)hipStreamDestroy(h->alt_stream);
     if (h->alt2_stream) (void)hipStreamDestroy(h->alt2_stream);
     if (h->ev_prev) (void)hipEventDestroy(h->ev_prev);
+    for (hipEvent_t ev : {h->ev_surf, h->ev_psurf, h->ev_motion})
+        if (ev) (void)hipEventDestroy(ev);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {
         if (h->ev_join[q]) (void)hipEventDestroy(h->ev_join[q]);

@@ -155,6 +155,11 @@ struct ReuseArgs {
     const uint4 *psurf;
     int32_t prev_row_lo, prev_row_hi;
     unsigned long long *clip;  // nullptr: not counted
+    // the start kernel's job slots (bit k: slot k) and, for the part that runs before the
+    // previous frame's spatial output is complete, the reprojection test without the history's
+    // confidence (motion_geom: slot 2 is created wherever the geometry passes; the combine uses
+    // its result only where that confidence is nonzero)
+    uint32_t motion_slots, motion_geom;
 };
 // the motion temporal pass's jobs per pixel: the canonical sample at home, the reprojected
 // history sample here, the canonical sample in the previous frame's domain

@@ -486,6 +486,10 @@ __device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseAr
     const f3 x0p = x0_prev(A, sc, m.px, m.py);
     const float dp = length(pp - x0p), dc = length(P - x0p);
     if (!(fabsf(dp - dc) <= 0.05f * dc)) return m;
+    if (A.motion_geom) {  // (the history itself is not complete yet: geometry only)
+        m.ok = true;
+        return m;
+    }
     m.C = min(A.hist[8 * (ptrdiff_t)m.pp + 7].y, A.cap);
     m.ok = m.C != 0u;
     return m;
@@ -512,7 +516,7 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
         const uint32_t cC = valid ? rv[7].y : 0u, clen = valid ? rv[5].w : 0u;
         const bool canon = valid && cC != 0u && clen >= 2u;
         // slot 0: the canonical sample at home (PT_1's state when it still describes it)
-        {
+        if (A.motion_slots & 1u) {
             const uint32_t jid = job_id(A, pix, 0u);
             Job s;
             bool act = canon && job_begin(sc, A, s, x, y, (int32_t)pix, (int32_t)pix);
@@ -520,9 +524,10 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
             const bool live = job_emit(sc, g, A, act, s, jid, act ? rv[0].x : 0u);
             job_finish(g, JL, A, live, s, jid);
         }
-        const MotionHist mh = valid ? motion_hist(sc, A, X1, true) : MotionHist{false, 0, 0u, 0u, 0u};
+        const bool count = (A.motion_slots & 2u) != 0u;  // (once per pixel: with slot 1)
+        const MotionHist mh = valid ? motion_hist(sc, A, X1, count) : MotionHist{false, 0, 0u, 0u, 0u};
         // slot 1: the history sample at p' in this pixel's domain
-        {
+        if (A.motion_slots & 2u) {
             const uint32_t jid = job_id(A, pix, 1u);
             Job s;
             bool act = false;
@@ -541,7 +546,7 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
         }
         // slot 2: the canonical sample in the previous frame's domain at p' (used only when the
         // canonical evaluation is valid; created whenever it may be)
-        {
+        if (A.motion_slots & 4u) {
             const uint32_t jid = job_id(A, pix, 2u);
             Job s;
             bool act = false;
