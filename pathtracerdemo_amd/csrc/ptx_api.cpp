@@ -1058,8 +1058,11 @@ static int timed_wave_frame(ptx_handle *h) {
     // frame's stream once that frame's PT_1 is done (ev_surf) and its slot-0 / slot-2 jobs run
     // before the wait for the previous frame; otherwise they are copied first on the previous
     // frame's stream (the current one here) and the whole pass runs after the wait.
-    // PTX_AB=MOTION_SPLIT=0: the latter always.
-    static const bool msplit_on = ab_knob("MOTION_SPLIT", 1) != 0;
+    // Measured (moving-camera bench, same box, 2 reps): split 313.2 / 312.2 Msamples/s, whole
+    // 315.5 / 314.8 -- the early jobs compete with the previous frame's spatial pass instead of
+    // shortening the chain; so PTX_AB=MOTION_SPLIT=1 (A/B) selects the split, the default runs
+    // the whole pass after the wait.
+    static const bool msplit_on = ab_knob("MOTION_SPLIT", 0) != 0;
     bool moved = h->hist_valid && h->hist_moved && has_reuse(h) && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
     const bool msplit = moved && pipe && msplit_on && pipe_depth() == 2 && h->ev_surf_ok && h->d_surf.p;
     const DevBuf prev_surf = h->d_surf;  // (the previous frame's context, before the swap)
