@@ -586,7 +586,11 @@ static ReuseArgs motion_args(ptx_handle *h, int pass) {
     A.motion_geom = pass == kPassTemporalMotionJobs ? 1u : 0u;
     A.hist_valid = h->hist_valid ? 1u : 0u;
     A.use_init = h->init_state_valid ? 1u : 0u;
-    A.fold_last = 0u;
+    // light segments finished by the combine, as in the still passes -- in the part that ends
+    // with the combine (the split's early jobs finish in their steps: the later part's trace
+    // rounds reuse the result buffers).  PTX_AB=MOTION_FOLD=0 / FOLD_LAST_STEP=0: off.
+    static const bool fold_on = ab_knob("FOLD_LAST_STEP", 1) != 0 && ab_knob("MOTION_FOLD", 1) != 0;
+    A.fold_last = fold_on && pass != kPassTemporalMotionJobs ? 1u : 0u;
     A.motion = 1u;
     std::memcpy(A.vpinv_prev, h->hist_camera, sizeof A.vpinv_prev);  // (words 4..19 of that frame)
     mat4_inverse(A.vpinv_prev, A.vp_prev);

@@ -584,7 +584,7 @@ __global__ __launch_bounds__(WB) void wtmotion_combine(Scene sc, WaveBufs w, Reu
         uint4 *rv = A.cur + 8u * (size_t)pix;
         uint32_t seed = reuse_seed(sc, x, y, SALT_TEMPORAL);
         const uint4 r5 = rv[5], r7 = rv[7];
-        const float4 er = (r7.y != 0u && r5.w >= 2u) ? A.jres[job_id(A, pix, 0u)] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float4 er = (r7.y != 0u && r5.w >= 2u) ? job_at(A, w, pix, 0u) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float ecp = er.w > 0.0f ? luminance(mk(er.x, er.y, er.z)) : 0.0f, ecq = er.w;
         const bool canon_ok = ecq > 0.0f && ecp > 0.0f;
         const float cc = 1.0f, pc = ecp, qc = ecq, Wc = asf(r7.x);
@@ -601,7 +601,7 @@ __global__ __launch_bounds__(WB) void wtmotion_combine(Scene sc, WaveBufs w, Reu
             hlen = h5.w;
             const float ph = asf(h6.x), qh = asf(h6.y), Wh = asf(h7.x);
             if (h5.w >= 2u && ph > 0.0f) {
-                const float4 Fr = A.jres[job_id(A, pix, 1u)];
+                const float4 Fr = job_at(A, w, pix, 1u);
                 if (Fr.w > 0.0f) {
                     const float Fp = luminance(mk(Fr.x, Fr.y, Fr.z)), Fq = Fr.w;
                     const float J = qh / Fq;
@@ -618,7 +618,7 @@ __global__ __launch_bounds__(WB) void wtmotion_combine(Scene sc, WaveBufs w, Reu
         // backward: the canonical sample's weight from its shift into the previous domain
         float Q = 1.0f;
         if (canon_ok && Cp != 0u) {
-            const float4 B = A.jres[job_id(A, pix, 2u)];
+            const float4 B = job_at(A, w, pix, 2u);
             if (B.w > 0.0f) {
                 const float pbc = luminance(mk(B.x, B.y, B.z)) * qc / B.w;
                 const float den = cc * pc + cp * pbc;
