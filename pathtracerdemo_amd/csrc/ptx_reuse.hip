@@ -495,7 +495,10 @@ __device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseAr
     return m;
 }
 
-__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(2, 8)))
+#ifndef MOTION_START_WAVES
+#define MOTION_START_WAVES 3
+#endif
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(MOTION_START_WAVES, 8)))
 void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
     PTX_WAVE_TIMER(sc, KID_TEMP_START | (w.seg_base ? 0x80u : 0u));
     __shared__ uint32_t lds[3];
@@ -515,43 +518,32 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
         const uint4 *rv = A.cur + 8u * (size_t)pix;
         const uint32_t cC = valid ? rv[7].y : 0u, clen = valid ? rv[5].w : 0u;
         const bool canon = valid && cC != 0u && clen >= 2u;
-        // slot 0: the canonical sample at home (PT_1's state when it still describes it)
-        if (A.motion_slots & 1u) {
-            const uint32_t jid = job_id(A, pix, 0u);
-            Job s;
-            bool act = canon && job_begin(sc, A, s, x, y, (int32_t)pix, (int32_t)pix);
-            if (act && A.use_init) act = temporal_from_init(sc, w, A, s, pix, jid);
-            const bool live = job_emit(sc, g, A, act, s, jid, act ? rv[0].x : 0u);
-            job_finish(g, JL, A, live, s, jid);
-        }
         const bool count = (A.motion_slots & 2u) != 0u;  // (once per pixel: with slot 1)
         const MotionHist mh = valid ? motion_hist(sc, A, X1, count) : MotionHist{false, 0, 0u, 0u, 0u};
-        // slot 1: the history sample at p' in this pixel's domain
-        if (A.motion_slots & 2u) {
-            const uint32_t jid = job_id(A, pix, 1u);
+        // the pixel's jobs through ONE job_emit site (three inlined copies needed 256 VGPRs)
+#pragma unroll 1
+        for (uint32_t slot = 0; slot < kMotionJobs; ++slot) {  // (uniform)
+            if (!(A.motion_slots & (1u << slot))) continue;
+            const uint32_t jid = job_id(A, pix, slot);
             Job s;
             bool act = false;
             uint32_t s0 = 0u;
-            if (mh.ok) {
-                const uint4 *hv = A.hist + 8 * (ptrdiff_t)mh.pp;
-                const uint4 h0 = hv[0], h5 = hv[5], h6 = hv[6];
-                act = h5.w >= 2u && asf(h6.x) > 0.0f;
-                if (act) {
-                    job_init(s, x0_of(sc, x, y), X1, mref, kHistRef + mh.pp, h5.w, h0.y, (int32_t)pix);
-                    s0 = h0.x;
+            if (slot == 0u) {  // the canonical sample at home (PT_1's state when it still describes it)
+                act = canon && job_begin(sc, A, s, x, y, (int32_t)pix, (int32_t)pix);
+                if (act && A.use_init) act = temporal_from_init(sc, w, A, s, pix, jid);
+                if (act) s0 = rv[0].x;
+            } else if (slot == 1u) {  // the history sample at p' in this pixel's domain
+                if (mh.ok) {
+                    const uint4 *hv = A.hist + 8 * (ptrdiff_t)mh.pp;
+                    const uint4 h0 = hv[0], h5 = hv[5], h6 = hv[6];
+                    act = h5.w >= 2u && asf(h6.x) > 0.0f;
+                    if (act) {
+                        job_init(s, x0_of(sc, x, y), X1, mref, kHistRef + mh.pp, h5.w, h0.y, (int32_t)pix);
+                        s0 = h0.x;
+                    }
                 }
-            }
-            const bool live = job_emit(sc, g, A, act, s, jid, s0);
-            job_finish(g, JL, A, live, s, jid);
-        }
-        // slot 2: the canonical sample in the previous frame's domain at p' (used only when the
-        // canonical evaluation is valid; created whenever it may be)
-        if (A.motion_slots & 4u) {
-            const uint32_t jid = job_id(A, pix, 2u);
-            Job s;
-            bool act = false;
-            uint32_t s0 = 0u;
-            if (mh.ok && canon) {
+            } else if (mh.ok && canon) {  // the canonical sample in the previous frame's domain at p'
+                // (used only when the canonical evaluation is valid; created whenever it may be)
                 Surface Xp;
                 uint32_t pref;
                 act = surf_load(sc, A.psurf, mh.pp, Xp, pref);
