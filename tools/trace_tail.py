@@ -100,6 +100,7 @@ def main():
         frames.append(launches(buf[:n].copy()))
     r.close()
     summary = []
+    nbhd = {}
     print(f"{a.pipeline} {a.scene} {a.width}x{a.height}: {len(frames[0])} trace launches per frame")
     print("launch  span_us  drain_us  tail_us  tail%  waves  mean_res  plateau  batches  b_p50  b_p99  b_max"
           "  sched_meas  lpt_true  lpt_prev  corr_prev")
@@ -128,6 +129,14 @@ def main():
                 key = pd[bi] if len(pd) > bi.max() else np.zeros_like(bd)
                 lpt_prev = list_schedule(bd[np.argsort(-key, kind="stable")], plateau)
                 corr = float(np.corrcoef(key, bd)[0, 1]) if len(bd) > 2 else None
+                # the previous frame's durations around the same batch index (neighbouring tiles):
+                # max over a +-W window -- a per-region cost a scheduler could know
+                for W in (4, 16, 64):
+                    if len(pd):
+                        pm = np.maximum.reduce([np.roll(np.pad(pd, W), -s)[W:W + len(pd)] for s in range(-W, W + 1)])
+                        nk = pm[np.minimum(bi, len(pm) - 1)]
+                        row_nb = list_schedule(bd[np.argsort(-nk, kind="stable")], plateau)
+                        nbhd[W] = nbhd.get(W, []) + [(meas, row_nb, lpt_true)]
             row = {"frame": fi, "launch": li, "span_us": span, "drain_us": drain, "tail_us": tail,
                    "waves": int(len(w)), "mean_resident": mean_res, "plateau": plateau, "batches": int(len(b)),
                    "batch_p50": float(np.percentile(bd, 50)) if len(bd) else 0.0,
@@ -139,6 +148,10 @@ def main():
             print(f"{fi}.{li:<4d} {span:8.1f} {drain:9.1f} {tail:8.1f} {100*tail/span:5.1f} {len(w):6d} {mean_res:9.0f}"
                   f" {plateau:8d} {len(b):8d} {row['batch_p50']:6.1f} {row['batch_p99']:6.1f} {row['batch_max']:6.1f}"
                   f" {meas:11.1f} {lpt_true:9.1f} " + (f"{lpt_prev:9.1f} {corr:10.3f}" if lpt_prev is not None else ""))
+    for W, v in sorted(nbhd.items()):
+        m, nb, lt = (sum(x[i] for x in v) for i in range(3))
+        print(f"longest-first by the previous frame's max over batches +-{W}: summed makespan {nb:9.1f} us "
+              f"(measured order {m:9.1f}, true longest-first {lt:9.1f})")
     # what the slow batches do: wave-level iterations per region vs duration (last frame)
     allb = np.concatenate([b for _, b in frames[-1]])
     dur = (allb[:, 1] - allb[:, 0]) / 100.0
