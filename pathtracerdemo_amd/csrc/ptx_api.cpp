@@ -736,8 +736,62 @@ hipError_t spatial_summaries(ptx_handle *h, hipStream_t st) {
 }
 
 static bool whole_band_sequences(const ptx_handle *h);
+// A band's spatial pass + PT_4 with the halo in flight (PTX_FLAG_HALO_OVERLAP): only the start
+// kernel runs per tile set -- the interior rows' shift jobs (their neighbourhood lies inside the
+// band) while the halo is in flight, the edge rows' once it has landed (`halo`) -- and every
+// trace round is ONE launch over both sets' queue slots (the edge set's slots follow the
+// interior's: band_sets), so the overlap costs no extra trace launch tails; steps and combines
+// run per set.  One launch sequence.  The same jobs, rays and results as the whole-band pass.
+static hipError_t spatial_overlap_seq(ptx_handle *h, const Scene &sc, const WaveBufs &interior, const WaveBufs &edge,
+                                      hipEvent_t halo) {
+    hipStream_t st = h->stream;
+    hipError_t e = hipSuccess;
+    WaveBufs wi = interior, we = edge;
+    static const int dyn_env = ab_knob("TRACE_DYN", -1);
+    const bool use_dyn = dyn_env == 1 || (dyn_env != 0 && whole_band_sequences(h));
+    const size_t dyn0 = 2u * kWaveMaxRounds * (size_t)interior.cnt_stride;
+    wi.dyn = use_dyn ? (uint32_t *)h->d_wctr.p + dyn0 : nullptr;
+    we.dyn = use_dyn ? (uint32_t *)h->d_wctr.p + dyn0 + (size_t)ptx_handle::kMaxSplit * kWaveMaxRounds * kDynRoundWords
+                     : nullptr;
+    wi.pool = we.pool = nullptr;
+    if (we.seg_phys != wi.seg_phys + wi.nseg) return hipErrorInvalidValue;  // (band_sets: contiguous slots)
+    WaveBufs wt = wi;  // the trace launches: both sets' slots
+    wt.seg_count = wi.seg_count + we.seg_count;
+    ReuseArgs A = reuse_args(h, PTX_PASS_SPATIAL);
+    if (A.fold_last && wi.res[2]) wi.nres = we.nres = wt.nres = 3;
+    else A.fold_last = 0u;
+    if (wi.surf && !h->surf_valid) {  // (primary-hit surface records older than the G-buffer)
+        if ((e = wave_surface(sc, wi, gbuf_band(h), st)) != hipSuccess) return e;
+        if ((e = wave_surface(sc, we, gbuf_band(h), st)) != hipSuccess) return e;
+        h->surf_valid = true;
+    }
+    const int nr = reuse_rounds(0, A);
+    for (int r = 0; e == hipSuccess && r <= nr + 1; ++r) {
+        if (r > 0 && r <= nr) {
+            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
+            e = wave_trace(sc, wt, r - 1, 1, h->stack_depth, st);
+            event_end(t, st);
+            if (e != hipSuccess) break;
+        }
+        if (r == nr && A.fold_last) continue;  // (the combine finishes these jobs)
+        TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
+        e = wave_reuse_round(sc, wi, 0, r, A, st);
+        if (e == hipSuccess && r == 0 && halo) e = hipStreamWaitEvent(st, halo, 0);
+        if (e == hipSuccess) e = wave_reuse_round(sc, we, 0, r, A, st);
+        event_end(t, st);
+    }
+    for (const WaveBufs *ws : {&wi, &we})
+        if (e == hipSuccess) e = launch_wave_seq(h, sc, *ws, PTX_PASS_FINAL, st);
+    return e;
+}
+
 hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, const int *passes, int npasses,
                              bool summaries, const WaveBufs *then, hipEvent_t then_wait) {
+    // (PTX_AB=OVERLAP_START=0: the overlapped band pass as two whole sequences, one per tile set)
+    static const bool overlap_start = ab_knob("OVERLAP_START", 1) != 0;
+    if (then && overlap_start && npasses == 2 && passes[0] == PTX_PASS_SPATIAL && passes[1] == PTX_PASS_FINAL &&
+        h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !summaries)
+        return spatial_overlap_seq(h, sc, w, *then, then_wait);
     static const int env_k = ab_knob("WAVE_STREAMS", 0);
     // pipelined frames: each of the two contexts in flight runs its passes as ONE launch
     // sequence (whole-band launches, dynamic trace batches); measured at 1080p C3 reuse: 1
