@@ -744,44 +744,80 @@ static bool whole_band_sequences(const ptx_handle *h);
 // run per set.  One launch sequence.  The same jobs, rays and results as the whole-band pass.
 static hipError_t spatial_overlap_seq(ptx_handle *h, const Scene &sc, const WaveBufs &interior, const WaveBufs &edge,
                                       hipEvent_t halo) {
-    hipStream_t st = h->stream;
     hipError_t e = hipSuccess;
-    WaveBufs wi = interior, we = edge;
+    // launch sequences as the plain pass runs its back half (two when pipelined): sequence q
+    // takes share q of each tile set, and its two shares get ADJACENT physical queue slots --
+    // interior share q at slots [a_q + E_q, b_q + E_q), edge share q right after (E_q = the edge
+    // slots of the sequences before) -- so each sequence's trace rounds are one launch over one
+    // contiguous slot range
+    static const int env_bk = ab_knob("PIPE_BACK_STREAMS", 2);
+    int k = env_bk > 0 && h->alt_stream && pipelined(h) ? env_bk : 1;
+    if (h->cfg.flags & PTX_FLAG_SINGLE_STREAM) k = 1;
+    k = std::max(1, std::min<int>({k, ptx_handle::kMaxSplit, (int)interior.nseg, (int)edge.nseg}));
     static const int dyn_env = ab_knob("TRACE_DYN", -1);
     const bool use_dyn = dyn_env == 1 || (dyn_env != 0 && whole_band_sequences(h));
     const size_t dyn0 = 2u * kWaveMaxRounds * (size_t)interior.cnt_stride;
-    wi.dyn = use_dyn ? (uint32_t *)h->d_wctr.p + dyn0 : nullptr;
-    we.dyn = use_dyn ? (uint32_t *)h->d_wctr.p + dyn0 + (size_t)ptx_handle::kMaxSplit * kWaveMaxRounds * kDynRoundWords
-                     : nullptr;
-    wi.pool = we.pool = nullptr;
-    if (we.seg_phys != wi.seg_phys + wi.nseg) return hipErrorInvalidValue;  // (band_sets: contiguous slots)
-    WaveBufs wt = wi;  // the trace launches: both sets' slots
-    wt.seg_count = wi.seg_count + we.seg_count;
     ReuseArgs A = reuse_args(h, PTX_PASS_SPATIAL);
-    if (A.fold_last && wi.res[2]) wi.nres = we.nres = wt.nres = 3;
-    else A.fold_last = 0u;
-    if (wi.surf && !h->surf_valid) {  // (primary-hit surface records older than the G-buffer)
-        if ((e = wave_surface(sc, wi, gbuf_band(h), st)) != hipSuccess) return e;
-        if ((e = wave_surface(sc, we, gbuf_band(h), st)) != hipSuccess) return e;
-        h->surf_valid = true;
-    }
+    const bool fold = A.fold_last && interior.res[2];
+    if (!fold) A.fold_last = 0u;
     const int nr = reuse_rounds(0, A);
-    for (int r = 0; e == hipSuccess && r <= nr + 1; ++r) {
-        if (r > 0 && r <= nr) {
-            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
-            e = wave_trace(sc, wt, r - 1, 1, h->stack_depth, st);
-            event_end(t, st);
-            if (e != hipSuccess) break;
+    if (k > 1) {
+        if (!h->ev_fork && (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return e;
+        for (int q = 1; q < k; ++q) {
+            if (!h->sub[q] && (e = hipStreamCreateWithFlags(&h->sub[q], hipStreamNonBlocking)) != hipSuccess) return e;
+            if (!h->ev_join[q] && (e = hipEventCreateWithFlags(&h->ev_join[q], hipEventDisableTiming)) != hipSuccess)
+                return e;
         }
-        if (r == nr && A.fold_last) continue;  // (the combine finishes these jobs)
-        TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
-        e = wave_reuse_round(sc, wi, 0, r, A, st);
-        if (e == hipSuccess && r == 0 && halo) e = hipStreamWaitEvent(st, halo, 0);
-        if (e == hipSuccess) e = wave_reuse_round(sc, we, 0, r, A, st);
-        event_end(t, st);
+        if ((e = hipEventRecord(h->ev_fork, h->stream)) != hipSuccess) return e;
+        for (int q = 1; q < k; ++q)
+            if ((e = hipStreamWaitEvent(h->sub[q], h->ev_fork, 0)) != hipSuccess) return e;
     }
-    for (const WaveBufs *ws : {&wi, &we})
-        if (e == hipSuccess) e = launch_wave_seq(h, sc, *ws, PTX_PASS_FINAL, st);
+    const bool surf_stale = interior.surf && !h->surf_valid;
+    uint32_t E = 0u;  // edge slots of the sequences before
+    for (int q = 0; q < k && e == hipSuccess; ++q) {
+        hipStream_t st = q ? h->sub[q] : h->stream;
+        WaveBufs wi = interior, we = edge;
+        wi.seg_base = (uint32_t)((uint64_t)interior.nseg * q / k);
+        wi.seg_count = (uint32_t)((uint64_t)interior.nseg * (q + 1) / k) - wi.seg_base;
+        we.seg_base = (uint32_t)((uint64_t)edge.nseg * q / k);
+        we.seg_count = (uint32_t)((uint64_t)edge.nseg * (q + 1) / k) - we.seg_base;
+        wi.seg_phys = interior.seg_phys + E;
+        we.seg_phys = interior.seg_phys + E + wi.seg_base + wi.seg_count - we.seg_base;
+        E += we.seg_count;
+        wi.dyn = use_dyn ? (uint32_t *)h->d_wctr.p + dyn0 + (size_t)q * kWaveMaxRounds * kDynRoundWords : nullptr;
+        we.dyn = use_dyn ? (uint32_t *)h->d_wctr.p + dyn0 +
+                               (size_t)(ptx_handle::kMaxSplit + q) * kWaveMaxRounds * kDynRoundWords
+                         : nullptr;
+        wi.pool = we.pool = nullptr;
+        if (fold) wi.nres = we.nres = 3;
+        WaveBufs wt = wi;  // this sequence's trace launches: both shares' slots
+        wt.seg_count = wi.seg_count + we.seg_count;
+        if (surf_stale) {  // (primary-hit surface records older than the G-buffer)
+            if ((e = wave_surface(sc, wi, gbuf_band(h), st)) != hipSuccess) return e;
+            if ((e = wave_surface(sc, we, gbuf_band(h), st)) != hipSuccess) return e;
+        }
+        for (int r = 0; e == hipSuccess && r <= nr + 1; ++r) {
+            if (r > 0 && r <= nr) {
+                TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
+                e = wave_trace(sc, wt, r - 1, 1, h->stack_depth, st);
+                event_end(t, st);
+                if (e != hipSuccess) break;
+            }
+            if (r == nr && A.fold_last) continue;  // (the combine finishes these jobs)
+            TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
+            e = wave_reuse_round(sc, wi, 0, r, A, st);
+            if (e == hipSuccess && r == 0 && halo) e = hipStreamWaitEvent(st, halo, 0);
+            if (e == hipSuccess) e = wave_reuse_round(sc, we, 0, r, A, st);
+            event_end(t, st);
+        }
+        for (const WaveBufs *ws : {&wi, &we})
+            if (e == hipSuccess) e = launch_wave_seq(h, sc, *ws, PTX_PASS_FINAL, st);
+    }
+    if (surf_stale && e == hipSuccess) h->surf_valid = true;
+    for (int q = 1; q < k && e == hipSuccess; ++q) {
+        if ((e = hipEventRecord(h->ev_join[q], h->sub[q])) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(h->stream, h->ev_join[q], 0)) != hipSuccess) return e;
+    }
     return e;
 }
 
