@@ -28,6 +28,19 @@ def test_library_exports_every_declared_symbol():
     assert lib.ptx_abi_version() == _native.PTX_ABI_VERSION == 4
 
 
+def test_header_constants_match_the_python_binding():
+    """Every PTX_* integer #define of include/ptx.h that the Python binding mirrors has the
+    header's value (buffer ids, pass / stats slots, flags, counter words)."""
+    from pathtracerdemo_amd import _native as N
+    txt = open(os.path.join(ROOT, "include", "ptx.h")).read()
+    defs = {k: int(v, 0) for k, v in re.findall(r"^#define\s+(PTX_\w+)\s+(0x[0-9a-fA-F]+|\d+)u?\b", txt, re.M)}
+    mirrored = [k for k in defs if hasattr(N, k)]
+    assert len(mirrored) >= 15
+    for k in mirrored:
+        assert getattr(N, k) == defs[k], f"{k}: binding {getattr(N, k)} != header {defs[k]}"
+    assert N.PTX_COUNTER_MOTION_CLIP == 6
+
+
 def test_create_rejects_bad_config_without_touching_gpu():
     from pathtracerdemo_amd import _native as N
     lib = N.load()
