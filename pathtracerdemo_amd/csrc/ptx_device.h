@@ -458,6 +458,15 @@ __device__ __forceinline__ bool inst_may_hit(const Inst &I, f3 o, f3 winv, float
 #ifndef PTX_INST_CULL
 #define PTX_INST_CULL 1
 #endif
+#ifndef PTX_EARLY_LEAF_K  // trace_core_flat's early leaf phase (0 = off)
+#define PTX_EARLY_LEAF_K 8
+#endif
+#ifndef PTX_EARLY_LEAF_L
+#define PTX_EARLY_LEAF_L 4
+#endif
+#ifndef PTX_EARLY_REFILL_K  // trace_core_flat's early exit from the refill loop (0 = off; K = 4 / 8 / 16 measured -0.5 to -1 %)
+#define PTX_EARLY_REFILL_K 0
+#endif
 
 // TraceRay (SH/PT_1_InitPass.wgsl:605-715; PT_01:509-621): closest hit over every
 // instance and sub-mesh root, ordered-stack BLAS traversal, ties replace (`if (best < t)
@@ -815,9 +824,18 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
     for (;;) {
         // refill: a lane with no leaf, no stack and no queued root takes its instance's next
         // chunk of 32 roots or its next instance (transform + root pre-filter)
-        for (;;) {
+        for (uint32_t refills = 0u;; ++refills) {
             const bool need = !done && leaf == 0u && sp < 0 && mask == 0u;
-            if (wballot(need) == 0ull) break;
+            const unsigned long long nm = wballot(need);
+            if (nm == 0ull) break;
+            // early exit (PTX_EARLY_REFILL_K > 0): after one refill, when at most K lanes still
+            // look for a root that passes, the lanes that have one walk it now and those K go on
+            // at the next refill.  Per lane nothing moves; only the interleaving across lanes.
+            if constexpr (PTX_EARLY_REFILL_K > 0) {
+                if (refills > 0u && __builtin_popcountll(nm) <= PTX_EARLY_REFILL_K &&
+                    wballot(leaf != 0u || sp >= 0 || mask != 0u) != 0ull)
+                    break;
+            }
 #ifdef PTX_WG_TIMES
             if (dbg) dbg[0]++;
 #endif
@@ -866,7 +884,17 @@ __device__ __forceinline__ Hit trace_core_flat(const Scene &sc, const SubRoot *s
         // node loop: pops and root takes through one LDS read (as trace_core_tab UNI)
         for (;;) {
             const bool want = leaf == 0u && (sp >= 0 || mask != 0u);
-            if (wballot(want) == 0ull) break;
+            const unsigned long long wm = wballot(want);
+            if (wm == 0ull) break;
+            // early leaf phase (PTX_EARLY_LEAF_K > 0): once at most K lanes still descend and
+            // at least L hold a leaf, the holders test their leaves now and the descending lanes
+            // go on after it, joined by the holders' next pops.  Per lane nothing moves (its leaf
+            // is tested before its next pop either way); only the interleaving across lanes.
+            if constexpr (PTX_EARLY_LEAF_K > 0) {
+                if (__builtin_popcountll(wm) <= PTX_EARLY_LEAF_K &&
+                    __builtin_popcountll(wballot(leaf != 0u)) >= PTX_EARLY_LEAF_L)
+                    break;
+            }
 #ifdef PTX_WG_TIMES
             if (dbg) dbg[1]++;
 #endif
