@@ -464,6 +464,9 @@ __device__ __forceinline__ bool inst_may_hit(const Inst &I, f3 o, f3 winv, float
 #ifndef PTX_EARLY_LEAF_L
 #define PTX_EARLY_LEAF_L 4
 #endif
+#ifndef PTX_EARLY_LEAF_TAB  // the same in trace_core_tab (scenes of < 3 instances, G-buffer, PT_4)
+#define PTX_EARLY_LEAF_TAB 1
+#endif
 #ifndef PTX_EARLY_REFILL_K  // trace_core_flat's early exit from the refill loop (0 = off; K = 4 / 8 / 16 measured -0.5 to -1 %)
 #define PTX_EARLY_REFILL_K 0
 #endif
@@ -613,7 +616,14 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                 // lane the root tests, pops, tests and pushes are the reference's sequence.
                 for (;;) {
                     const bool want = leaf == 0u && (sp >= 0 || mask != 0u);
-                    if (wballot(want) == 0ull) break;
+                    const unsigned long long wm = wballot(want);
+                    if (wm == 0ull) break;
+                    // early leaf phase (as trace_core_flat; only where the cooperative phase runs)
+                    if constexpr (PTX_EARLY_LEAF_K > 0 && PTX_EARLY_LEAF_TAB && COOP) {
+                        if (wave_coop && __builtin_popcountll(wm) <= PTX_EARLY_LEAF_K &&
+                            __builtin_popcountll(wballot(leaf != 0u)) >= PTX_EARLY_LEAF_L)
+                            break;
+                    }
                     if (PROF && want) pf.hit(PROF_NODE);
                     uint32_t ref = 0u;
                     bool node = false;
@@ -736,7 +746,10 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                         continue;
                     }
                 }
-                if (leaf == 0u) break;  // roots and stack exhausted
+                if (leaf == 0u) {  // roots and stack exhausted -- or still descending after an
+                    if (sp >= 0 || mask != 0u) continue;  // early leaf phase that saw a NaN t
+                    break;
+                }
                 if (PROF && !wave_coop) pf.hit(PROF_LEAF);
                 const uint32_t first = leaf & LEAF_FIRST_MASK;
                 const uint32_t count = (leaf >> 24) & 0x7Fu;

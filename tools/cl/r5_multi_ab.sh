@@ -1,10 +1,11 @@
 # Same-box A/B of the default build against several variant builds (make -C pathtracerdemo_amd/csrc
 # variant NAME=x ALT_DEFS=...): first the bit-exact GPU parity + reuse tests on every variant, then
-# REPS interleaved headline benches.  usage: VARIANTS="e1 e2" REPS=2 TAG=name bash tools/cl/r5_multi_ab.sh
+# REPS interleaved headline benches (SKIP_TESTS=1: benches only).  usage: VARIANTS="e1 e2" REPS=2 TAG=name bash tools/cl/r5_multi_ab.sh
 set -o pipefail
 P=$PWD/pathtracerdemo_amd
 TAG=${TAG:-mab}
 for v in ${VARIANTS}; do
+  [ -n "${SKIP_TESTS:-}" ] && break
   PTX_LIB_PATH=$P/libptx_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_reuse.py -m gpu -x -q \
       --timeout 240 --timeout-method thread > gpurun_out/${TAG}_tests_$v.log 2>&1 \
     || { echo "tests $v failed"; tail -30 gpurun_out/${TAG}_tests_$v.log; exit 1; }
