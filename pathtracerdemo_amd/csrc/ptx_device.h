@@ -467,6 +467,12 @@ __device__ __forceinline__ bool inst_may_hit(const Inst &I, f3 o, f3 winv, float
 #ifndef PTX_EARLY_LEAF_TAB  // the same in trace_core_tab (scenes of < 3 instances, G-buffer, PT_4)
 #define PTX_EARLY_LEAF_TAB 1
 #endif
+#ifndef PTX_EARLY_LEAF_TAB_K
+#define PTX_EARLY_LEAF_TAB_K PTX_EARLY_LEAF_K
+#endif
+#ifndef PTX_EARLY_LEAF_TAB_L
+#define PTX_EARLY_LEAF_TAB_L PTX_EARLY_LEAF_L
+#endif
 #ifndef PTX_EARLY_REFILL_K  // trace_core_flat's early exit from the refill loop (0 = off; K = 4 / 8 / 16 measured -0.5 to -1 %)
 #define PTX_EARLY_REFILL_K 0
 #endif
@@ -620,8 +626,8 @@ __device__ __forceinline__ Hit trace_core_tab(const Scene &sc, const SubRoot *su
                     if (wm == 0ull) break;
                     // early leaf phase (as trace_core_flat; only where the cooperative phase runs)
                     if constexpr (PTX_EARLY_LEAF_K > 0 && PTX_EARLY_LEAF_TAB && COOP) {
-                        if (wave_coop && __builtin_popcountll(wm) <= PTX_EARLY_LEAF_K &&
-                            __builtin_popcountll(wballot(leaf != 0u)) >= PTX_EARLY_LEAF_L)
+                        if (wave_coop && __builtin_popcountll(wm) <= PTX_EARLY_LEAF_TAB_K &&
+                            __builtin_popcountll(wballot(leaf != 0u)) >= PTX_EARLY_LEAF_TAB_L)
                             break;
                     }
                     if (PROF && want) pf.hit(PROF_NODE);
