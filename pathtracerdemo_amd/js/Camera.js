@@ -29,6 +29,15 @@ class Camera {
     return mat4.invert(mat4.multiply(T, R));
   }
 
+  GetForwardVector() {                                               // Camera.ts:66-73
+    const q = quat.fromEuler(this.Pitch, this.Yaw, this.Roll, 'yxz');
+    return vec3.normalize(vec3.transformQuat(vec3.fromValues(0, 0, -1), q));
+  }
+
+  GetRightVector() {                                                 // Camera.ts:75-81
+    return vec3.cross(this.GetForwardVector(), vec3.fromValues(0, 1, 0));
+  }
+
   GetLocation() { return this.Location; }
   SetPitch(deg) { this.Pitch = Math.min(Math.PI, Math.max(-Math.PI, (deg * Math.PI) / 180.0)); }
   SetYaw(deg) { this.Yaw = ((deg * Math.PI) / 180.0) % (2 * Math.PI); }

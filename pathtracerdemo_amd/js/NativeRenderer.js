@@ -55,48 +55,99 @@ function buildUniform(width, height, camera, frameCount, world) {
   return u32;
 }
 
+function isCanvas(x) {
+  return !!x && typeof x === 'object' && typeof x.width === 'number' && typeof x.height === 'number';
+}
+
 class NativeRenderer {
   /**
-   * @param {number} width  image width (Canvas.width in the reference)
-   * @param {number} height image height
+   * Three call forms:
+   *   new NativeRenderer(adapter, device, canvas, [options])  -- Renderer_TEST's own
+   *     (Renderer_TEST.ts:83-88, WebGPUEngine.ts:83); adapter / device are not used;
+   *   new NativeRenderer(canvas, [options]);
+   *   new NativeRenderer(width, height, [options]).
+   * `canvas` is anything with numeric width / height (an HTMLCanvasElement, an OffscreenCanvas,
+   * a plain object): like Renderer_TEST, Initialize() reads its size each time it is called, so
+   * WebGPUEngine.resize (set canvas.width / height, then Initialize(world), WebGPUEngine.ts:132-142)
+   * recreates the handle at the new size.
    * @param {object} [options] {pipeline: 'restir'|'mcpt'|'reuse'|'gi', device, rowBegin, rowEnd, flags,
    *   reuseRadius, reuseNeighbors, temporalCap}
    */
-  constructor(width, height, options = {}) {
-    this.Width = width;
-    this.Height = height;
+  constructor(a, b, c, d) {
+    let options;
+    if (typeof a === 'number') {
+      this.Canvas = null;
+      this.Width = a;
+      this.Height = b;
+      options = c || {};
+    } else if (isCanvas(a)) {
+      this.Canvas = a;
+      options = b || {};
+    } else if (isCanvas(c)) {
+      this.Canvas = c;
+      options = d || {};
+    } else {
+      throw new TypeError('NativeRenderer: expected (width, height), (canvas) or (adapter, device, canvas)');
+    }
+    if (this.Canvas) {
+      this.Width = this.Canvas.width;
+      this.Height = this.Canvas.height;
+    }
+    this.Options = options;
     this.Pipeline = options.pipeline || 'restir';
     if (!(this.Pipeline in PIPELINE)) throw new Error(`unknown pipeline ${this.Pipeline}`);
-    this.RowBegin = options.rowBegin || 0;
-    this.RowEnd = options.rowEnd || height;
-    this.Handle = addon.create({
-      width, height, rowBegin: this.RowBegin, rowEnd: this.RowEnd,
-      device: options.device === undefined ? -1 : options.device,
-      pipeline: PIPELINE[this.Pipeline], flags: options.flags || 0,
-      reuseRadius: options.reuseRadius || 0, reuseNeighbors: options.reuseNeighbors || 0,
-      temporalCap: options.temporalCap || 0,
-    });
+    this.Handle = null;
+    this.createHandle();
     this.World = null;
     this.Camera = null;
     this.FrameCount = 0;
     this.Uniform = null;
   }
 
+  /** A handle for this.Width x this.Height (rows rowBegin..rowEnd of it). */
+  createHandle() {
+    const o = this.Options;
+    this.RowBegin = o.rowBegin || 0;
+    this.RowEnd = o.rowEnd || this.Height;
+    this.Handle = addon.create({
+      width: this.Width, height: this.Height, rowBegin: this.RowBegin, rowEnd: this.RowEnd,
+      device: o.device === undefined ? -1 : o.device,
+      pipeline: PIPELINE[this.Pipeline], flags: o.flags || 0,
+      reuseRadius: o.reuseRadius || 0, reuseNeighbors: o.reuseNeighbors || 0,
+      temporalCap: o.temporalCap || 0,
+    });
+  }
+
   GetCamera() { return this.Camera; }
 
   ResetFrameCount() { this.FrameCount = 0; }
 
-  /** Renderer_TEST.Initialize (:141-163): camera at (0,0,6), yaw/pitch 0, upload the world. */
+  /**
+   * Renderer_TEST.Initialize (:141-163): the canvas's current size (a changed size recreates the
+   * handle, as DestroyGPUResources + CreateGPUResources do), a new camera at (0,0,6) with
+   * yaw / pitch 0, FrameCount 0, the world uploaded.
+   */
   async Initialize(world) {
-    this.Camera = new Camera(this.Width, this.Height);
-    this.Camera.SetLocationFromXYZ(0, 0, 6);
-    this.Camera.SetYaw(0);
-    this.Camera.SetPitch(0);
     // a reference World is serialized here (SerializeWorldData); a serialized one is taken as is
     if (world && world.InstancesPool instanceof Map) world = SerializeWorldData(world);
     if (!world || !(world.scene instanceof Uint32Array) || !Array.isArray(world.offsets) || world.offsets.length !== 7) {
       throw new TypeError('Initialize: expected a World or a serialized world {scene, geometry, accel, offsets[7]}');
     }
+    if (this.Canvas && (this.Canvas.width !== this.Width || this.Canvas.height !== this.Height)) {
+      if (this.Options.rowBegin || this.Options.rowEnd) {
+        throw new Error('Initialize: a row-band renderer cannot follow a canvas resize');
+      }
+      if (!(this.Canvas.width > 0 && this.Canvas.height > 0)) throw new RangeError('Initialize: empty canvas');
+      if (this.Handle) addon.destroy(this.Handle);
+      this.Handle = null;
+      this.Width = this.Canvas.width;
+      this.Height = this.Canvas.height;
+      this.createHandle();
+    }
+    this.Camera = new Camera(this.Width, this.Height);
+    this.Camera.SetLocationFromXYZ(0, 0, 6);
+    this.Camera.SetYaw(0);
+    this.Camera.SetPitch(0);
     this.World = world;
     this.ResetFrameCount();
     addon.uploadScene(this.Handle, world.scene, world.geometry, world.accel);

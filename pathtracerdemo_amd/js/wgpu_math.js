@@ -130,9 +130,28 @@ const vec3 = {
   len(v) {
     return Math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
   },
+  length(v) {
+    return Math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  },
   normalize(v) {
     const l = Math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
     return l > 0.00001 ? out([v[0] / l, v[1] / l, v[2] / l]) : out([0, 0, 0]);
+  },
+  // a + b * scale, into dst when given (InputController.ts:92-110 accumulates in place)
+  addScaled(a, b, scale, dst) {
+    const r = [a[0] + b[0] * scale, a[1] + b[1] * scale, a[2] + b[2] * scale];
+    if (!dst) return out(r);
+    dst[0] = r[0]; dst[1] = r[1]; dst[2] = r[2];
+    return dst;
+  },
+  // v rotated by the unit quaternion q: v + 2w (q.xyz x v) + 2 q.xyz x (q.xyz x v)  (Camera.ts:71)
+  transformQuat(v, q) {
+    const qx = q[0], qy = q[1], qz = q[2], w2 = q[3] * 2;
+    const x = v[0], y = v[1], z = v[2];
+    const uvX = qy * z - qz * y, uvY = qz * x - qx * z, uvZ = qx * y - qy * x;
+    return out([x + uvX * w2 + (qy * uvZ - qz * uvY) * 2,
+      y + uvY * w2 + (qz * uvX - qx * uvZ) * 2,
+      z + uvZ * w2 + (qx * uvY - qy * uvX) * 2]);
   },
 };
 

@@ -36,6 +36,32 @@ class Camera:
     def set_pitch(self, deg):
         self.pitch = min(math.pi, max(-math.pi, deg * math.pi / 180.0))
 
+    # Camera.ts:116-130 (degrees in, radians stored; JS % is fmod)
+    def add_pitch(self, deg):
+        self.pitch = min(math.pi / 2, max(-math.pi / 2, self.pitch + deg * math.pi / 180.0))
+
+    def add_yaw(self, deg):
+        self.yaw = math.fmod(self.yaw + deg * math.pi / 180.0, 2 * math.pi)
+
+    # Camera.ts:139-146: the Float32Array location, component by component
+    def add_location_offset(self, o):
+        o = np.asarray(o, dtype=np.float32)
+        for i in range(3):
+            self.location[i] = np.float32(float(self.location[i]) + float(o[i]))
+
+    # Camera.ts:157-163
+    def set_aspect_ratio(self, width, height):
+        self.aspect = width / height
+        self.projection = wm.mat4_perspective(self.fov, self.aspect, self.near, self.far)
+
+    # Camera.ts:66-81
+    def forward_vector(self) -> np.ndarray:
+        q = wm.quat_from_euler(self.pitch, self.yaw, self.roll, "yxz")
+        return wm.vec3_normalize(wm.vec3_transform_quat(np.array([0, 0, -1], np.float32), q))
+
+    def right_vector(self) -> np.ndarray:
+        return wm.vec3_cross(self.forward_vector(), np.array([0, 1, 0], np.float32))
+
     def view_matrix(self) -> np.ndarray:
         t = wm.mat4_translation(self.location)
         r = wm.mat4_from_quat(wm.quat_from_euler(self.pitch, self.yaw, self.roll, "yxz"))

@@ -150,3 +150,21 @@ def vec3_cross(a, b) -> np.ndarray:
 def vec3_len(v) -> float:
     v = np.asarray(v, dtype=np.float32).astype(np.float64)
     return math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+
+
+def vec3_add_scaled(a, b, scale: float) -> np.ndarray:
+    """wgpu-matrix vec3.addScaled: a + b * scale (InputController.ts:92-110)."""
+    a = np.asarray(a, dtype=np.float32).astype(np.float64)
+    b = np.asarray(b, dtype=np.float32).astype(np.float64)
+    return _out([a[0] + b[0] * scale, a[1] + b[1] * scale, a[2] + b[2] * scale])
+
+
+def vec3_transform_quat(v, q) -> np.ndarray:
+    """wgpu-matrix vec3.transformQuat: v + 2w (q.xyz x v) + 2 q.xyz x (q.xyz x v) (Camera.ts:71)."""
+    x, y, z = (float(c) for c in np.asarray(v, dtype=np.float32))
+    qx, qy, qz, qw = (float(c) for c in np.asarray(q, dtype=np.float32))
+    w2 = qw * 2
+    ux, uy, uz = qy * z - qz * y, qz * x - qx * z, qx * y - qy * x
+    return _out([x + ux * w2 + (qy * uz - qz * uy) * 2,
+                 y + uy * w2 + (qz * ux - qx * uz) * 2,
+                 z + uz * w2 + (qx * uy - qy * ux) * 2])
