@@ -1192,7 +1192,9 @@ static void temporal_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t *cur,
  *  - VP' = the f32 rounding of the double-precision inverse of the previous VP^-1
  *    (pto_mat4_inverse: cofactors along the first column, one fixed operation order);
  *  - p' = floor(((VP' (P, 1)).xy / w + 1) * 0.5 * (W, H)), P = the current primary hit;
- *    none when w <= 0 or p' is outside the image (a disocclusion past the border);
+ *    none when w <= 0 or p' is outside the image (a disocclusion past the border), and none
+ *    when p' lies more than `radius` rows from the pixel (motion_rows): a row band's motion
+ *    halo holds exactly those rows, so any split of the frame gives the same history;
  *  - the history is used iff x1' exists, n(x1') . n(x1) >= 0.9 and the depths along the
  *    previous view agree within 5 %: | |x1' - x0'| - |P - x0'| | <= 0.05 |P - x0'| (geometry
  *    only: the confidence never depends on a sample);
@@ -1242,6 +1244,10 @@ static int reproject(const float *vp, v3 P, uint32_t W, uint32_t H, uint32_t *px
     *py = (uint32_t)fy;
     return 1;
 }
+/* p' row within `radius` rows of the pixel's row y (the build's motion rule above) */
+static inline int motion_rows(uint32_t py, uint32_t y, uint32_t radius) {
+    return (py > y ? py - y : y - py) <= radius;
+}
 /* the disocclusion test of the history at p' (x1' = Sp with camera point x0p) for the
  * current primary hit P with normal Nc */
 static int motion_valid(const surface *Sp, v3 x0p, v3 P, v3 Nc) {
@@ -1266,7 +1272,7 @@ static void temporal_motion_pixel(const ctx *c, const ctx *cprev, const float *v
     const uint32_t *h = NULL;
     if (prm->hist_valid) {
         const surface S1 = get_surface(c, x1);
-        if (reproject(vp_prev, S1.pos, W, H, &px, &py)) {
+        if (reproject(vp_prev, S1.pos, W, H, &px, &py) && motion_rows(py, y, prm->radius)) {
             x1p = decode_compact(gbuffer_prev + 4u * (py * W + px));
             if (x1p.valid) {
                 const surface Sp = get_surface(c, x1p);

@@ -18,7 +18,9 @@
 //
 // RCCL is loaded with dlopen at ptx_comm_init: in a process that already holds one (torch's
 // bundled librccl.so.1) the loader hands back that copy, and libptx.so stays loadable where
-// no RCCL is installed.
+// no RCCL is installed.  PTX_RCCL_LIB names another library with the same entry points (the
+// tests' in-process loopback communicator, tests/loopback/, runs several band handles of one
+// GPU through this exact code).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -50,6 +52,7 @@ struct Rccl {
     // optional (non-blocking communicator init with a deadline; absent -> blocking init)
     ncclResult_t (*init_rank_config)(ncclComm_t *, int, ncclUniqueId, int, ncclConfig_t *) = nullptr;
     ncclResult_t (*abort)(ncclComm_t) = nullptr;
+    ncclResult_t (*finalize)(ncclComm_t) = nullptr;
     bool ok = false;
     std::string why;
 };
@@ -58,11 +61,18 @@ const Rccl &rccl() {
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
-        void *lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        const char *path = std::getenv("PTX_RCCL_LIB");
+        void *lib = nullptr;
+        if (path && *path) {
+            lib = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+        } else {
+            path = "librccl.so.1";
+            lib = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
+            if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        }
         if (!lib) {
             const char *e = dlerror();
-            r.why = std::string("dlopen librccl.so.1: ") + (e ? e : "not found");
+            r.why = std::string("dlopen ") + path + ": " + (e ? e : "not found");
             return;
         }
         bool all = true;
@@ -86,6 +96,7 @@ const Rccl &rccl() {
         r.ok = all;
         r.init_rank_config = reinterpret_cast<decltype(r.init_rank_config)>(dlsym(lib, "ncclCommInitRankConfig"));
         r.abort = reinterpret_cast<decltype(r.abort)>(dlsym(lib, "ncclCommAbort"));
+        r.finalize = reinterpret_cast<decltype(r.finalize)>(dlsym(lib, "ncclCommFinalize"));
     });
     return r;
 }
@@ -93,8 +104,10 @@ const Rccl &rccl() {
 #define NCCL_CHECK(h, expr)                                                                                  \
     do {                                                                                                     \
         ncclResult_t r_ = (expr);                                                                            \
-        if (r_ != ncclSuccess)                                                                               \
+        if (r_ != ncclSuccess) {                                                                             \
+            (h)->comm_broken = (h)->comm != nullptr;                                                         \
             return fail((h), PTX_E_HIP, "%s: %s (%s:%d)", #expr, rccl().error_string(r_), __FILE__, __LINE__); \
+        }                                                                                                    \
     } while (0)
 
 // Non-blocking communicators (ptx_comm_init): the init and every group end return at once and
@@ -121,6 +134,7 @@ ncclResult_t comm_wait(ncclComm_t c, int seconds) {
 int group_end_wait(ptx_handle *h) {
     ncclResult_t r = rccl().group_end();
     if (r == ncclInProgress) r = comm_wait((ncclComm_t)h->comm, comm_timeout_s());
+    if (r != ncclSuccess) h->comm_broken = true;
     if (r == ncclInProgress)
         return fail(h, PTX_E_HIP, "RCCL group (rank %d of %d) not enqueued within %d s", h->rank, h->world,
                     comm_timeout_s());
@@ -206,6 +220,16 @@ BandSets band_sets(const ptx_handle *h, const WaveBufs &w) {
 // neighbours' rows of its spatial output arrive as the motion halo before the temporal pass.
 // ev_prev marks everything enqueued before this frame on the previous frame's stream (pipelined
 // or not: a neighbour's motion-halo copy waits for it).
+//
+// Whether the motion halo is exchanged (`xchg`, motion_exchange) is decided from state every rank
+// shares -- the frames rendered and the uniform sequence -- never from this rank's history state:
+// a rank that dropped its history (a reset, a scene upload) still sends and receives its rows and
+// renders the frame without history (`moved` false), so no rank waits on a send its neighbour
+// never posts.
+bool motion_exchange(const ptx_handle *h) {
+    return h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && h->band_frames > 0 &&
+           std::memcmp(h->band_camera, h->uniform + 4, sizeof h->band_camera) != 0;
+}
 int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w, bool &pipe, bool &moved) {
     if (!has_reuse(h)) return fail(h, PTX_E_INVALID, "band frames need the reuse or GI pipeline");
     if (h->cfg.flags & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK))
@@ -215,7 +239,7 @@ int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w, bool &pipe, bool &moved)
         if (int rc = build_layout(h)) return rc;
     sc = make_scene(h);
     if (!tables_fit_lds(sc)) return fail(h, PTX_E_SCENE, "band frames need the LDS root / instance tables");
-    moved = h->hist_valid && h->hist_moved && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
+    moved = motion_exchange(h) && h->hist_valid && h->hist_moved;
     if (moved) {
         if (int rc = motion_prepare(h, h->stream)) return rc;
         moved = h->hist_moved;
@@ -346,6 +370,8 @@ int band_back(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *fr
     }
     if (e != hipSuccess) return fail(h, PTX_E_HIP, "band spatial / final passes: %s", hipGetErrorString(e));
     mark_history(h);
+    std::memcpy(h->band_camera, h->uniform + 4, sizeof h->band_camera);
+    h->band_frames++;
     HIP_CHECK(h, hipEventRecord(frame_t->stop, h->stream));
     frame_t->pass = PTX_STAT_FRAME;
     frame_t->pending = true;
@@ -359,9 +385,11 @@ int band_back(ptx_handle *h, const Scene &sc, const WaveBufs &w, TimedLaunch *fr
 int comm_health(ptx_handle *h) {
     ncclResult_t st = ncclSuccess;
     NCCL_CHECK(h, rccl().async_error((ncclComm_t)h->comm, &st));
-    if (st != ncclSuccess && st != ncclInProgress)
+    if (st != ncclSuccess && st != ncclInProgress) {
+        h->comm_broken = true;
         return fail(h, PTX_E_HIP, "RCCL communicator (rank %d of %d) reports: %s", h->rank, h->world,
                     rccl().error_string(st));
+    }
     return PTX_OK;
 }
 
@@ -391,12 +419,16 @@ int check_neighbours(ptx_handle *h) {
     }
     if (r != ncclSuccess) {
         (void)R.group_end();
+        h->comm_broken = true;
         return done(fail(h, PTX_E_HIP, "neighbour check: %s", R.error_string(r)));
     }
     if (int rc = group_end_wait(h)) return done(rc);
     e = hipMemcpyAsync(got, d + 6, sizeof got, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    if (e != hipSuccess) return done(fail(h, PTX_E_HIP, "neighbour check: %s", hipGetErrorString(e)));
+    if (e != hipSuccess) {
+        h->comm_broken = true;
+        return done(fail(h, PTX_E_HIP, "neighbour check: %s", hipGetErrorString(e)));
+    }
     const uint32_t *up = got[0], *dn = got[1];
     if (h->rank > 0 && (up[0] != mine[0] || up[1] != mine[1] || up[3] != mine[2] || up[5] != mine[4]))
         return done(fail(h, PTX_E_INVALID,
@@ -419,10 +451,11 @@ int render_band_nccl(ptx_handle *h) {
     Scene sc{};
     WaveBufs w{};
     bool pipe = false, moved = false;
+    const bool xchg = motion_exchange(h);  // (before band_prepare: the same on every rank)
     if (int rc = band_prepare(h, sc, w, pipe, moved)) return rc;
     TimedLaunch *ft = nullptr;
     if (int rc = band_front(h, sc, w, ft, pipe, moved)) return rc;
-    if (moved) {
+    if (xchg) {
         NCCL_CHECK(h, rccl().group_start());
         const int rc = nccl_motion_halo(h);
         if (rc) {
@@ -549,7 +582,9 @@ int ptx_comm_init(ptx_handle *h, const void *unique_id, size_t bytes, int rank, 
     h->comm = c;
     h->rank = rank;
     h->world = world;
+    h->comm_broken = false;
     if (int rc = check_neighbours(h)) {
+        h->comm_broken = true;  // (the peers' view of this exchange is unknown: abort, never flush)
         comm_destroy(h);
         return rc;
     }
@@ -613,6 +648,13 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
         if (h->band_h < h->reuse_radius && n > 1)
             return fail(h, PTX_E_INVALID, "ptx_render_bands: band %d has fewer rows than the reuse radius", i);
     }
+    // the bands agree on the motion halo before any of them enqueues work (motion_exchange)
+    const bool xchg = motion_exchange(h0);
+    for (int i = 1; i < n; ++i)
+        if (motion_exchange(hs[i]) != xchg)
+            return fail(hs[i], PTX_E_INVALID,
+                        "ptx_render_bands: band %d %s the motion halo and band 0 %s (different camera or frame count)",
+                        i, xchg ? "skips" : "needs", xchg ? "needs it" : "skips it");
     std::vector<Scene> sc(n);
     std::vector<WaveBufs> w(n);
     std::vector<TimedLaunch *> ft(n);
@@ -626,11 +668,7 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
         moved[i] = m;
         if (int rc = band_front(hs[i], sc[i], w[i], ft[i], p, m)) return rc;
     }
-    for (int i = 1; i < n; ++i)
-        if (moved[i] != moved[0])
-            return fail(hs[i], PTX_E_INVALID, "ptx_render_bands: band %d %s the history and band 0 %s", i,
-                        moved[i] ? "reprojects" : "does not reproject", moved[0] ? "does" : "does not");
-    if (moved[0]) {  // the motion halo: the neighbours' rows of the previous frame's spatial output
+    if (xchg) {  // the motion halo: the neighbours' rows of the previous frame's spatial output
         if (nccl) {
             NCCL_CHECK(h0, rccl().group_start());
             int rc = PTX_OK;
@@ -706,7 +744,7 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
     }
     for (int i = 0; i < n; ++i) {
         HIP_CHECK(hs[i], hipSetDevice(hs[i]->device));
-        if (moved[0] && !nccl) {  // (the neighbours have copied this band's history rows)
+        if (xchg && !nccl) {  // (the neighbours have copied this band's history rows)
             if (i > 0) HIP_CHECK(hs[i], hipStreamWaitEvent(hs[i]->stream, hs[i - 1]->ev_mhalo, 0));
             if (i + 1 < n) HIP_CHECK(hs[i], hipStreamWaitEvent(hs[i]->stream, hs[i + 1]->ev_mhalo, 0));
         }
@@ -734,9 +772,29 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
 }  // extern "C"
 
 namespace ptx {
+// A communicator that timed out or reported an error is aborted: ncclCommDestroy would flush
+// operations a dead or absent peer never matches.  A healthy non-blocking one is finalized
+// against the deadline first (an abort if that does not complete), then destroyed.
 void comm_destroy(ptx_handle *h) {
-    if (h->comm && rccl().ok) (void)rccl().destroy((ncclComm_t)h->comm);
+    const Rccl &R = rccl();
+    if (h->comm && R.ok) {
+        ncclComm_t c = (ncclComm_t)h->comm;
+        bool gone = false;
+        if (h->comm_broken && R.abort) {
+            (void)R.abort(c);
+            gone = true;
+        } else if (R.finalize) {
+            ncclResult_t r = R.finalize(c);
+            if (r == ncclInProgress) r = comm_wait(c, comm_timeout_s());
+            if (r != ncclSuccess && R.abort) {
+                (void)R.abort(c);
+                gone = true;
+            }
+        }
+        if (!gone) (void)R.destroy(c);
+    }
     h->comm = nullptr;
+    h->comm_broken = false;
     if (h->xstream) {
         (void)hipStreamSynchronize(h->xstream);
         (void)hipStreamDestroy(h->xstream);

@@ -145,6 +145,14 @@ struct ptx_handle {
     // (the neighbours' previous spatial output) -- their spatial passes overwrite it after this
     hipEvent_t ev_mhalo = nullptr;
     uint64_t halo_bytes_sent = 0;  // halo bytes this handle's communicator has sent (ptx_comm_info)
+    // the communicator timed out or reported an error: torn down with ncclCommAbort (a destroy
+    // would flush operations a dead peer never matches)
+    bool comm_broken = false;
+    // the motion-halo decision of band frames, from state every rank shares (the uniform sequence
+    // and the frame count, never the per-rank history state): band frames rendered and the camera
+    // words (uniform 4..22) of the last one
+    uint64_t band_frames = 0;
+    uint32_t band_camera[19] = {0};
     // ptx_present's canvas on the device; the pinned staging buffer of read_to_host
     DevBuf d_canvas;
     void *host_stage = nullptr;

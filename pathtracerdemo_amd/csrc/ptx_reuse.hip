@@ -452,10 +452,12 @@ __device__ __forceinline__ f3 x0_prev(const ReuseArgs &A, const Scene &sc, uint3
     return xform_point(A.vpinv_prev, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
 }
 struct MotionHist { bool ok; int32_t pp; uint32_t px, py, C; };
-// p' of pixel pix's primary hit X1 and the disocclusion test (oracle reproject / motion_valid):
-// C = min(C_hist, cap) when the history at p' is usable, else 0
-// (count: this call counts a reprojection past the band's motion halo in A.clip)
-__device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseArgs &A, const Surface &X1,
+// p' of pixel (x, y)'s primary hit X1 and the disocclusion test (oracle reproject / motion_valid):
+// C = min(C_hist, cap) when the history at p' is usable, else 0.  A reprojection more than
+// `radius` rows from y gets none, in every handle (oracle motion_rows): a band's motion halo
+// holds exactly those rows, so a split frame matches one handle under any motion.
+// (count: this call counts such a clipped reprojection in A.clip)
+__device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseArgs &A, const Surface &X1, uint32_t y,
                                                   bool count = false) {
     MotionHist m{false, 0, 0u, 0u, 0u};
     if (!A.hist_valid) return m;
@@ -473,7 +475,7 @@ __device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseAr
     // p' in the band's addressing: the previous frame's rows this handle holds are its band and
     // the motion halo received from the neighbours (the whole image: every row)
     const int32_t ry = (int32_t)m.py - (int32_t)sc.row_begin;
-    if (ry < A.prev_row_lo || ry >= A.prev_row_hi) {
+    if (abs((int32_t)m.py - (int32_t)y) > (int32_t)A.radius || ry < A.prev_row_lo || ry >= A.prev_row_hi) {
         if (count && A.clip) atomicAdd(A.clip, 1ull);
         return m;
     }
@@ -519,7 +521,7 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
         const uint32_t cC = valid ? rv[7].y : 0u, clen = valid ? rv[5].w : 0u;
         const bool canon = valid && cC != 0u && clen >= 2u;
         const bool count = (A.motion_slots & 2u) != 0u;  // (once per pixel: with slot 1)
-        const MotionHist mh = valid ? motion_hist(sc, A, X1, count) : MotionHist{false, 0, 0u, 0u, 0u};
+        const MotionHist mh = valid ? motion_hist(sc, A, X1, y, count) : MotionHist{false, 0, 0u, 0u, 0u};
         // the pixel's jobs through ONE job_emit site (three inlined copies needed 256 VGPRs)
 #pragma unroll 1
         for (uint32_t slot = 0; slot < kMotionJobs; ++slot) {  // (uniform)
@@ -580,7 +582,7 @@ __global__ __launch_bounds__(WB) void wtmotion_combine(Scene sc, WaveBufs w, Reu
         const float ecp = er.w > 0.0f ? luminance(mk(er.x, er.y, er.z)) : 0.0f, ecq = er.w;
         const bool canon_ok = ecq > 0.0f && ecp > 0.0f;
         const float cc = 1.0f, pc = ecp, qc = ecq, Wc = asf(r7.x);
-        const MotionHist mh = motion_hist(sc, A, X1);
+        const MotionHist mh = motion_hist(sc, A, X1, y);
         const uint32_t Cp = mh.ok ? mh.C : 0u;
         const float cp = (float)Cp;
         const uint4 *hv = A.hist + 8 * (ptrdiff_t)mh.pp;

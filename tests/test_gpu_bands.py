@@ -235,22 +235,37 @@ def test_moving_camera_bands_bit_identical(scene3, cuts, overlap):
         r.close()
 
 
-def test_band_motion_past_the_halo_is_counted(scene3):
-    """A pitch jump that moves rows by more than the motion halo (R = 6 rows): the pixels whose
-    history lies past it get none, and are counted (PTX_COUNTER_MOTION_CLIP); the frames still
-    render, finite."""
+def test_band_motion_past_the_halo_is_split_invariant(scene3, oracle_mod):
+    """A pitch jump that moves rows by more than the motion halo (R = 6 rows): the build's motion
+    rule gives no history to a reprojection more than R rows away in EVERY handle (oracle
+    motion_rows), so the 2-band split still equals one handle bit for bit, both count the same
+    clipped pixels (PTX_COUNTER_MOTION_CLIP), and the one handle equals the oracle."""
     from pathtracerdemo_amd.renderer import Renderer
+    from helpers import uniform_for
     W, H, R = 64, 96, 6
+    one = make(scene3, W, H, radius=R)
     bands = [make(scene3, W, H, radius=R, row_begin=a, row_end=b) for a, b in ((0, 48), (48, 96))]
-    for f, pitch in enumerate((0.0, 0.0, 12.0, 12.0), start=1):
+    fr = oracle_mod.Frame(uniform_for(scene3, W, H, 1), scene3.scene, scene3.geometry, scene3.accel)
+    fr.reuse = (R, 3, 20)
+    for f, pitch in enumerate((0.0, 0.0, 12.0, 12.0, 5.0), start=1):
+        pose(one, (0.0, 0.0, 6.0), 0.0, pitch)
+        one.Render()
         for b in bands:
             pose(b, (0.0, 0.0, 6.0), 0.0, pitch)
         img = np.zeros((H, W, 4), np.float32)
         Renderer.render_bands(bands, img)
         assert np.isfinite(img).all()
-    assert sum(b.read_counters()["motion_clips"] for b in bands) > 0
-    for b in bands:
-        b.close()
+        assert_same(np.concatenate([b.read_reservoir() for b in bands]), one.read_reservoir(), f"temporal output, frame {f}")
+        assert_same(np.concatenate([b.read_history() for b in bands]), one.read_history(), f"spatial output, frame {f}")
+        assert_same(img, one.read_image(), f"radiance, frame {f}")
+        fr.set_camera(one.uniform)
+        fr.set_frame_index(f)
+        fr.run_reuse_frame(threads=16)
+        assert_same(one.read_image(), fr.accum, f"oracle radiance, frame {f}")
+    clips = sum(b.read_counters()["motion_clips"] for b in bands)
+    assert clips > 0 and clips == one.read_counters()["motion_clips"]
+    for r in [one] + bands:
+        r.close()
 
 
 def test_communicator_band_moving_camera(scene3):

@@ -143,7 +143,8 @@ def test_engine_loop_bit_exact(request, oracle_mod, tmp_path, which, pipeline, W
     d = export_compiled(cs, str(tmp_path / "scene"), which)
     out = str(tmp_path / "img")
     p = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "engine_loop.js"), json.dumps(
-        {"sceneDir": d, "width": W, "height": H, "pipeline": pipeline, "ticks": PATH, "dump": DUMP,
+        {"sceneDir": d, "width": W, "height": H, "pipeline": pipeline, "ticks": [{**ev, "dt": DT} for ev in PATH],
+         "dump": DUMP,
          "out": out})], capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert p.returncode == 0, p.stderr
     ticks = json.loads(p.stdout)["ticks"]
