@@ -16,6 +16,9 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 PASS_GBUFFER, PASS_INIT, PASS_FINAL, PASS_MCPT, PASS_RESTIR = 0, 1, 2, 3, 4
 PASS_TEMPORAL, PASS_SPATIAL = 5, 6
+# the reuse pipeline's PT_1 (x_{k+1} of a hybrid-shiftable sample in pad words 24..27) and PT_4
+# (a reused reservoir's stored contribution, pt_oracle.c final_rows)
+PASS_INIT_REUSE, PASS_FINAL_REUSE = 11, 12
 # ReSTIR GI passes (build-defined; pt_oracle_gi.c)
 GI_PASS_INIT, GI_PASS_TEMPORAL, GI_PASS_SPATIAL, GI_PASS_FINAL = 7, 8, 9, 10
 GI_WORDS = 16
@@ -206,14 +209,14 @@ class Frame:
         (run_temporal_motion) instead of the same-pixel temporal pass; clearing `hist_valid`
         drops it (ptx_upload_scene / ptx_reset_accumulation do)."""
         moved = self.hist_valid and self.camera_moved()
-        for p in (PASS_GBUFFER, PASS_INIT):
+        for p in (PASS_GBUFFER, PASS_INIT_REUSE):
             self.run(p, threads, rect)
         if moved:
             self.run_temporal_motion(threads, rect)
         else:
             self.run(PASS_TEMPORAL, threads, rect)
         self.run(PASS_SPATIAL, threads, rect)
-        self.run(PASS_FINAL, threads, rect, reservoir=self.res_hist)
+        self.run(PASS_FINAL_REUSE, threads, rect, reservoir=self.res_hist)
         self.hist_valid = True
         self.prev_uniform = self.uniform.copy()
         self.prev_gbuffer[...] = self.gbuffer
@@ -228,10 +231,10 @@ class Frame:
         T = (self.H + 7) // 8
         out = np.zeros((T, 5), dtype=np.uint64)
         keys = ("rays", "instance_xforms", "aabb_tests", "tri_tests", "hits")
-        for p in (PASS_GBUFFER, PASS_INIT, PASS_TEMPORAL, PASS_SPATIAL, PASS_FINAL):
+        for p in (PASS_GBUFFER, PASS_INIT_REUSE, PASS_TEMPORAL, PASS_SPATIAL, PASS_FINAL_REUSE):
             for t in range(T):
                 rect = (0, 8 * t, self.W, min(self.H, 8 * t + 8))
-                c = self.run(p, threads, rect, reservoir=self.res_hist if p == PASS_FINAL else None)
+                c = self.run(p, threads, rect, reservoir=self.res_hist if p == PASS_FINAL_REUSE else None)
                 out[t] += np.array([c[k] for k in keys], dtype=np.uint64)
         self.hist_valid = True
         return out

@@ -823,7 +823,8 @@ typedef struct path_state {
  * has Surface[0..i] = the chain's, Lobe[1..i-1] set (and Lobe[i] for env),
  * rSeed[2..i] = BSDF seeds of vertices 1..i-1, rSeed[i+1] = NEE seed (NEE) or BSDF seed
  * (env) of vertex i, zero elsewhere. */
-static void compress_path(const path_state *ps, int i, int is_env, const light_sample *XL, uint32_t *out) {
+static void compress_path(const path_state *ps, int i, int is_env, const light_sample *XL, uint32_t *out,
+                          int rcnext) {
     uint32_t lobe[8] = {0}, seed[8] = {0};
     for (int k = 1; k < i; ++k) { lobe[k] = ps->lobe[k]; seed[k + 1] = ps->bsdf_seed[k]; }
     if (is_env) { lobe[i] = ps->lobe[i]; seed[i + 1] = ps->bsdf_seed[i]; }
@@ -858,10 +859,13 @@ static void compress_path(const path_state *ps, int i, int is_env, const light_s
         out[22] = is_light ? LOBE_LIGHT : lobe[k];
         out[21] = lobe[k - 1];
         if (!is_light) encode_compact(ps->cs[k], out + 16);
+        /* the reuse pipeline's PT_1 (rcnext): the vertex after x_k in words 24..27 (pads in the
+         * reference layout, PT_4 never reads them) -- the hybrid shift keeps it fixed (RES_RC_NEXT) */
+        if (rcnext && k + 1u < length) encode_compact(ps->cs[k + 1u], out + 24);
     }
 }
 
-static void init_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t x, uint32_t y, uint32_t *res) {
+static void init_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t x, uint32_t y, uint32_t *res, int rcnext) {
     const uint32_t W = c->U[U_W];
     compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
     if (!x1.valid) { /* reservoir unobservable: PT_4 returns before LoadReservoir (:1404-1408) */
@@ -935,20 +939,24 @@ static void init_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t x, uint32
     }
     /* StoreReservoir, PT_1:1475-1483 */
     if (sel_i < 0) memset(res, 0, 4u * PTO_RESERVOIR_WORDS); /* zero Path(): length 0, k 0 */
-    else compress_path(&ps, sel_i, sel_env, &sel_XL, res);
+    else compress_path(&ps, sel_i, sel_env, &sel_XL, res, rcnext);
     res[28] = u32_of(w_sum / p_hat_sel);
     res[29] = C;
 }
 
-void pto_init(const pto_inputs *in, const uint32_t *gbuffer, int x0, int y0, int x1, int y1, uint32_t *reservoir,
-              pto_counters *cnt) {
+static void init_rows(const pto_inputs *in, const uint32_t *gbuffer, int x0, int y0, int x1, int y1,
+                      uint32_t *reservoir, pto_counters *cnt, int rcnext) {
     ctx c;
     ctx_init(&c, in, EPS_INIT, cnt);
     const uint32_t W = c.U[U_W];
     for (int y = y0; y < y1; ++y)
         for (int x = x0; x < x1; ++x)
             init_pixel(&c, gbuffer, (uint32_t)x, (uint32_t)y,
-                       reservoir + PTO_RESERVOIR_WORDS * ((uint32_t)y * W + (uint32_t)x));
+                       reservoir + PTO_RESERVOIR_WORDS * ((uint32_t)y * W + (uint32_t)x), rcnext);
+}
+void pto_init(const pto_inputs *in, const uint32_t *gbuffer, int x0, int y0, int x1, int y1, uint32_t *reservoir,
+              pto_counters *cnt) {
+    init_rows(in, gbuffer, x0, y0, x1, y1, reservoir, cnt, 0);
 }
 
 /* ================================================================== PT_4 final shading */
@@ -1005,16 +1013,29 @@ static void final_pixel(const ctx *c, const uint32_t *gbuffer, const uint32_t *r
     write_color(c, px, vscale(f, f32_of(res[28])));
 }
 
-void pto_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *reservoir, int x0, int y0, int x1,
-               int y1, float *accum, pto_counters *cnt) {
+/* reuse: PT_4 of the reuse pipeline -- a reservoir a reuse pass wrote carries its sample's
+ * PathContribution at this pixel (words 26, 27, 30; flag word 31, write_reused): f * UCW, the
+ * contribution of the shifted path it holds (a hybrid-shifted sample is NOT its seeds' replay);
+ * any other reservoir is PT_4's replay (final_pixel). */
+static void final_rows(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *reservoir, int x0, int y0,
+                       int x1, int y1, float *accum, pto_counters *cnt, int reuse) {
     ctx c;
     ctx_init(&c, in, EPS_FINAL, cnt);
     const uint32_t W = c.U[U_W];
     for (int y = y0; y < y1; ++y)
         for (int x = x0; x < x1; ++x) {
             uint32_t p = (uint32_t)y * W + (uint32_t)x;
-            final_pixel(&c, gbuffer, reservoir + PTO_RESERVOIR_WORDS * p, (uint32_t)x, (uint32_t)y, accum + 4u * p);
+            const uint32_t *res = reservoir + PTO_RESERVOIR_WORDS * p;
+            float *px = accum + 4u * p;
+            if (reuse && decode_compact(gbuffer + 4u * p).valid && res[29] != 0u && res[23] >= 2u && res[31] == 1u)
+                write_color(&c, px, vscale(V3(f32_of(res[26]), f32_of(res[27]), f32_of(res[30])), f32_of(res[28])));
+            else
+                final_pixel(&c, gbuffer, res, (uint32_t)x, (uint32_t)y, px);
         }
+}
+void pto_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *reservoir, int x0, int y0, int x1,
+               int y1, float *accum, pto_counters *cnt) {
+    final_rows(in, gbuffer, reservoir, x0, y0, x1, y1, accum, cnt, 0);
 }
 
 /* ================================================================== reuse passes
@@ -1072,9 +1093,68 @@ static void rr_step(const surface *X, v3 V, v3 L, float pdf, v3 *f, float *p, fl
     if (ps > 1.0f) *beta /= ps;
 }
 
-/* The reservoir sample `res` replayed in the domain of pixel (x, y) with G-buffer hit x1:
- * RegeneratePath + PathContribution of PT_4:1306-1384 plus the shift's pdf product. */
-static eval_out eval_sample(const ctx *c, uint32_t x, uint32_t y, compact x1, const uint32_t *res) {
+/* ---- the hybrid (reconnection) shift, docs/theory/memo.md:174-229 ----
+ * PT_1's CompressPath stores k = SafeReconnectionIndex(path) (PT_1:1262-1353): the first vertex
+ * x_k (k >= 2) whose edge from x_{k-1} is long (>= RECONNECTION_DISTANCE) and rough at both ends
+ * (>= RECONNECTION_ROUGHNESS; a Lambert lobe counts as rough), else k = length when the last
+ * vertex may reconnect to the light sample, else 0.  RcVertex = x_k's compact surface.
+ *  - k in [2, length-1] (a surface reconnection): the shifted path into domain y is
+ *      y0 -> y1 -> (random replay of the seeds) -> y_{k-1} -> x_k -> x_{k+1} -> .. -> XL:
+ *    the prefix up to y_{k-1} replays the sample's seeds from y's primary hit, x_k and the
+ *    suffix after it are kept (x_{k+1}: RES_RC_NEXT, the light sample XL).  Valid iff the prefix
+ *    replays (every traced ray hits), the shifted path has the SAME reconnection index (its
+ *    edges before k are not safe, (y_{k-1}, x_k) is -- the lobes: the replayed ones, then the
+ *    stored Lobe_{k-1}, Lobe_k), and nothing lies between y_{k-1} and x_k (the closest hit along
+ *    the connection, if any, at >= 0.999 of its length).
+ *  - k = length (light) or 0 (unshiftable): random replay of every vertex with the light
+ *    endpoint kept (the build's shift of round 1).
+ * Measure and Jacobian.  The reuse passes integrate in PT_1's measure (solid angle per sampled
+ * direction, the light sample's own at the end), J(x -> y) = q(x) / q(y):
+ *    random replay:     q = prod_{replayed i} pdf_i / (g beta)            (g: rect light geometry)
+ *    hybrid, vertex k:  q = (prod_{i <= k-2} pdf_i * |x_k - x_{k-1}|^2 / |n_k . w|) / beta
+ * -- the replayed directions keep their primary samples (dw_y / dw_x = pdf_x / pdf_y), the
+ * reconnection keeps x_k in area (dw = dA |n_k . w| / d^2), the suffix is unchanged.  This is the
+ * memo's J = J_y / J_x written in PT_1's measure instead of primary-sample space (there the
+ * pdfs of picking x_k and x_{k+1} enter; here the pdfs of the directions the shift changes are
+ * not part of the sample's measure).  beta is PT_1's Russian-roulette factor along the path
+ * (rr_step), recomputed with the shifted path's own directions.
+ * Every shift keeps the sample's reconnection index: the shifted path's own SafeReconnectionIndex
+ * must be k (else the shift is invalid), so a path of a domain is reached only under the label
+ * PT_1 would give it there and the MIS weights of the techniques that reach it sum to one.  (The
+ * lobes: the replayed ones, the stored Lobe_{k-1} / Lobe_k, an env escape's lobe Lobe_{k-1} when
+ * k = length, else taken as GGX -- material roughness -- exact whenever the Lambert promotion of
+ * IsSafeToReconnect decides nothing, as in the benchmark scenes: opaque roughness >= 0.5, glass 0.)
+ * Evaluating the canonical sample AT HOME (its own pixel, the reference-layout PT_1 output)
+ * replays it (PT_4's RegeneratePath: same vertices), with q in its sample's form above.
+ * Reuse layout: a reservoir a reuse pass wrote (RES_REUSE_LAYOUT in word 20) holds x_{k+1} in
+ * words 0..3 -- seeds a hybrid shift at k = 2 never replays -- because words 24..31 carry
+ * p_hat, q and f there; PT_1's output holds it in 24..27. */
+#define RES_REUSE_LAYOUT 0x100u
+static inline int safe_edge(const surface *A, uint32_t la, const surface *B, uint32_t lb) { /* IsSafeToReconnect */
+    const float ra = la == LOBE_LAMBERT ? 1.0f : A->mat.roughness;
+    const float rb = lb == LOBE_LAMBERT ? 1.0f : B->mat.roughness;
+    const int rough = fmin_(ra, rb) >= RECONNECTION_ROUGHNESS;
+    const int far = vlength(vsub(A->pos, B->pos)) >= RECONNECTION_DISTANCE;
+    return far && rough;
+}
+/* SafeReconnectionIndex (PT_1:1281-1296) of a shifted path S[0..length-1] with lobes[1..]
+ * (compress_path's conventions: the NEE vertex's lobe 0 = Lambert) and light sample XL */
+static uint32_t path_label(const surface *S, const uint32_t *lobes, uint32_t length, const light_sample *XL) {
+    for (uint32_t kk = 2u; kk < length; ++kk)
+        if (safe_edge(&S[kk - 1u], lobes[kk - 1u], &S[kk], lobes[kk])) return kk;
+    const int rough = S[length - 1u].mat.roughness >= RECONNECTION_ROUGHNESS;
+    const int dirl = XL->type == LIGHT_DIRECTION || XL->type == LIGHT_ENV;
+    const int far = dirl || vlength(vsub(S[length - 1u].pos, XL->pos)) >= RECONNECTION_DISTANCE;
+    return (far && rough) ? length : 0u;
+}
+static inline const uint32_t *res_rc_next(const uint32_t *r) { /* RES_RC_NEXT: x_{k+1}'s compact */
+    return (r[20] & RES_REUSE_LAYOUT) ? r : r + 24;
+}
+
+/* The reservoir sample `res` in the domain of pixel (x, y) with G-buffer hit x1 (home: the
+ * pixel's own PT_1 sample, replayed): PathContribution of PT_4:1306-1336 over the shifted path
+ * plus the shift's measure q. */
+static eval_out eval_sample(const ctx *c, uint32_t x, uint32_t y, compact x1, const uint32_t *res, int home) {
     eval_out o = {0, 0.0f, 0.0f, {0.0f, 0.0f, 0.0f}};
     const uint32_t length = res[23];
     if (!x1.valid || res[29] == 0u || length < 2u) return o;
@@ -1085,24 +1165,53 @@ static eval_out eval_sample(const ctx *c, uint32_t x, uint32_t y, compact x1, co
     XL.id = (int32_t)res[11];
     XL.Le = V3(f32_of(res[12]), f32_of(res[13]), f32_of(res[14]));
     XL.pdf = f32_of(res[15]);
+    const uint32_t k = res[20] & 0xFFu;
+    const int hyb = k >= 2u && k < length;   /* reconnection at the surface vertex x_k */
+    const int shift = hyb && !home;          /* replay only the prefix up to y_{k-1} */
     surface S[8];
     memset(S, 0, sizeof S);
+    uint32_t lobes[8] = {0};
     S[0].pos = get_x0(c, x, y);
     S[1] = get_surface(c, x1);
     float prod = 1.0f, beta = 1.0f, rr_p = 1.0f;
     v3 rr_f = V3(1.0f, 1.0f, 1.0f);
     int rr_ok = 1;
-    for (uint32_t i = 1; i + 1u < length; ++i) {
+    const uint32_t reach = shift ? k - 1u : length - 1u; /* the replay reaches S[reach] */
+    for (uint32_t i = 1; i < reach; ++i) {
         v3 V = vnormalize(vsub(S[i - 1].pos, S[i].pos));
         uint32_t seed = res[i - 1u], lobe;
         v3 dir = sample_bsdf(&seed, &S[i], V, &lobe);
+        lobes[i] = lobe;
         const float pdf = pdf_bsdf(&S[i], V, dir);
-        prod *= pdf;
+        if (!hyb || i + 2u <= k) prod *= pdf; /* (hybrid: the replayed prefix only) */
         rr_step(&S[i], V, dir, pdf, &rr_f, &rr_p, &beta, &rr_ok);
         ray r = {S[i].pos, dir};
         hit h = trace_ray(c, r);
         if (!h.valid) return o; /* the replayed path escapes: no such path in this domain */
         S[i + 1] = get_surface(c, h.s);
+    }
+    if (shift) {
+        S[k] = get_surface(c, decode_compact(res + 16));
+        lobes[k - 1u] = res[21];
+        lobes[k] = res[22];
+        if (path_label(S, lobes, k + 1u, &XL) != k) return o; /* the same reconnection index */
+        const v3 dv = vsub(S[k].pos, S[k - 1u].pos);
+        const float dist = vlength(dv);
+        const v3 dir = vdivs(dv, dist);
+        ray r = {S[k - 1u].pos, dir};
+        hit h = trace_ray(c, r);
+        if (h.valid && h.t < dist * 0.999f) return o; /* occluded: nothing between y_{k-1} and x_k */
+        const v3 V = vnormalize(vsub(S[k - 2u].pos, S[k - 1u].pos));
+        rr_step(&S[k - 1u], V, dir, pdf_bsdf(&S[k - 1u], V, dir), &rr_f, &rr_p, &beta, &rr_ok);
+        if (k + 1u < length) { /* the kept vertex after x_k */
+            S[k + 1u] = get_surface(c, decode_compact(res_rc_next(res)));
+            const v3 V2 = vnormalize(vsub(S[k - 1u].pos, S[k].pos));
+            const v3 L2 = vnormalize(vsub(S[k + 1u].pos, S[k].pos));
+            rr_step(&S[k], V2, L2, pdf_bsdf(&S[k], V2, L2), &rr_f, &rr_p, &beta, &rr_ok);
+        }
+    } else if (!home) { /* random replay keeps the label too (k = length or 0) */
+        if (XL.type == LIGHT_ENV) lobes[length - 1u] = k == length ? res[21] : LOBE_GGX;
+        if (path_label(S, lobes, length, &XL) != k) return o;
     }
     v3 f = V3(1.0f, 1.0f, 1.0f);
     for (uint32_t i = 1; i + 1u < length; ++i) {
@@ -1123,7 +1232,15 @@ static eval_out eval_sample(const ctx *c, uint32_t x, uint32_t y, compact x1, co
         g = fabsf(vdot(get_light(c, (uint32_t)XL.id).dir, Ld)) / vdot(r, r);
     }
     f = vmul(f, vscale(l_emit(c, &XL, Xc), visibility(c, Xc->pos, XL.pos)));
-    const float q = prod / (g * beta);
+    float q;
+    if (hyb) { /* the reconnection edge's area -> solid angle factor at x_k */
+        const v3 dv = vsub(S[k].pos, S[k - 1u].pos);
+        const float d2 = vdot(dv, dv);
+        const float ck = fabsf(vdot(S[k].nrm, vdivs(dv, sqrtf(d2))));
+        q = (prod * (d2 / ck)) / beta;
+    } else {
+        q = prod / (g * beta);
+    }
     o.valid = rr_ok && q > 0.0f && q <= 3.402823466e38f;
     o.phat = o.valid ? luminance(f) : 0.0f;
     o.q = o.valid ? q : 0.0f;
@@ -1143,6 +1260,11 @@ static void write_reused(uint32_t *out, const uint32_t *src, float p_sel, float 
                          uint32_t C) {
     uint32_t tmp[24];
     memcpy(tmp, src, sizeof tmp); /* src may alias out (temporal works in place) */
+    if (f_sel.known && !(tmp[20] & RES_REUSE_LAYOUT)) { /* a PT_1 sample: into the reuse layout */
+        const uint32_t k = tmp[20] & 0xFFu;
+        if (k >= 2u && k + 1u < tmp[23]) memcpy(tmp, src + 24, 4u * 4u); /* x_{k+1} over unused seeds */
+        tmp[20] |= RES_REUSE_LAYOUT;
+    }
     memset(out, 0, 4u * PTO_RESERVOIR_WORDS);
     memcpy(out, tmp, sizeof tmp);
     out[24] = u32_of(p_sel);
@@ -1165,7 +1287,7 @@ static void temporal_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t *cur,
     compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
     if (!x1.valid) return; /* PT_1 wrote the zero reservoir; PT_4 never reads it */
     uint32_t seed = reuse_seed(c, x, y, SALT_TEMPORAL);
-    eval_out ec = eval_sample(c, x, y, x1, cur);
+    eval_out ec = eval_sample(c, x, y, x1, cur, 1);
     const int canon_ok = ec.valid && ec.phat > 0.0f;
     /* confidences depend on geometry and history only, never on the samples: a PT_1
      * reservoir counts 1, the history min(C_hist, cap) */
@@ -1263,7 +1385,7 @@ static void temporal_motion_pixel(const ctx *c, const ctx *cprev, const float *v
     compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
     if (!x1.valid) return; /* PT_1 wrote the zero reservoir; PT_4 never reads it */
     uint32_t seed = reuse_seed(c, x, y, SALT_TEMPORAL);
-    eval_out ec = eval_sample(c, x, y, x1, cur);
+    eval_out ec = eval_sample(c, x, y, x1, cur, 1);
     const int canon_ok = ec.valid && ec.phat > 0.0f;
     const float cc = 1.0f, pc = ec.phat, qc = ec.q, Wc = f32_of(cur[28]);
     /* the history pixel p' and its domain */
@@ -1289,7 +1411,7 @@ static void temporal_motion_pixel(const ctx *c, const ctx *cprev, const float *v
     sel_f ff = {0, {0.0f, 0.0f, 0.0f}};
     if (Cp != 0u && h[23] >= 2u && f32_of(h[24]) > 0.0f) {
         const float ph = f32_of(h[24]), qh = f32_of(h[25]), Wh = f32_of(h[28]);
-        eval_out F = eval_sample(c, x, y, x1, h);
+        eval_out F = eval_sample(c, x, y, x1, h, 0);
         if (F.valid) {
             const float J = qh / F.q;
             const float pb = ph / J;
@@ -1304,7 +1426,7 @@ static void temporal_motion_pixel(const ctx *c, const ctx *cprev, const float *v
     /* backward: this pixel's sample in the previous domain (its weight) */
     float Q = 1.0f;
     if (canon_ok && Cp != 0u) {
-        eval_out B = eval_sample(cprev, px, py, x1p, cur);
+        eval_out B = eval_sample(cprev, px, py, x1p, cur, 0);
         if (B.valid) {
             const float pbc = B.phat * qc / B.q;
             const float den = cc * pc + cp * pbc;
@@ -1391,7 +1513,7 @@ static void spatial_pixel(const ctx *c, const uint32_t *gbuffer, const uint32_t 
             const float cn = (float)rn[29], pn = f32_of(rn[24]), qn = f32_of(rn[25]), Wn = f32_of(rn[28]);
             Csum += rn[29];
             if (rn[23] >= 2u && pn > 0.0f) { /* forward: the neighbour's sample in this pixel's domain */
-                eval_out F = eval_sample(c, x, y, x1, rn);
+                eval_out F = eval_sample(c, x, y, x1, rn, 0);
                 if (F.valid) {
                     const float J = qn / F.q;
                     const float pb = pn / J;
@@ -1404,7 +1526,7 @@ static void spatial_pixel(const ctx *c, const uint32_t *gbuffer, const uint32_t 
                 }
             }
             if (canon_ok) { /* backward: this pixel's sample in the neighbour's domain */
-                eval_out B = eval_sample(c, nx, ny, decode_compact(gbuffer + 4u * nb[k]), rc);
+                eval_out B = eval_sample(c, nx, ny, decode_compact(gbuffer + 4u * nb[k]), rc, 0);
                 if (B.valid) {
                     const float pbc = B.phat * qc / B.q;
                     const float den = cc * pc + Mf * cn * pbc;
@@ -1434,7 +1556,7 @@ void pto_eval_sample(const pto_inputs *in, const uint32_t *gbuffer, uint32_t x, 
                      float out[3]) {
     ctx c;
     ctx_init(&c, in, EPS_FINAL, NULL);
-    eval_out o = eval_sample(&c, x, y, decode_compact(gbuffer + 4u * (y * c.U[U_W] + x)), res);
+    eval_out o = eval_sample(&c, x, y, decode_compact(gbuffer + 4u * (y * c.U[U_W] + x)), res, 0);
     out[0] = (float)o.valid;
     out[1] = o.phat;
     out[2] = o.q;
@@ -1605,6 +1727,8 @@ static void *worker(void *arg) {
         switch (j->pass) {
         case 0: pto_gbuffer(j->in, j->x0, y, j->x1, y + 1, j->gbuffer, &j->cnt); break;
         case 1: pto_init(j->in, j->gbuffer, j->x0, y, j->x1, y + 1, j->reservoir, &j->cnt); break;
+        case 11: init_rows(j->in, j->gbuffer, j->x0, y, j->x1, y + 1, j->reservoir, &j->cnt, 1); break;
+        case 12: final_rows(j->in, j->gbuffer, j->reservoir, j->x0, y, j->x1, y + 1, j->accum, &j->cnt, 1); break;
         case 2: pto_final(j->in, j->gbuffer, j->reservoir, j->x0, y, j->x1, y + 1, j->accum, &j->cnt); break;
         case 3: pto_mcpt(j->in, j->x0, y, j->x1, y + 1, j->accum, &j->cnt); break;
         case 5: pto_temporal(j->in, j->gbuffer, j->reservoir, j->res_hist, j->prm, j->x0, y, j->x1, y + 1, &j->cnt); break;
@@ -1663,7 +1787,7 @@ int pto_run(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1
         if (!rc) rc = run_pass(2, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, NULL, NULL, accum, cnt);
         return rc;
     }
-    if (pass < 0 || pass > 3) return -2;
+    if ((pass < 0 || pass > 3) && pass != 11 && pass != 12) return -2;
     return run_pass(pass, nthreads, in, x0, y0, x1, y1, gbuffer, reservoir, NULL, NULL, accum, cnt);
 }
 

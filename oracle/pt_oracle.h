@@ -61,7 +61,9 @@ void pto_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t *re
 void pto_mcpt(const pto_inputs *in, int x0, int y0, int x1, int y1, float *accum /* W*H*4 in/out */,
               pto_counters *cnt);
 
-/* Multithreaded driver: pass = 0 gbuffer, 1 init, 2 final, 3 mcpt, 4 restir frame (0,1,2).
+/* Multithreaded driver: pass = 0 gbuffer, 1 init, 2 final, 3 mcpt, 4 restir frame (0,1,2);
+ * the reuse pipeline's PT_1 (11: x_{k+1} of a hybrid-shiftable sample in pad words 24..27) and
+ * PT_4 (12: a reused reservoir's stored contribution f * UCW, a PT_1 reservoir replayed).
  * Rows [y0,y1) are interleaved over nthreads pthreads.  Returns 0 on success. */
 int pto_run(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, uint32_t *gbuffer,
             uint32_t *reservoir, float *accum, pto_counters *cnt);

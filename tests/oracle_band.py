@@ -5,7 +5,7 @@ import ctypes
 
 import numpy as np
 
-PASS_MAP = {0: 0, 1: 1, 2: 2, 3: 3, 8: 5, 9: 6}  # include/ptx.h pass ids -> oracle passes
+PASS_MAP = {0: 0, 1: 11, 2: 12, 3: 3, 8: 5, 9: 6}  # include/ptx.h pass ids -> the reuse pipeline's oracle passes
 GI_PASS_MAP = {1: 7, 2: 10, 8: 8, 9: 9}           # ... of a GI handle (PTX_PIPELINE_RESTIR_GI)
 
 
@@ -28,7 +28,7 @@ class OracleBand:
                     fr.hist_valid = True
                 continue
             op = PASS_MAP[p]
-            if op == self.O.PASS_FINAL:
+            if op == self.O.PASS_FINAL_REUSE:
                 fr.run(op, threads=2, rect=rect, reservoir=fr.res_hist)
             else:
                 fr.run(op, threads=2, rect=rect)

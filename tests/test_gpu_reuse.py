@@ -51,7 +51,7 @@ def test_temporal_and_spatial_passes_bit_exact(scene1, oracle_mod, native, prm):
     fr.set_frame_index(1)
     fr.run_reuse_frame(threads=8)
     fr.set_frame_index(2)
-    for p in (O.PASS_GBUFFER, O.PASS_INIT):
+    for p in (O.PASS_GBUFFER, O.PASS_INIT_REUSE):
         fr.run(p)
     hist_prev = fr.res_hist.copy()
     r = reuse_renderer(scene1, W, H, prm)
@@ -72,7 +72,7 @@ def test_temporal_and_spatial_passes_bit_exact(scene1, oracle_mod, native, prm):
     fr.run(O.PASS_SPATIAL)
     assert_same(r.read_history(), fr.res_hist, "spatial output")
     r.run_pass(native.PTX_PASS_FINAL)
-    fr.run(O.PASS_FINAL, reservoir=fr.res_hist)
+    fr.run(O.PASS_FINAL_REUSE, reservoir=fr.res_hist)
     assert_same(r.read_image(), fr.accum, "PT_4 on the spatial output")
     r.close()
 
@@ -391,7 +391,7 @@ def test_write_buffer_passes_beside_a_rendering_handle(scene1, scene3, oracle_mo
     fr.set_frame_index(1)
     fr.run_reuse_frame(threads=8)
     fr.set_frame_index(2)
-    for p in (O.PASS_GBUFFER, O.PASS_INIT):
+    for p in (O.PASS_GBUFFER, O.PASS_INIT_REUSE):
         fr.run(p)
     hist_prev = fr.res_hist.copy()
     a = reuse_renderer(scene1, W, H)
@@ -415,7 +415,7 @@ def test_write_buffer_passes_beside_a_rendering_handle(scene1, scene3, oracle_mo
     fr.run(O.PASS_SPATIAL)
     assert_same(a.read_history(), fr.res_hist, "spatial output")
     a.run_pass(native.PTX_PASS_FINAL)
-    fr.run(O.PASS_FINAL, reservoir=fr.res_hist)
+    fr.run(O.PASS_FINAL_REUSE, reservoir=fr.res_hist)
     assert_same(a.read_image(), fr.accum, "PT_4 on the spatial output")
     assert_same(b.read_history(), frb.res_hist, "the other handle's spatial output")
     assert_same(b.read_image(), frb.accum, "the other handle's radiance")

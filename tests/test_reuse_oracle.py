@@ -53,9 +53,43 @@ def test_temporal_spatial_reuse_converges_to_plain(oracle_mod, scene1):
     blocks = lambda m: (m * valid).reshape(4, 8, 4, 8).sum((1, 3)) / np.maximum(valid.reshape(4, 8, 4, 8).sum((1, 3)), 1)
     ba, bb = blocks(a.mean(0)), blocks(b.mean(0))
     dense = valid.reshape(4, 8, 4, 8).sum((1, 3)) >= 16
-    assert np.abs(bb / ba - 1)[dense].max() < 0.04, bb / ba
+    # (correlated frames: block means vary by +-3.5 % between seeds on the build before the
+    # hybrid shift too; the per-pixel unbiasedness is test_temporal_spatial_reuse_is_unbiased_per_pixel)
+    assert np.abs(bb / ba - 1)[dense].max() < 0.06, bb / ba
     assert abs(b.mean(0)[valid].mean() / a.mean(0)[valid].mean() - 1) < 0.015
     assert b.var(0)[valid].mean() < 0.25 * a.var(0)[valid].mean()
+
+
+@pytest.mark.parametrize("scene", ["scene1", "scene3"])
+def test_temporal_spatial_reuse_is_unbiased_per_pixel(request, oracle_mod, scene):
+    """The whole pipeline (temporal history capped at 20, spatial 3 neighbours in radius 30)
+    over 384 independent 3-frame sequences against plain PT_1 + PT_4: per-pixel z-scores of the
+    third frame's estimate have mean ~0.  The hybrid shift carries ~20 % of the reused samples
+    (k in [2, length-1]: reconnection at x_k), random replay the rest; each keeps its label."""
+    O = oracle_mod
+    cs = request.getfixturevalue(scene)
+    a, valid = frames(O, cs, 512, None, f0=100000)
+    n, L = 384, 3
+    b = np.zeros((n, H, W))
+    hyb = tot = 0
+    for sq in range(n):
+        fr = O.Frame(uniform_for(cs, W, H), cs.scene, cs.geometry, cs.accel)
+        fr.reuse = (30, 3, 20)
+        for j in range(L):
+            f = 1 + sq * L + j
+            fr.set_frame_index(f)
+            fr.accum[:] = 0
+            fr.run_reuse_frame(threads=8)
+        b[sq] = fr.accum[..., :3].astype(np.float64).mean(-1) * (f + 1)
+        r = fr.res_hist
+        k, ln, v = r[..., 20] & 0xFF, r[..., 23], r[..., 29] > 0
+        hyb += int((v & (k >= 2) & (k < ln)).sum())
+        tot += int(v.sum())
+    se = np.sqrt(a.var(0) / len(a) + b.var(0) / len(b)) + 1e-30
+    z = ((b.mean(0) - a.mean(0)) / se)[valid]
+    assert abs(z.mean()) < 0.2, z.mean()
+    assert (np.abs(z) > 4.5).mean() < 0.01
+    assert hyb > 0.1 * tot
 
 
 def test_reuse_passes_are_deterministic_across_threads(oracle_mod, scene3):
@@ -77,7 +111,7 @@ def test_reused_reservoirs_store_their_own_domain_target(oracle_mod, scene1):
     fr = O.Frame(uniform_for(scene1, W, H), scene1.scene, scene1.geometry, scene1.accel)
     for f in (1, 2):
         fr.set_frame_index(f)
-        for p in (O.PASS_GBUFFER, O.PASS_INIT, O.PASS_TEMPORAL):
+        for p in (O.PASS_GBUFFER, O.PASS_INIT_REUSE, O.PASS_TEMPORAL):
             fr.run(p, 4)
         if f == 1:
             fr.run(O.PASS_SPATIAL, 4)
@@ -86,18 +120,28 @@ def test_reused_reservoirs_store_their_own_domain_target(oracle_mod, scene1):
     lib.pto_eval_sample.argtypes = [ctypes.POINTER(O.Inputs), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                     ctypes.c_void_p, ctypes.c_void_p]
     inp = O.Inputs(fr.uniform.ctypes.data, fr.scene.ctypes.data, fr.geometry.ctypes.data, fr.accel.ctypes.data)
-    checked = 0
+    checked = hybrid = 0
     for y in range(0, H, 3):
         for x in range(0, W, 3):
             rv = np.ascontiguousarray(fr.reservoir[y, x])
             if rv[23] < 2 or rv[29] == 0:
                 continue
             out = np.zeros(3, np.float32)
+            # (the shift into its own pixel: random replay, or the hybrid shift's prefix replay +
+            # reconnection, which reach the same vertices)
             lib.pto_eval_sample(ctypes.byref(inp), fr.gbuffer.ctypes.data, x, y, rv.ctypes.data, out.ctypes.data)
             if out[0]:
-                assert out[1] == rv[24:25].view(np.float32)[0] and out[2] == rv[25:26].view(np.float32)[0]
+                p, q = rv[24:25].view(np.float32)[0], rv[25:26].view(np.float32)[0]
+                assert out[1] == p
+                if 2 <= (rv[20] & 0xFF) < rv[23]:
+                    # hybrid: the same path and f; beta's roulette terms along the connection's
+                    # direction instead of the sampled one (rounding)
+                    assert abs(out[2] / q - 1) < 1e-4
+                    hybrid += 1
+                else:
+                    assert out[2] == q
                 checked += 1
-    assert checked > 20
+    assert checked > 20 and hybrid > 3
 
 
 # ------------------------------------------------------------------ temporal reuse under camera motion
@@ -155,7 +199,7 @@ def test_motion_reprojection_is_the_identity_for_a_still_camera(oracle_mod, scen
     fr = O.Frame(u, scene1.scene, scene1.geometry, scene1.accel)
     fr.run_reuse_frame(threads=8)
     fr.set_frame_index(2)
-    for p in (O.PASS_GBUFFER, O.PASS_INIT):
+    for p in (O.PASS_GBUFFER, O.PASS_INIT_REUSE):
         fr.run(p, threads=8)
     hist = fr.res_hist.copy()
     fr.run_temporal_motion(threads=8)

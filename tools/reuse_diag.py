@@ -29,7 +29,7 @@ for f in range(1, frames + 1):
     fr.set_frame_index(f)
     r.Update()
     # GPU pass by pass, oracle pass by pass, compare after each
-    for gp, op, nm in ((N.PTX_PASS_GBUFFER, O.PASS_GBUFFER, "gbuffer"), (N.PTX_PASS_INIT, O.PASS_INIT, "init"),
+    for gp, op, nm in ((N.PTX_PASS_GBUFFER, O.PASS_GBUFFER, "gbuffer"), (N.PTX_PASS_INIT, O.PASS_INIT_REUSE, "init"),
                        (N.PTX_PASS_TEMPORAL, O.PASS_TEMPORAL, "temporal"), (N.PTX_PASS_SPATIAL, O.PASS_SPATIAL, "spatial")):
         r.run_pass(gp)
         fr.run(op, threads=8)
@@ -50,5 +50,5 @@ for f in range(1, frames + 1):
             elif nm != "gbuffer":
                 r.write_buffer(N.PTX_BUF_RESERVOIR, fr.reservoir)
     r.run_pass(N.PTX_PASS_FINAL)
-    fr.run(O.PASS_FINAL, threads=8, reservoir=fr.res_hist)
+    fr.run(O.PASS_FINAL_REUSE, threads=8, reservoir=fr.res_hist)
     fr.hist_valid = True
