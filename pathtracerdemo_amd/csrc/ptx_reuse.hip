@@ -22,7 +22,7 @@ namespace ptx {
 constexpr uint32_t SALT_TEMPORAL = 0x54454D50u, SALT_SPATIAL = 0x53504154u;
 
 // Job state, SoA float4 slots (slot k of job j at jstate[k * njobs + j]):
-// HDR {i | length << 8 | phase << 16, rSeed[1], ray idx, sample ref}; F {f, prod | q};
+// HDR {hw, rSeed[1], ray idx, sample ref}; F {f, prod | q};
 // CUR {pos, inst << 16 | mat}; NRM {nrm, beta}; PREV {prev pos, rr_p}; RRF {rr_f, -}.
 // A FRESH job (its first regenerated ray just emitted from the domain's primary hit: i == 1,
 // phase 0 -- most jobs of a start kernel) stores 48 B instead of 96: HDR {.. | 1 << 24, domain
@@ -30,14 +30,21 @@ constexpr uint32_t SALT_TEMPORAL = 0x54454D50u, SALT_SPATIAL = 0x53504154u;
 // data the next step can gather with the same bits: f = (1, 1, 1), the current vertex = the
 // domain's surface record, the previous one = its camera point (x0_of), rSeed[1] = word 1 of
 // the sample's reservoir.
+// hw = i | length << 8 | phase << 16 (2 bits) | lab << 18 (3) | rok << 21 | shift << 22 |
+// fresh << 24 | k << 25 (3).  phase: 0 a regenerated BSDF ray out, 1 the light segment's
+// Visibility out, 2 the hybrid shift's connection ray out.  shift / k / lab / rok: the hybrid
+// shift and the label check (oracle eval_sample), below.
 enum : uint32_t { JS_HDR, JS_F, JS_CUR, JS_NRM, JS_PREV, JS_RRF, JS_COUNT };
 constexpr uint32_t kJobFresh = 1u << 24;
+constexpr uint32_t kResReuseLayout = 0x100u;  // word 20 of a reservoir a reuse pass wrote (oracle RES_REUSE_LAYOUT)
 #ifndef PTX_JOB_FRESH
 #define PTX_JOB_FRESH 1  // (A/B: 0 stores every job in the full 96-byte layout)
 #endif
 
 struct Job {
     uint32_t i, length, phase, seed1, idx, matref;
+    uint32_t k, lab;  // the sample's reconnection index; shift: the shifted path's first safe edge so far
+    bool shift, rok;  // a shift into another domain (else the sample at home); the current vertex's rough bit
     int32_t ref;  // reservoir index of the sample (band-relative; halo rows are < 0 or >= npix)
     int32_t dom;  // band index of the domain pixel (its camera point and primary hit)
     f3 f;
@@ -66,21 +73,28 @@ __device__ __forceinline__ const uint4 *res_of(const ReuseArgs &A, int32_t ref) 
 // stored in the full layout, as the fresh one re-derives the domain from this frame's records
 constexpr int32_t kDomPrev = INT32_MIN;
 
+__device__ __forceinline__ uint32_t job_hw(const Job &s) {
+    return s.i | (s.length << 8) | (s.phase << 16) | (s.lab << 18) | (s.rok ? 1u << 21 : 0u) |
+           (s.shift ? 1u << 22 : 0u) | (s.k << 25);
+}
+__device__ __forceinline__ void job_unhw(Job &s, uint32_t hw) {
+    s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = (hw >> 16) & 3u;
+    s.lab = (hw >> 18) & 7u; s.rok = (hw >> 21) & 1u; s.shift = (hw >> 22) & 1u; s.k = (hw >> 25) & 7u;
+}
 // A job waiting for its light segment's Visibility (phase 1) only needs HDR and F.
 __device__ __forceinline__ void job_store(const ReuseArgs &A, uint32_t jid, const Job &s) {
     const size_t n = A.njobs;
     float4 *st = A.jstate;
     if (PTX_JOB_FRESH && s.i == 1u && s.phase == 0u && s.dom != kDomPrev) {  // fresh: 48 B (see above)
-        st[JS_HDR * n + jid] = make_float4(asf(1u | (s.length << 8) | kJobFresh), asf((uint32_t)s.dom), asf(s.idx),
+        st[JS_HDR * n + jid] = make_float4(asf(job_hw(s) | kJobFresh), asf((uint32_t)s.dom), asf(s.idx),
                                            asf((uint32_t)s.ref));
         st[JS_F * n + jid] = make_float4(s.rr_f.x, s.rr_f.y, s.rr_f.z, s.prod);
         st[JS_RRF * n + jid] = make_float4(s.beta, s.rr_p, 0.0f, 0.0f);
         return;
     }
-    st[JS_HDR * n + jid] = make_float4(asf(s.i | (s.length << 8) | (s.phase << 16)), asf(s.seed1), asf(s.idx),
-                                       asf((uint32_t)s.ref));
+    st[JS_HDR * n + jid] = make_float4(asf(job_hw(s)), asf(s.seed1), asf(s.idx), asf((uint32_t)s.ref));
     st[JS_F * n + jid] = make_float4(s.f.x, s.f.y, s.f.z, s.prod);
-    if (s.phase != 0u) return;
+    if (s.phase == 1u) return;
     st[JS_CUR * n + jid] = make_float4(s.cur.pos.x, s.cur.pos.y, s.cur.pos.z, asf(s.matref));
     st[JS_NRM * n + jid] = make_float4(s.cur.nrm.x, s.cur.nrm.y, s.cur.nrm.z, s.beta);
     st[JS_PREV * n + jid] = make_float4(s.prev.x, s.prev.y, s.prev.z, s.rr_p);
@@ -91,7 +105,7 @@ __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, ui
     const float4 *st = A.jstate;
     const float4 hd = st[JS_HDR * n + jid], fv = st[JS_F * n + jid];
     const uint32_t hw = asu(hd.x);
-    s.i = hw & 0xffu; s.length = (hw >> 8) & 0xffu; s.phase = (hw >> 16) & 0xffu;
+    job_unhw(s, hw);
     s.idx = asu(hd.z); s.ref = (int32_t)asu(hd.w);
     if (hw & kJobFresh) {  // the fresh layout: gather what it leaves out (same bits)
         const float4 rf = st[JS_RRF * n + jid];
@@ -107,7 +121,7 @@ __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, ui
     }
     s.seed1 = asu(hd.y);
     s.f = mk(fv.x, fv.y, fv.z); s.prod = fv.w;
-    if (s.phase != 0u) return;
+    if (s.phase == 1u) return;
     const float4 cu = st[JS_CUR * n + jid], nr = st[JS_NRM * n + jid];
     const float4 pv = st[JS_PREV * n + jid], rf = st[JS_RRF * n + jid];
     s.matref = asu(cu.w);
@@ -131,11 +145,14 @@ __device__ __forceinline__ bool rr_step(Job &s, const Surface &X, f3 L, f3 fv, f
     return ok;
 }
 
-// A fresh job: sample `ref` (length >= 2) replayed from the domain's camera point x0 and
-// primary-hit surface X1 (flat material index matref).
+// A fresh job: sample `ref` (length >= 2, reconnection index k) in the domain of camera point x0
+// and primary-hit surface X1 (flat material index matref); shift: a shift into that domain (the
+// hybrid shift at k, else random replay, either keeping the sample's label), else the sample at
+// home (its own PT_1 path, replayed).
 __device__ __forceinline__ void job_init(Job &s, f3 x0, const Surface &X1, uint32_t matref, int32_t ref,
-                                         uint32_t length, uint32_t seed1, int32_t dom) {
+                                         uint32_t length, uint32_t seed1, int32_t dom, uint32_t k, bool shift) {
     s.i = 1u; s.length = length; s.phase = 0u; s.seed1 = seed1; s.idx = 0u; s.ref = ref; s.dom = dom;
+    s.k = min(k, 7u); s.lab = 0u; s.shift = shift; s.rok = false;
     s.f = mk(1.0f, 1.0f, 1.0f); s.prod = 1.0f;
     s.prev = x0;
     s.cur = X1;
@@ -147,17 +164,45 @@ __device__ __forceinline__ void job_init(Job &s, f3 x0, const Surface &X1, uint3
 __device__ __forceinline__ bool job_begin(const Scene &sc, const ReuseArgs &A, Job &s, uint32_t x, uint32_t y,
                                           int32_t dom, int32_t ref) {
     const uint4 *rv = res_at(A.cur, ref);
-    const uint32_t C = rv[7].y, length = rv[5].w;
+    const uint4 r5 = rv[5];
+    const uint32_t C = rv[7].y, length = r5.w;
     Surface X1;
     uint32_t matref;
     if (C == 0u || length < 2u || !surf_load(sc, A.surf, dom, X1, matref)) return false;
-    job_init(s, x0_of(sc, x, y), X1, matref, ref, length, rv[0].y, dom);
+    job_init(s, x0_of(sc, x, y), X1, matref, ref, length, rv[0].y, dom, r5.x & 0xffu, false);
     return true;
 }
+// The hybrid shift (oracle eval_sample): a sample whose reconnection index k lies in [2, length-1]
+// reconnects its shifted prefix y_{k-1} to its stored x_k; `hyb` also selects that sample's
+// measure q = (prod_{i <= k-2} pdf_i * d^2 / |n_k . w|) / beta.
+__device__ __forceinline__ bool job_hyb(const Job &s) { return s.k >= 2u && s.k < s.length; }
+// IsSafeToReconnect (PT_1:1262-1271) of the edge (a, b), each end's rough bit under its lobe given
+// (min(ra, rb) >= R of the oracle's safe_edge: the roughnesses are finite)
+__device__ __forceinline__ bool rough_under(const Surface &X, uint32_t lobe) {
+    return (lobe == LOBE_LAMBERT ? 1.0f : X.mat.rough) >= RECONNECTION_ROUGHNESS;
+}
+__device__ __forceinline__ bool safe_edge(bool ra, bool rb, f3 a, f3 b) {
+    return length(a - b) >= RECONNECTION_DISTANCE && ra && rb;
+}
+// the area -> solid angle factor of the reconnection edge prev -> Xk (oracle: d2 / ck)
+__device__ __forceinline__ float rc_geo(f3 prev, const Surface &Xk) {
+    const f3 dv = Xk.pos - prev;
+    const float d2 = dot(dv, dv);
+    const float ck = fabsf(dot(Xk.nrm, dv / __builtin_sqrtf(d2)));
+    return d2 / ck;
+}
+// x_{k+1} of a sample: reservoir words 0..3 in the reuse layout, PT_1's pad words 24..27 otherwise
+__device__ __forceinline__ uint4 rc_next(const uint4 *rv, uint32_t w20) {
+    return (w20 & kResReuseLayout) ? rv[0] : rv[6];
+}
 
-// The job's next ray: a regenerated BSDF direction (PT_4:1367-1381) or the light
-// segment's Visibility (PT_4:1323-1333).  Called by every lane of the wave; `emit` selects
-// the lanes with a live job.  Returns whether the job continues (else its result is out).
+// The job's next ray: a regenerated BSDF direction (PT_4:1367-1381), the hybrid shift's
+// connection y_{k-1} -> x_k (a closest-hit query: nothing may lie between), or the light
+// segment's Visibility (PT_4:1323-1333).  A shift job tracks the shifted path's
+// SafeReconnectionIndex on the way (the first safe edge, `lab`; each vertex's rough bit under its
+// lobe, `rok`, once that lobe is known) and is invalid unless it equals the sample's k (oracle
+// path_label).  Called by every lane of the wave; `emit` selects the lanes with a live job.
+// Returns whether the job continues (else its result is out).
 // seed0: word 0 of the sample's reservoir (its first replayed draw's seed), read when s.i == 1.
 __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const ReuseArgs &A, bool emit, Job &s,
                                          uint32_t jid, uint32_t seed0) {
@@ -167,23 +212,58 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
     if (emit) {
         const uint4 *rv = res_of(A, s.ref);
         const f3 V = normalize(s.prev - s.cur.pos);
+        const bool hyb = job_hyb(s);
         bool ok = true;
-        if (s.i + 1u < s.length) {
+        if (s.shift && hyb && s.i + 1u == s.k) {  // y_{k-1}: the connection to the stored x_k
+            const uint4 r4 = rv[4], r5 = rv[5];
+            const Surface Xk = get_surface(sc, gdecode(r4));
+            const bool rk1 = rough_under(s.cur, r5.y), rk = rough_under(Xk, r5.z);
+            if (s.i >= 2u && s.lab == 0u && safe_edge(s.rok, rk1, s.prev, s.cur.pos)) s.lab = s.i;
+            if (s.lab == 0u && safe_edge(rk1, rk, s.cur.pos, Xk.pos)) s.lab = s.k;
+            ok = s.lab == s.k;
+            const f3 dv = Xk.pos - s.cur.pos;
+            const float dist = length(dv);
+            const f3 dir = dv / dist;
+            if (ok) {
+                float pdf;
+                const f3 fv = bsdf_pdf(s.cur, V, dir, pdf);
+                ok = rr_step(s, s.cur, dir, fv, pdf);
+            }
+            s.phase = 2u;
+            o = s.cur.pos; d = dir;
+        } else if (s.i + 1u < s.length) {
             uint32_t seed = s.i == 1u ? seed0 : s.seed1, lobe;
             const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
             float pdf;
             const f3 fv = bsdf_pdf(s.cur, V, dir, pdf);
-            s.prod *= pdf;
+            if (!hyb || s.i + 2u <= s.k) s.prod *= pdf;  // (hybrid: the replayed prefix only)
             ok = rr_step(s, s.cur, dir, fv, pdf);
+            if (s.shift) {
+                const bool rl = rough_under(s.cur, lobe);
+                if (s.i >= 2u && s.lab == 0u && safe_edge(s.rok, rl, s.prev, s.cur.pos)) s.lab = s.i;
+                s.rok = rl;
+            }
             s.phase = 0u;
             o = s.cur.pos; d = dir;
         } else {
             const LightSample XL = load_xl(rv);
+            if (s.shift && !hyb) {  // random replay: the label of the whole path (the last vertex's lobe:
+                                   // NEE Lambert, an env escape's stored Lobe_{k-1} when k = length)
+                const uint32_t ll = XL.type == LIGHT_ENV ? (s.k == s.length ? rv[5].y : LOBE_GGX) : LOBE_LAMBERT;
+                const bool rl = rough_under(s.cur, ll);
+                if (s.i >= 2u && s.lab == 0u && safe_edge(s.rok, rl, s.prev, s.cur.pos)) s.lab = s.i;
+                if (s.lab == 0u) {
+                    const bool rough = s.cur.mat.rough >= RECONNECTION_ROUGHNESS;
+                    const bool dirl = XL.type == LIGHT_DIRECTION || XL.type == LIGHT_ENV;
+                    if ((dirl || length(s.cur.pos - XL.pos) >= RECONNECTION_DISTANCE) && rough) s.lab = s.length;
+                }
+                ok = s.lab == s.k;
+            }
             const f3 L = direction_to_light(s.cur, XL);
             if (XL.type == LIGHT_ENV) {
                 float pdf;
                 const f3 fv = bsdf_pdf(s.cur, V, L, pdf);
-                ok = rr_step(s, s.cur, L, fv, pdf);
+                ok = rr_step(s, s.cur, L, fv, pdf) && ok;
             }
             s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
             float gl = 1.0f;
@@ -192,7 +272,7 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
                 const f3 Ld = normalize(r);
                 gl = fabsf(dot(get_light(sc, (uint32_t)XL.id).dir, Ld)) / dot(r, r);
             }
-            s.prod = s.prod / (gl * s.beta);  // q
+            s.prod = hyb ? s.prod / s.beta : s.prod / (gl * s.beta);  // q
             Le = l_emit<true>(XL, s.cur);
             s.phase = 1u;
             const float dist = length(XL.pos - s.cur.pos);
@@ -218,9 +298,9 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
 __device__ __forceinline__ void job_finish(const Seg &g, const JobLists &JL, const ReuseArgs &A, bool live,
                                            const Job &s, uint32_t jid) {
     if (live) job_store(A, jid, s);
-    const bool fold = live && A.fold_last && s.phase != 0u;
+    const bool fold = live && A.fold_last && s.phase == 1u;
     if (fold) A.jres[jid] = make_float4(asf(s.idx), asf(g.out_sel), 0.0f, asf(kJobPending));
-    job_keep(g, JL, live && !fold, live && s.phase != 0u, jid);
+    job_keep(g, JL, live && !fold, live && s.phase == 1u, jid);
 }
 
 #ifndef JOB_STEP_WAVES
@@ -254,11 +334,49 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
                     const f3 V = normalize(s.prev - s.cur.pos);
                     const f3 L = normalize(next.pos - s.cur.pos);
                     s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+                    if (!s.shift && job_hyb(s) && s.i + 1u == s.k) s.prod = s.prod * rc_geo(s.cur.pos, next);
                     s.prev = s.cur.pos;
                     s.cur = next;
                     s.matref = mat_index(sc, h.s.inst, h.s.mat);
                     s.i += 1u;
                     emit = true;
+                }
+            } else if (s.phase == 2u) {  // the connection's closest hit: nothing before x_k?
+                const Hit h = get_hit(g.res_in, s.idx);
+                const uint4 *rv = res_of(A, s.ref);
+                const uint4 r4 = rv[4], r5 = rv[5];
+                const Compact ck = gdecode(r4);
+                const Surface Xk = get_surface(sc, ck);
+                const float dist = length(Xk.pos - s.cur.pos);
+                if (h.valid && h.t < dist * 0.999f) {
+                    A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // occluded: no such shifted path
+                } else {
+                    const f3 V = normalize(s.prev - s.cur.pos);
+                    const f3 L = normalize(Xk.pos - s.cur.pos);
+                    s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+                    s.prod = s.prod * rc_geo(s.cur.pos, Xk);
+                    s.prev = s.cur.pos;
+                    s.cur = Xk;
+                    s.matref = mat_index(sc, ck.inst, ck.mat);
+                    s.i = s.k;
+                    if (s.k + 1u < s.length) {  // the kept vertex after x_k: no trace
+                        const Compact cn = gdecode(rc_next(rv, r5.x));
+                        const Surface Xn = get_surface(sc, cn);
+                        const f3 V2 = normalize(s.prev - s.cur.pos);
+                        const f3 L2 = normalize(Xn.pos - s.cur.pos);
+                        float pdf;
+                        const f3 fv = bsdf_pdf(s.cur, V2, L2, pdf);
+                        const bool rr = rr_step(s, s.cur, L2, fv, pdf);
+                        s.f = s.f * (bsdf(s.cur, L2, V2) * fabsf(dot(s.cur.nrm, L2)));
+                        s.prev = s.cur.pos;
+                        s.cur = Xn;
+                        s.matref = mat_index(sc, cn.inst, cn.mat);
+                        s.i += 1u;
+                        if (!rr) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        emit = rr;
+                    } else {
+                        emit = true;
+                    }
                 }
             } else {  // the light segment's Visibility arrived
                 const float4 a = g.res_in[2u * s.idx];
@@ -310,7 +428,13 @@ __device__ __forceinline__ SelF stored_f(const uint4 *r) {
 __device__ __forceinline__ void write_reused(uint4 *out, const uint4 *src, float p_sel, float q_sel, SelF fs,
                                              float w_sum, uint32_t C) {
     // all loads before the stores: src may be out itself (temporal)
-    const uint4 a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], a4 = src[4], a5 = src[5];
+    uint4 a0 = src[0], a5 = src[5];
+    const uint4 a1 = src[1], a2 = src[2], a3 = src[3], a4 = src[4];
+    if (fs.known && !(a5.x & kResReuseLayout)) {  // a PT_1 sample: into the reuse layout (oracle write_reused)
+        const uint32_t k = a5.x & 0xffu;
+        if (k >= 2u && k + 1u < a5.w) a0 = src[6];  // x_{k+1} over seeds the hybrid shift never replays
+        a5.x |= kResReuseLayout;
+    }
     out[0] = a0; out[1] = a1; out[2] = a2; out[3] = a3; out[4] = a4; out[5] = a5;
     out[6] = make_uint4(asu(p_sel), asu(q_sel), fs.known ? asu(fs.f.x) : 0u, fs.known ? asu(fs.f.y) : 0u);
     out[7] = make_uint4(asu(p_sel > 0.0f ? w_sum / p_sel : 0.0f), C, fs.known ? asu(fs.f.z) : 0u, fs.known ? 1u : 0u);
@@ -318,9 +442,13 @@ __device__ __forceinline__ void write_reused(uint4 *out, const uint4 *src, float
 
 // The spatial pass's 16-byte neighbour summary of a reservoir (see wnbr_summary below).
 constexpr uint32_t kNbrEscape = 0xFFFFFFFFu;
+// word w: valid << 31 | length << 27 | k << 23 | C (r5 = words 20..23: {k | layout, -, -, length});
+// a length or k past 15 or a C past 2^23 - 2 takes the escape
 __device__ __forceinline__ uint4 nbr_pack(bool valid, uint4 r5, uint4 r6, uint4 r7) {
     uint32_t w = 0u;
-    if (valid) w = (r5.w > 0x7fu || r7.y > 0xfffffeu) ? kNbrEscape : (1u << 31) | (r5.w << 24) | r7.y;
+    const uint32_t k = r5.x & 0xffu;
+    if (valid)
+        w = (r5.w > 0xfu || k > 0xfu || r7.y > 0x7ffffeu) ? kNbrEscape : (1u << 31) | (r5.w << 27) | (k << 23) | r7.y;
     return make_uint4(r6.x, r6.y, r7.x, w);
 }
 
@@ -334,13 +462,14 @@ __device__ __forceinline__ uint4 nbr_pack(bool valid, uint4 r5, uint4 r6, uint4 
 __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBufs &w, const ReuseArgs &A, Job &s,
                                                    uint32_t pix, uint32_t jid) {
     const uint4 *rv = res_at(A.cur, s.ref);
+    const bool hyb = job_hyb(s);
     while (s.i + 1u < s.length) {
         f3 V = normalize(s.prev - s.cur.pos);
         uint32_t seed = s.i == 1u ? rv[0].x : s.seed1, lobe;
         const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
         float pdf;
         const f3 fv = bsdf_pdf(s.cur, V, dir, pdf);
-        s.prod *= pdf;
+        if (!hyb || s.i + 2u <= s.k) s.prod *= pdf;
         if (!rr_step(s, s.cur, dir, fv, pdf)) {
             A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             return false;
@@ -350,6 +479,7 @@ __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBu
         V = normalize(s.prev - s.cur.pos);
         const f3 L = normalize(next.pos - s.cur.pos);
         s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
+        if (hyb && s.i + 1u == s.k) s.prod = s.prod * rc_geo(s.cur.pos, next);
         s.prev = s.cur.pos;
         s.cur = next;
         s.i += 1u;
@@ -366,7 +496,7 @@ __device__ __forceinline__ bool temporal_from_init(const Scene &sc, const WaveBu
         const f3 Ld = normalize(r);
         gl = fabsf(dot(get_light(sc, (uint32_t)XL.id).dir, Ld)) / dot(r, r);
     }
-    s.prod = s.prod / (gl * s.beta);
+    s.prod = hyb ? s.prod / s.beta : s.prod / (gl * s.beta);
     const f3 Le = l_emit<true>(XL, s.cur);
     s.f = s.f * (Le * T);
     const float qv = s.prod;
@@ -434,7 +564,7 @@ __global__ __launch_bounds__(WB) void wtemporal_combine(Scene sc, WaveBufs w, Re
         write_reused(rv, from_hist ? hv : rv, p_sel, q_sel, from_hist ? stored_f(hv) : job_f(er), w_sum, 1u + Cp);
         // the spatial pass's summary of the output (words 23, 24, 25, 28, 29 as written above)
         const float W = p_sel > 0.0f ? w_sum / p_sel : 0.0f;
-        A.nbr_out[pix] = nbr_pack(true, make_uint4(0u, 0u, 0u, from_hist ? h5.w : r5.w),
+        A.nbr_out[pix] = nbr_pack(true, make_uint4(from_hist ? h5.x : r5.x, 0u, 0u, from_hist ? h5.w : r5.w),
                                   make_uint4(asu(p_sel), asu(q_sel), 0u, 0u), make_uint4(asu(W), 1u + Cp, 0u, 0u));
     }
 }
@@ -518,7 +648,8 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
             valid = surf_load(sc, A.surf, pix, X1, mref);
         }
         const uint4 *rv = A.cur + 8u * (size_t)pix;
-        const uint32_t cC = valid ? rv[7].y : 0u, clen = valid ? rv[5].w : 0u;
+        const uint4 r5c = valid ? rv[5] : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t cC = valid ? rv[7].y : 0u, clen = r5c.w, ck = r5c.x & 0xffu;
         const bool canon = valid && cC != 0u && clen >= 2u;
         const bool count = (A.motion_slots & 2u) != 0u;  // (once per pixel: with slot 1)
         const MotionHist mh = valid ? motion_hist(sc, A, X1, y, count) : MotionHist{false, 0, 0u, 0u, 0u};
@@ -540,7 +671,8 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
                     const uint4 h0 = hv[0], h5 = hv[5], h6 = hv[6];
                     act = h5.w >= 2u && asf(h6.x) > 0.0f;
                     if (act) {
-                        job_init(s, x0_of(sc, x, y), X1, mref, kHistRef + mh.pp, h5.w, h0.y, (int32_t)pix);
+                        job_init(s, x0_of(sc, x, y), X1, mref, kHistRef + mh.pp, h5.w, h0.y, (int32_t)pix, h5.x & 0xffu,
+                                 true);
                         s0 = h0.x;
                     }
                 }
@@ -550,7 +682,7 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 uint32_t pref;
                 act = surf_load(sc, A.psurf, mh.pp, Xp, pref);
                 if (act) {
-                    job_init(s, x0_prev(A, sc, mh.px, mh.py), Xp, pref, (int32_t)pix, clen, rv[0].y, kDomPrev);
+                    job_init(s, x0_prev(A, sc, mh.px, mh.py), Xp, pref, (int32_t)pix, clen, rv[0].y, kDomPrev, ck, true);
                     s0 = rv[0].x;
                 }
             }
@@ -589,10 +721,11 @@ __global__ __launch_bounds__(WB) void wtmotion_combine(Scene sc, WaveBufs w, Reu
         // forward: the history sample shifted here
         float wh = 0.0f, pf = 0.0f, qf = 0.0f;
         SelF ff{false, mk(0.0f, 0.0f, 0.0f)};
-        uint32_t hlen = 0u;
+        uint32_t hlen = 0u, hk = 0u;
         if (Cp != 0u) {
             const uint4 h5 = hv[5], h6 = hv[6], h7 = hv[7];
             hlen = h5.w;
+            hk = h5.x;
             const float ph = asf(h6.x), qh = asf(h6.y), Wh = asf(h7.x);
             if (h5.w >= 2u && ph > 0.0f) {
                 const float4 Fr = job_at(A, w, pix, 1u);
@@ -626,7 +759,7 @@ __global__ __launch_bounds__(WB) void wtmotion_combine(Scene sc, WaveBufs w, Reu
         if (wrs_update(w_sum, wh, seed)) { from_hist = true; p_sel = pf; q_sel = qf; }
         write_reused(rv, from_hist ? hv : rv, p_sel, q_sel, from_hist ? ff : job_f(er), w_sum, 1u + Cp);
         const float Wo = p_sel > 0.0f ? w_sum / p_sel : 0.0f;
-        A.nbr_out[pix] = nbr_pack(true, make_uint4(0u, 0u, 0u, from_hist ? hlen : r5.w),
+        A.nbr_out[pix] = nbr_pack(true, make_uint4(from_hist ? hk : r5.x, 0u, 0u, from_hist ? hlen : r5.w),
                                   make_uint4(asu(p_sel), asu(q_sel), 0u, 0u), make_uint4(asu(Wo), 1u + Cp, 0u, 0u));
     }
 }
@@ -654,14 +787,17 @@ __device__ __forceinline__ int32_t band_index(const Scene &sc, uint32_t x, uint3
 // spatial jobs start): {p_hat (word 24), q (25), W (28), G-buffer valid << 31 | length << 24 |
 // C}, or w = kNbrEscape when length or C does not fit (then read the reservoir itself).  A
 // neighbour costs one 16-byte gather instead of a G-buffer line and a reservoir line.
-struct Nbr { bool valid; uint32_t length, C; float p, q, W; };
+struct Nbr { bool valid; uint32_t length, C; float p, q, W; uint32_t k; };
+__device__ __forceinline__ Nbr nbr_unpack(uint4 v) {
+    return Nbr{(v.w >> 31) != 0u, (v.w >> 27) & 0xfu, v.w & 0x7fffffu, asf(v.x), asf(v.y), asf(v.z), (v.w >> 23) & 0xfu};
+}
 __device__ __forceinline__ Nbr nbr_at(const ReuseArgs &A, int32_t idx) {
     const uint4 v = A.nbr[idx];
     if (v.w != kNbrEscape)
-        return Nbr{(v.w >> 31) != 0u, (v.w >> 24) & 0x7fu, v.w & 0xffffffu, asf(v.x), asf(v.y), asf(v.z)};
+        return nbr_unpack(v);
     const uint4 *rv = res_at(A.cur, idx);
     const uint4 r5 = rv[5], r6 = rv[6], r7 = rv[7];
-    return Nbr{gdecode(A.gbuf[idx]).valid != 0u, r5.w, r7.y, asf(r6.x), asf(r6.y), asf(r7.x)};
+    return Nbr{gdecode(A.gbuf[idx]).valid != 0u, r5.w, r7.y, asf(r6.x), asf(r6.y), asf(r7.x), r5.x & 0xffu};
 }
 __global__ __launch_bounds__(WB) void wnbr_summary(Scene sc, const uint4 *gbuf, const uint4 *res, uint4 *nbr,
                                                    uint4 *surf, size_t npx) {
@@ -721,7 +857,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
         Surface X1{};
         f3 x0{};
         uint4 c0 = make_uint4(0u, 0u, 0u, 0u);
-        uint32_t clen = 0u;
+        uint32_t clen = 0u, ck = 0u;
         if (q < np && tile_xy(sc, q, x, y)) {
             pix = (y - sc.row_begin) * sc.width + x;
             seed = reuse_seed(sc, x, y, SALT_SPATIAL);
@@ -733,7 +869,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 const uint4 *rc = A.cur + 8u * (size_t)pix;  // this pixel's sample, shifted to each neighbour
                 const uint4 r5 = rc[5];
                 canon = valid && rc[7].y != 0u && r5.w >= 2u && asf(rc[6].x) > 0.0f;
-                if (canon) { c0 = rc[0]; clen = r5.w; }
+                if (canon) { c0 = rc[0]; clen = r5.w; ck = r5.x & 0xffu; }
             }
         }
         // every neighbour's offset first, then its summary + seeds (forward) or surface record
@@ -783,12 +919,10 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                 nx = pxy & 0xffffu; ny = pxy >> 16;
                 bool want = false;
                 if (present && !backward) {  // the neighbour's sample in this pixel's domain
-                    const Nbr nb = a.w != kNbrEscape ? Nbr{(a.w >> 31) != 0u, (a.w >> 24) & 0x7fu, a.w & 0xffffffu,
-                                                           asf(a.x), asf(a.y), asf(a.z)}
-                                                     : nbr_at(A, ni);
+                    const Nbr nb = a.w != kNbrEscape ? nbr_unpack(a) : nbr_at(A, ni);
                     want = nb.valid && nb.length >= 2u && nb.p > 0.0f;
                     act = want && nb.C != 0u;
-                    if (act) { job_init(s, x0, X1, mref, ni, nb.length, b.y, (int32_t)pix); s0 = b.x; }
+                    if (act) { job_init(s, x0, X1, mref, ni, nb.length, b.y, (int32_t)pix, nb.k, true); s0 = b.x; }
                 } else if (present && canon) {  // this pixel's sample in the neighbour's domain
                     want = act = a.w != kNoSurface;
                     if (act) {
@@ -796,7 +930,7 @@ void wspatial_start(Scene sc, WaveBufs w, ReuseArgs A) {
                         Xn.pos = mk(asf(a.x), asf(a.y), asf(a.z));
                         Xn.nrm = mk(asf(b.x), asf(b.y), asf(b.z));
                         Xn.mat = material_at(sc, a.w);
-                        job_init(s, x0_of(sc, nx, ny), Xn, a.w, (int32_t)pix, clen, c0.y, ni);
+                        job_init(s, x0_of(sc, nx, ny), Xn, a.w, (int32_t)pix, clen, c0.y, ni, ck, true);
                         s0 = c0.x;
                     }
                 }
@@ -881,9 +1015,7 @@ __device__ __forceinline__ void combine_pixel(const Scene &sc, const ReuseArgs &
         Nbr nb[MT];
 #pragma unroll
         for (uint32_t m = 0; m < MT; ++m) {
-            nb[m] = nv[m].w != kNbrEscape ? Nbr{(nv[m].w >> 31) != 0u, (nv[m].w >> 24) & 0x7fu, nv[m].w & 0xffffffu,
-                                                asf(nv[m].x), asf(nv[m].y), asf(nv[m].z)}
-                                          : nbr_at(A, nid[m]);
+            nb[m] = nv[m].w != kNbrEscape ? nbr_unpack(nv[m]) : nbr_at(A, nid[m]);
             if (!pres[m]) nb[m].valid = false;
         }
 #pragma unroll
@@ -976,9 +1108,7 @@ __global__ __launch_bounds__(WB) void wspatial_combine_shfl(Scene sc, WaveBufs w
             const uint4 nv = A.nbr[nid];
             Fr = job_at(A, w, pix, 2u * m);
             B = job_at(A, w, pix, 2u * m + 1u);
-            nb = nv.w != kNbrEscape ? Nbr{(nv.w >> 31) != 0u, (nv.w >> 24) & 0x7fu, nv.w & 0xffffffu, asf(nv.x),
-                                          asf(nv.y), asf(nv.z)}
-                                    : nbr_at(A, nid);
+            nb = nv.w != kNbrEscape ? nbr_unpack(nv) : nbr_at(A, nid);
             if (!pres) nb.valid = false;
         }
         const float Q = nb.valid ? canon_q(c, Mf, nb.C, B) : 1.0f;

@@ -581,8 +581,11 @@ struct WInit {
 __device__ __forceinline__ uint32_t lobe_of(uint32_t flags, uint32_t k) { return (flags >> (8u + 2u * (k - 1u))) & 3u; }
 
 // CompressPath for the candidate (vertex i, NEE or env) -- same rules as ptx_persist.hip.
+// rcnext (the reuse pipeline): x_{k+1}'s compact in pad words 24..27 when the hybrid shift keeps
+// a vertex after x_k (k = 2, length 4: x3), as the oracle's compress_path.
 __device__ __forceinline__ void wcompress(const Scene &sc, const WInit &s, const float4 *state, uint32_t npix,
-                                          uint32_t pix, bool is_env, const LightSample &XL, uint4 *out) {
+                                          uint32_t pix, bool is_env, const LightSample &XL, uint4 *out,
+                                          bool rcnext) {
     const uint32_t i = s.i, length = i + 1u;
     const uint32_t L1 = (i > 1u || is_env) ? lobe_of(s.flags, 1u) : 0u;
     const uint32_t L2 = (i > 2u || (is_env && i == 2u)) ? lobe_of(s.flags, 2u) : 0u;
@@ -623,7 +626,12 @@ __device__ __forceinline__ void wcompress(const Scene &sc, const WInit &s, const
     out[3] = make_uint4(asu(XL.Le.x), asu(XL.Le.y), asu(XL.Le.z), asu(XL.pdf));
     out[4] = rc;
     out[5] = make_uint4(k, lk1, lk, length);
-    out[6] = make_uint4(0u, 0u, 0u, 0u);
+    uint4 nx = make_uint4(0u, 0u, 0u, 0u);
+    if (rcnext && k == 2u && length == 4u) {
+        const float4 c = state[IS_CS3 * npix + pix];
+        nx = make_uint4(asu(c.x), asu(c.y), asu(c.z), asu(c.w));
+    }
+    out[6] = nx;
 }
 
 // Vertex i of the path tree up to (not including) its traces (PT_1:1403-1442): NEE sample,
@@ -796,7 +804,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                          : ls.type == LIGHT_POINT  ? normalize(s.xpos - ls.pos)
                          : ls.type == LIGHT_RECT   ? normalize(s.xpos - s.xlpos)
                                                    : mk(0.0f, 0.0f, 0.0f);
-                wcompress(sc, s, state, npix, pix, false, XL, reservoir + 8u * (size_t)pix);
+                wcompress(sc, s, state, npix, pix, false, XL, reservoir + 8u * (size_t)pix, w.surf != nullptr);
             }
             if (!(s.flags & F_BSDF)) {
                 winit_finish(s, reservoir, pix);  // i == 3 or Russian roulette ended the path
@@ -819,7 +827,7 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                         env.id = -1;
                         env.Le = mk(ENV_C, ENV_C, ENV_C);
                         env.pdf = s.pdf_env;
-                        wcompress(sc, s, state, npix, pix, true, env, reservoir + 8u * (size_t)pix);
+                        wcompress(sc, s, state, npix, pix, true, env, reservoir + 8u * (size_t)pix, w.surf != nullptr);
                     }
                     winit_finish(s, reservoir, pix);
                 } else {  // 2b. next vertex (PT_1:1464-1468)
