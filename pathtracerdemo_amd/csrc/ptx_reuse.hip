@@ -206,7 +206,7 @@ __device__ __forceinline__ uint4 rc_next(const uint4 *rv, uint32_t w20) {
 // seed0: word 0 of the sample's reservoir (its first replayed draw's seed), read when s.i == 1.
 __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const ReuseArgs &A, bool emit, Job &s,
                                          uint32_t jid, uint32_t seed0) {
-    bool ray = false, vis = false;
+    bool ray = false, vis = false, go = false;
     f3 o = mk(0.0f, 0.0f, 0.0f), d = o, Le = o;
     float remain = -1.0f;
     if (emit) {
@@ -214,37 +214,42 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
         const f3 V = normalize(s.prev - s.cur.pos);
         const bool hyb = job_hyb(s);
         bool ok = true;
-        if (s.shift && hyb && s.i + 1u == s.k) {  // y_{k-1}: the connection to the stored x_k
-            const uint4 r4 = rv[4], r5 = rv[5];
-            const Surface Xk = get_surface(sc, gdecode(r4));
-            const bool rk1 = rough_under(s.cur, r5.y), rk = rough_under(Xk, r5.z);
-            if (s.i >= 2u && s.lab == 0u && safe_edge(s.rok, rk1, s.prev, s.cur.pos)) s.lab = s.i;
-            if (s.lab == 0u && safe_edge(rk1, rk, s.cur.pos, Xk.pos)) s.lab = s.k;
-            ok = s.lab == s.k;
-            const f3 dv = Xk.pos - s.cur.pos;
-            const float dist = length(dv);
-            const f3 dir = dv / dist;
-            if (ok) {
-                float pdf;
-                const f3 fv = bsdf_pdf(s.cur, V, dir, pdf);
-                ok = rr_step(s, s.cur, dir, fv, pdf);
+        if (s.i + 1u < s.length) {
+            // the direction out of the current vertex: to the stored x_k from y_{k-1} (conn, the
+            // connection ray follows), to the kept x_{k+1} from x_k (fixd, no ray: the next step
+            // takes the vertex), or a regenerated BSDF sample
+            const bool conn = s.shift && hyb && s.i + 1u == s.k;
+            const bool fixd = s.shift && hyb && s.i == s.k;  // (then k + 1 < length)
+            f3 dir;
+            uint32_t lobe = LOBE_LAMBERT;
+            if (conn || fixd) {
+                const uint4 r5 = rv[5];
+                const Surface Xt = get_surface(sc, gdecode(conn ? rv[4] : rc_next(rv, r5.x)));
+                if (conn) {  // the shifted path's label: edges (k-2, k-1) and (k-1, k)
+                    const bool rk1 = rough_under(s.cur, r5.y), rk = rough_under(Xt, r5.z);
+                    if (s.i >= 2u && s.lab == 0u && safe_edge(s.rok, rk1, s.prev, s.cur.pos)) s.lab = s.i;
+                    if (s.lab == 0u && safe_edge(rk1, rk, s.cur.pos, Xt.pos)) s.lab = s.k;
+                    ok = s.lab == s.k;
+                }
+                const f3 dv = Xt.pos - s.cur.pos;
+                dir = dv / length(dv);
+            } else {
+                uint32_t seed = s.i == 1u ? seed0 : s.seed1;
+                dir = sample_bsdf(seed, s.cur, V, lobe);
             }
-            s.phase = 2u;
-            o = s.cur.pos; d = dir;
-        } else if (s.i + 1u < s.length) {
-            uint32_t seed = s.i == 1u ? seed0 : s.seed1, lobe;
-            const f3 dir = sample_bsdf(seed, s.cur, V, lobe);
             float pdf;
             const f3 fv = bsdf_pdf(s.cur, V, dir, pdf);
-            if (!hyb || s.i + 2u <= s.k) s.prod *= pdf;  // (hybrid: the replayed prefix only)
-            ok = rr_step(s, s.cur, dir, fv, pdf);
-            if (s.shift) {
+            if (!conn && !fixd && (!hyb || s.i + 2u <= s.k)) s.prod *= pdf;  // (hybrid: the replayed prefix only)
+            ok = rr_step(s, s.cur, dir, fv, pdf) && ok;
+            if (s.shift && !conn && !fixd) {
                 const bool rl = rough_under(s.cur, lobe);
                 if (s.i >= 2u && s.lab == 0u && safe_edge(s.rok, rl, s.prev, s.cur.pos)) s.lab = s.i;
                 s.rok = rl;
             }
-            s.phase = 0u;
+            s.phase = conn ? 2u : (fixd ? 3u : 0u);
             o = s.cur.pos; d = dir;
+            ray = ok && !fixd;
+            go = ok;
         } else {
             const LightSample XL = load_xl(rv);
             if (s.shift && !hyb) {  // random replay: the label of the whole path (the last vertex's lobe:
@@ -278,9 +283,9 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
             const float dist = length(XL.pos - s.cur.pos);
             o = s.cur.pos; d = (XL.pos - s.cur.pos) / dist; remain = dist;
             vis = true;
+            ray = go = ok;
         }
-        if (ok) ray = true;
-        else A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // PT_1 would have ended such a path
+        if (!go) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // PT_1 would have ended such a path
     }
     const uint32_t idx = g.rbase + wave_alloc(g.l_ray, ray ? 1u : 0u);
     if (ray) {
@@ -288,7 +293,7 @@ __device__ __forceinline__ bool job_emit(const Scene &sc, const Seg &g, const Re
         put_ray(g.rays, idx, o, d, remain, vis ? Q_VIS : Q_CLOSEST);
         if (vis) g.res_out[2u * idx] = make_float4(0.0f, Le.x, Le.y, Le.z);
     }
-    return ray;
+    return go;
 }
 
 // After job_emit: store a live job's state and queue it for the next step -- except a job whose
@@ -304,10 +309,12 @@ __device__ __forceinline__ void job_finish(const Seg &g, const JobLists &JL, con
 }
 
 #ifndef JOB_STEP_WAVES
-// 5 waves per SIMD (96 VGPRs, 80 B/lane spilled) beside the 5-wave flattened trace: reuse 464.6
-// vs 461.8 at 4 (3 reps, tools/cl/js5_ab.sh); every start / step kernel at 5 (LOGIC_WAVES):
-// reuse +1.0 %, but ReSTIR -3.2 %, TEST_MCPT -10 % (tools/cl/lw5_ab.sh)
-#define JOB_STEP_WAVES 5
+// 4 waves per SIMD since the hybrid shift (round 5): its connection / kept-vertex arrivals spill
+// 160 B/lane at 96 VGPRs -- reuse 467.4 vs 460.1 at 5 (2 reps, tools/cl/r5_hyb4.sh).  Before it, 5
+// (96 VGPRs, 80 B/lane spilled) beside the 5-wave flattened trace: 464.6 vs 461.8 at 4
+// (tools/cl/js5_ab.sh); every start / step kernel at 5 (LOGIC_WAVES): reuse +1.0 %, but ReSTIR
+// -3.2 %, TEST_MCPT -10 % (tools/cl/lw5_ab.sh)
+#define JOB_STEP_WAVES 4
 #endif
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(JOB_STEP_WAVES, 8)))
 void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
@@ -325,58 +332,41 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
         if (q < n) {
             jid = split_at(g, JL, q, nh);
             job_load(sc, A, jid, s);
-            if (s.phase == 0u) {  // regenerated vertex i+1 arrived (PT_4:1378-1380)
-                const Hit h = get_hit(g.res_in, s.idx);
-                if (!h.valid) {
-                    A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // the replayed path escapes here
+            if (s.phase != 1u) {  // the next vertex: a regenerated BSDF ray's hit (PT_4:1378-1380), or the
+                                  // hybrid shift's x_k once its connection is clear / its kept x_{k+1}
+                bool ok = true;
+                Surface next;
+                uint32_t nref = 0u;
+                if (s.phase == 0u) {
+                    const Hit h = get_hit(g.res_in, s.idx);
+                    ok = h.valid;  // (else the replayed path escapes here)
+                    if (ok) {
+                        next = surface_at(sc, h.s, h.pos);
+                        nref = mat_index(sc, h.s.inst, h.s.mat);
+                    }
                 } else {
-                    const Surface next = surface_at(sc, h.s, h.pos);
+                    const uint4 *rv = res_of(A, s.ref);
+                    const Compact cc = gdecode(s.phase == 2u ? rv[4] : rc_next(rv, rv[5].x));
+                    next = get_surface(sc, cc);
+                    nref = mat_index(sc, cc.inst, cc.mat);
+                    if (s.phase == 2u) {  // nothing between y_{k-1} and x_k
+                        const Hit h = get_hit(g.res_in, s.idx);
+                        ok = !(h.valid && h.t < length(next.pos - s.cur.pos) * 0.999f);
+                    }
+                }
+                if (!ok) {
+                    A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                } else {
                     const f3 V = normalize(s.prev - s.cur.pos);
                     const f3 L = normalize(next.pos - s.cur.pos);
                     s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
-                    if (!s.shift && job_hyb(s) && s.i + 1u == s.k) s.prod = s.prod * rc_geo(s.cur.pos, next);
+                    if (s.phase == 2u || (!s.shift && job_hyb(s) && s.i + 1u == s.k))  // arriving at x_k
+                        s.prod = s.prod * rc_geo(s.cur.pos, next);
                     s.prev = s.cur.pos;
                     s.cur = next;
-                    s.matref = mat_index(sc, h.s.inst, h.s.mat);
+                    s.matref = nref;
                     s.i += 1u;
                     emit = true;
-                }
-            } else if (s.phase == 2u) {  // the connection's closest hit: nothing before x_k?
-                const Hit h = get_hit(g.res_in, s.idx);
-                const uint4 *rv = res_of(A, s.ref);
-                const uint4 r4 = rv[4], r5 = rv[5];
-                const Compact ck = gdecode(r4);
-                const Surface Xk = get_surface(sc, ck);
-                const float dist = length(Xk.pos - s.cur.pos);
-                if (h.valid && h.t < dist * 0.999f) {
-                    A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // occluded: no such shifted path
-                } else {
-                    const f3 V = normalize(s.prev - s.cur.pos);
-                    const f3 L = normalize(Xk.pos - s.cur.pos);
-                    s.f = s.f * (bsdf(s.cur, L, V) * fabsf(dot(s.cur.nrm, L)));
-                    s.prod = s.prod * rc_geo(s.cur.pos, Xk);
-                    s.prev = s.cur.pos;
-                    s.cur = Xk;
-                    s.matref = mat_index(sc, ck.inst, ck.mat);
-                    s.i = s.k;
-                    if (s.k + 1u < s.length) {  // the kept vertex after x_k: no trace
-                        const Compact cn = gdecode(rc_next(rv, r5.x));
-                        const Surface Xn = get_surface(sc, cn);
-                        const f3 V2 = normalize(s.prev - s.cur.pos);
-                        const f3 L2 = normalize(Xn.pos - s.cur.pos);
-                        float pdf;
-                        const f3 fv = bsdf_pdf(s.cur, V2, L2, pdf);
-                        const bool rr = rr_step(s, s.cur, L2, fv, pdf);
-                        s.f = s.f * (bsdf(s.cur, L2, V2) * fabsf(dot(s.cur.nrm, L2)));
-                        s.prev = s.cur.pos;
-                        s.cur = Xn;
-                        s.matref = mat_index(sc, cn.inst, cn.mat);
-                        s.i += 1u;
-                        if (!rr) A.jres[jid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        emit = rr;
-                    } else {
-                        emit = true;
-                    }
                 }
             } else {  // the light segment's Visibility arrived
                 const float4 a = g.res_in[2u * s.idx];
