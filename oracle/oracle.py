@@ -83,6 +83,8 @@ def lib(variant: str = ""):
                                     ctypes.c_int, ctypes.c_int, P, P, P, P, P, ctypes.POINTER(ReuseParams),
                                     ctypes.POINTER(Counters)]
         _lib.pto_run_gi.restype = ctypes.c_int
+        _lib.pto_run_gi_temporal_motion.argtypes = _lib.pto_run_temporal_motion.argtypes
+        _lib.pto_run_gi_temporal_motion.restype = ctypes.c_int
         _lib.pto_gi_shift.argtypes = [ctypes.POINTER(Inputs), P, ctypes.c_uint32, ctypes.c_uint32, P, P]
         _lib.pto_gi_sample_dir.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_uint32), P]
         _lib.pto_gi_sample_dir.restype = ctypes.c_float
@@ -260,12 +262,39 @@ class Frame:
         self.counters[("gi", pass_id)] = cnt.as_dict()
         return self.counters[("gi", pass_id)]
 
+    def run_gi_temporal_motion(self, threads: int = 0, rect=None) -> dict:
+        """GI temporal reuse with the history at each pixel's reprojection in the previous frame
+        (prev_uniform, prev_gbuffer; pt_oracle_gi.c gi_temporal_motion_pixel)."""
+        threads = threads or os.cpu_count() or 1
+        x0, y0, x1, y1 = rect if rect is not None else (0, 0, self.W, self.H)
+        r, m, cap = self.reuse
+        prm = ReuseParams(r, m, cap, 1 if self.hist_valid else 0)
+        cnt = Counters()
+        rc = lib(self.variant).pto_run_gi_temporal_motion(threads, ctypes.byref(self._inputs()), x0, y0, x1, y1,
+                                                         _ptr(self.gbuffer), _ptr(self.gi_res), _ptr(self.gi_hist),
+                                                         _ptr(self.prev_uniform), _ptr(self.prev_gbuffer),
+                                                         ctypes.byref(prm), ctypes.byref(cnt))
+        if rc != 0:
+            raise RuntimeError(f"oracle GI motion temporal pass failed ({rc})")
+        self.counters["gi_temporal_motion"] = cnt.as_dict()
+        return self.counters["gi_temporal_motion"]
+
     def run_gi_frame(self, threads: int = 0, rect=None) -> None:
-        """One ReSTIR GI frame: G-buffer -> GI init -> temporal -> spatial -> shade."""
+        """One ReSTIR GI frame: G-buffer -> GI init -> temporal -> spatial -> shade.  As in
+        run_reuse_frame, a camera moved since the history's frame reprojects the history
+        (run_gi_temporal_motion)."""
+        moved = self.hist_valid and self.camera_moved()
         self.run(PASS_GBUFFER, threads, rect)
-        for p in (GI_PASS_INIT, GI_PASS_TEMPORAL, GI_PASS_SPATIAL, GI_PASS_FINAL):
+        self.run_gi(GI_PASS_INIT, threads, rect)
+        if moved:
+            self.run_gi_temporal_motion(threads, rect)
+        else:
+            self.run_gi(GI_PASS_TEMPORAL, threads, rect)
+        for p in (GI_PASS_SPATIAL, GI_PASS_FINAL):
             self.run_gi(p, threads, rect)
         self.hist_valid = True
+        self.prev_uniform = self.uniform.copy()
+        self.prev_gbuffer[...] = self.gbuffer
 
     def gi_shift(self, x: int, y: int, s: np.ndarray):
         """The GI reconnection shift of reservoir `s` (16 words) into pixel (x, y):

@@ -1378,10 +1378,23 @@ static int motion_valid(const surface *Sp, v3 x0p, v3 P, v3 Nc) {
     return fabsf(dp - dc) <= 0.05f * dc;
 }
 
+/* The history of pixel (x, y) under camera motion (DI and GI): its primary hit S1 reprojected to p'
+ * = (px, py) in the previous frame, with that frame's hit x1p there passing the disocclusion test;
+ * 0 if none (the rules above) */
+static int motion_lookup(const ctx *c, const ctx *cprev, const float *vp_prev, const surface *S1, uint32_t y,
+                         const uint32_t *gbuffer_prev, uint32_t radius, uint32_t *px, uint32_t *py, compact *x1p) {
+    const uint32_t W = c->U[U_W], H = c->U[U_H];
+    if (!reproject(vp_prev, S1->pos, W, H, px, py) || !motion_rows(*py, y, radius)) return 0;
+    *x1p = decode_compact(gbuffer_prev + 4u * (*py * W + *px));
+    if (!x1p->valid) return 0;
+    const surface Sp = get_surface(c, *x1p);
+    return motion_valid(&Sp, get_x0(cprev, *px, *py), S1->pos, S1->nrm);
+}
+
 static void temporal_motion_pixel(const ctx *c, const ctx *cprev, const float *vp_prev, const uint32_t *gbuffer,
                                   uint32_t *cur, const uint32_t *hist_all, const uint32_t *gbuffer_prev,
                                   const pto_reuse_params *prm, uint32_t x, uint32_t y) {
-    const uint32_t W = c->U[U_W], H = c->U[U_H];
+    const uint32_t W = c->U[U_W];
     compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
     if (!x1.valid) return; /* PT_1 wrote the zero reservoir; PT_4 never reads it */
     uint32_t seed = reuse_seed(c, x, y, SALT_TEMPORAL);
@@ -1394,15 +1407,9 @@ static void temporal_motion_pixel(const ctx *c, const ctx *cprev, const float *v
     const uint32_t *h = NULL;
     if (prm->hist_valid) {
         const surface S1 = get_surface(c, x1);
-        if (reproject(vp_prev, S1.pos, W, H, &px, &py) && motion_rows(py, y, prm->radius)) {
-            x1p = decode_compact(gbuffer_prev + 4u * (py * W + px));
-            if (x1p.valid) {
-                const surface Sp = get_surface(c, x1p);
-                if (motion_valid(&Sp, get_x0(cprev, px, py), S1.pos, S1.nrm)) {
-                    h = hist_all + PTO_RESERVOIR_WORDS * (py * W + px);
-                    Cp = h[29] < prm->temporal_cap ? h[29] : prm->temporal_cap;
-                }
-            }
+        if (motion_lookup(c, cprev, vp_prev, &S1, y, gbuffer_prev, prm->radius, &px, &py, &x1p)) {
+            h = hist_all + PTO_RESERVOIR_WORDS * (py * W + px);
+            Cp = h[29] < prm->temporal_cap ? h[29] : prm->temporal_cap;
         }
     }
     const float cp = (float)Cp;

@@ -126,6 +126,13 @@ float pto_gi_sample_dir(const float n[3], const float mat[7], const float v[3], 
 int pto_run_gi(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, const uint32_t *gbuffer,
                uint32_t *res_cur, uint32_t *res_hist, float *direct, float *accum, const pto_reuse_params *prm,
                pto_counters *cnt);
+/* GI temporal reuse under camera motion (pt_oracle_gi.c gi_temporal_motion_pixel): res_cur in/out,
+ * res_hist = the previous frame's spatial output, rendered with prev_uniform over gbuffer_prev */
+#define PTO_GI_PASS_TEMPORAL_MOTION 13
+int pto_run_gi_temporal_motion(int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                               const uint32_t *gbuffer, uint32_t *res_cur, const uint32_t *res_hist,
+                               const uint32_t *prev_uniform, const uint32_t *gbuffer_prev,
+                               const pto_reuse_params *prm, pto_counters *cnt);
 
 /* Closest-hit queries, same record formats as ptx_trace (include/ptx.h):
  * rays n x 8 f32 {o, d.x | d.y, d.z, -, -}; hits n x 8 {t, flags|inst|mat, prim, bu, bv, pos}.

@@ -201,6 +201,72 @@ static void gi_temporal_pixel(const ctx *c, const uint32_t *gbuffer, uint32_t *c
     gi_write(cur, src, gi_v3(src + 12), f32_of(src[15]), w_sum, 1u + Cp);
 }
 
+/* Temporal GI reuse under camera motion (round 5; the DI pass's rules, temporal_motion_pixel in
+ * pt_oracle.c): the history lives at the reprojection p' of the pixel's primary hit in the
+ * previous frame's domain (its camera point x0' and hit x1'), so it is the spatial pass's pairwise
+ * rule with M = 1 -- the history sample shifted here (gi_shift, one occlusion ray, J = q_h / q_here)
+ * and the canonical sample shifted into the previous domain for its own weight; c_c = 1,
+ * c_h = min(C_hist, cap); canonical draw first, then the history. */
+static void gi_temporal_motion_pixel(const ctx *c, const ctx *cprev, const float *vp_prev, const uint32_t *gbuffer,
+                                     uint32_t *cur, const uint32_t *hist_all, const uint32_t *gbuffer_prev,
+                                     const pto_reuse_params *prm, uint32_t x, uint32_t y) {
+    const uint32_t W = c->U[U_W];
+    const compact x1 = decode_compact(gbuffer + 4u * (y * W + x));
+    if (!x1.valid) return;
+    uint32_t seed = reuse_seed(c, x, y, SALT_GI_TEMPORAL);
+    const v3 fc = gi_v3(cur + 12);
+    const float cc = 1.0f, pc = luminance(fc), qc = f32_of(cur[15]), Wc = f32_of(cur[7]);
+    const int canon_ok = cur[11] != 0u && pc > 0.0f;
+    uint32_t Cp = 0u, px = 0u, py = 0u;
+    compact x1p = {0u, 0u, 0u, 0u, 0.0f, 0.0f};
+    const uint32_t *h = NULL;
+    if (prm->hist_valid) {
+        const surface S1 = get_surface(c, x1);
+        if (motion_lookup(c, cprev, vp_prev, &S1, y, gbuffer_prev, prm->radius, &px, &py, &x1p)) {
+            h = hist_all + PTO_GI_WORDS * (py * W + px);
+            Cp = h[11] < prm->temporal_cap ? h[11] : prm->temporal_cap;
+        }
+    }
+    const float cp = (float)Cp;
+    /* forward: the history sample in this pixel's domain */
+    float wh = 0.0f, qf = 0.0f;
+    v3 ff = V3(0.0f, 0.0f, 0.0f);
+    if (Cp != 0u && luminance(gi_v3(h + 12)) > 0.0f) {
+        const float ph = luminance(gi_v3(h + 12)), qh = f32_of(h[15]), Wh = f32_of(h[7]);
+        v3 F;
+        float qF;
+        if (gi_shift(c, x, y, x1, h, &F, &qF)) {
+            const float pF = luminance(F);
+            const float J = qh / qF;
+            const float pb = ph / J;
+            const float den = cc * pF + cp * pb;
+            const float m = den > 0.0f ? (cp * pb) / den : 0.0f;
+            wh = m * pF * Wh * J;
+            ff = F;
+            qf = qF;
+        }
+    }
+    /* backward: this pixel's sample in the previous domain (its weight) */
+    float Q = 1.0f;
+    if (canon_ok && Cp != 0u) {
+        v3 B;
+        float qB;
+        if (gi_shift(cprev, px, py, x1p, cur, &B, &qB)) {
+            const float pbc = luminance(B) * qc / qB;
+            const float den = cc * pc + cp * pbc;
+            Q = den > 0.0f ? (cc * pc) / den : 1.0f;
+        }
+    }
+    const float wc = canon_ok ? Q * pc * Wc : 0.0f;
+    float w_sum = 0.0f;
+    const uint32_t *src = cur;
+    v3 fsel = fc;
+    float qsel = qc;
+    if (wrs_update(&w_sum, wc, &seed)) { src = cur; fsel = fc; qsel = qc; }
+    if (wrs_update(&w_sum, wh, &seed)) { src = h; fsel = ff; qsel = qf; }
+    gi_write(cur, src, fsel, qsel, w_sum, 1u + Cp);
+}
+
 /* Spatial GI reuse with pairwise MIS (the rule of spatial_pixel, pt_oracle.c), the shift
  * being gi_shift: forward = neighbour sample into this pixel, backward = this pixel's
  * sample into the neighbour. */
@@ -331,6 +397,25 @@ void pto_gi_final(const pto_inputs *in, const uint32_t *gbuffer, const uint32_t 
         }
 }
 
+void pto_gi_temporal_motion(const pto_inputs *in, const pto_motion *mot, const uint32_t *gbuffer, uint32_t *res_cur,
+                            const uint32_t *res_hist, const pto_reuse_params *prm, int x0, int y0, int x1, int y1,
+                            pto_counters *cnt) {
+    ctx c, cprev;
+    ctx_init(&c, in, EPS_INIT, cnt);
+    pto_inputs pin = *in;
+    pin.uniform = mot->prev_uniform;
+    ctx_init(&cprev, &pin, EPS_INIT, cnt);
+    float vp_prev[16];
+    pto_mat4_inverse((const float *)(mot->prev_uniform + U_VPINV), vp_prev);
+    const uint32_t W = c.U[U_W];
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            const uint32_t p = (uint32_t)y * W + (uint32_t)x;
+            gi_temporal_motion_pixel(&c, &cprev, vp_prev, gbuffer, res_cur + PTO_GI_WORDS * p, res_hist,
+                                     mot->gbuffer_prev, prm, (uint32_t)x, (uint32_t)y);
+        }
+}
+
 /* Test helper: gi_shift of GI reservoir `s` into pixel (x, y); out = {valid, f.rgb, q}. */
 void pto_gi_shift(const pto_inputs *in, const uint32_t *gbuffer, uint32_t x, uint32_t y, const uint32_t *s,
                   float out[5]) {
@@ -351,6 +436,7 @@ typedef struct gi_job {
     float *direct, *accum;
     const pto_reuse_params *prm;
     pto_counters cnt;
+    const pto_motion *mot;
 } gi_job;
 
 static void *gi_worker(void *arg) {
@@ -361,23 +447,44 @@ static void *gi_worker(void *arg) {
         case PTO_GI_PASS_TEMPORAL: pto_gi_temporal(j->in, j->gbuffer, j->res_cur, j->res_hist, j->prm, j->x0, y, j->x1, y + 1); break;
         case PTO_GI_PASS_SPATIAL: pto_gi_spatial(j->in, j->gbuffer, j->res_cur, j->res_hist, j->prm, j->x0, y, j->x1, y + 1, &j->cnt); break;
         case PTO_GI_PASS_FINAL: pto_gi_final(j->in, j->gbuffer, j->res_hist, j->direct, j->x0, y, j->x1, y + 1, j->accum); break;
+        case PTO_GI_PASS_TEMPORAL_MOTION:
+            pto_gi_temporal_motion(j->in, j->mot, j->gbuffer, j->res_cur, j->res_hist, j->prm, j->x0, y, j->x1, y + 1,
+                                   &j->cnt);
+            break;
         default: break;
         }
     }
     return NULL;
 }
 
+static int run_gi_m(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                    const uint32_t *gbuffer, uint32_t *res_cur, uint32_t *res_hist, float *direct, float *accum,
+                    const pto_reuse_params *prm, pto_counters *cnt, const pto_motion *mot);
 int pto_run_gi(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1, const uint32_t *gbuffer,
                uint32_t *res_cur, uint32_t *res_hist, float *direct, float *accum, const pto_reuse_params *prm,
                pto_counters *cnt) {
     if (pass < PTO_GI_PASS_INIT || pass > PTO_GI_PASS_FINAL || !prm || prm->neighbors > 16u) return -2;
+    return run_gi_m(pass, nthreads, in, x0, y0, x1, y1, gbuffer, res_cur, res_hist, direct, accum, prm, cnt, NULL);
+}
+int pto_run_gi_temporal_motion(int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                               const uint32_t *gbuffer, uint32_t *res_cur, const uint32_t *res_hist,
+                               const uint32_t *prev_uniform, const uint32_t *gbuffer_prev,
+                               const pto_reuse_params *prm, pto_counters *cnt) {
+    if (!prm || !prev_uniform || !gbuffer_prev) return -2;
+    pto_motion mot = {prev_uniform, gbuffer_prev};
+    return run_gi_m(PTO_GI_PASS_TEMPORAL_MOTION, nthreads, in, x0, y0, x1, y1, gbuffer, res_cur, (uint32_t *)res_hist,
+                    NULL, NULL, prm, cnt, &mot);
+}
+static int run_gi_m(int pass, int nthreads, const pto_inputs *in, int x0, int y0, int x1, int y1,
+                    const uint32_t *gbuffer, uint32_t *res_cur, uint32_t *res_hist, float *direct, float *accum,
+                    const pto_reuse_params *prm, pto_counters *cnt, const pto_motion *mot) {
     if (nthreads < 1) nthreads = 1;
     gi_job *jobs = (gi_job *)calloc((size_t)nthreads, sizeof(gi_job));
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     if (!jobs || !th) { free(jobs); free(th); return -1; }
     for (int t = 0; t < nthreads; ++t) {
         gi_job j = {pass, t, nthreads, x0, y0, x1, y1, in, gbuffer, res_cur, res_hist, direct, accum, prm,
-                    {0, 0, 0, 0, 0}};
+                    {0, 0, 0, 0, 0}, mot};
         jobs[t] = j;
         if (nthreads > 1) pthread_create(&th[t], NULL, gi_worker, &jobs[t]);
     }
