@@ -527,9 +527,11 @@ static void event_end(TimedLaunch *t, hipStream_t st) {
 static size_t px_with_halo(const ptx_handle *h) {
     return (size_t)(h->halo_top + h->band_h + h->halo_bot) * h->cfg.width;
 }
+// GI job words per pixel: the spatial pass's 2 per neighbour, the motion pass's kGiMotionSlots
+static uint32_t gi_job_slots(const ptx_handle *h) { return std::max(2u * h->reuse_neighbors, kGiMotionSlots); }
 int reuse_buffers(ptx_handle *h) {
     const size_t njobs = (size_t)h->band_h * h->cfg.width *
-                         (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI ? 2u * h->reuse_neighbors : reuse_jobs_per_px(h));
+                         (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI ? gi_job_slots(h) : reuse_jobs_per_px(h));
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) return alloc_buf(h, h->d_jres, njobs * 4u);  // ray index per job
     if (int rc = alloc_buf(h, h->d_jstate, njobs * 6u * 16u)) return rc;
     if (int rc = alloc_buf(h, h->d_nbr, px_with_halo(h) * 16u)) return rc;
@@ -604,7 +606,7 @@ static ReuseArgs motion_args(ptx_handle *h, int pass) {
     return A;
 }
 
-static GiArgs gi_args(ptx_handle *h) {
+static GiArgs gi_args(ptx_handle *h, bool motion) {
     GiArgs A{};
     A.gbuf = gbuf_band(h);
     A.cur = res_band(h);
@@ -618,10 +620,20 @@ static GiArgs gi_args(ptx_handle *h) {
     static const bool planes = ab_knob("GI_JOB_PLANES", 1) != 0;
     A.jpx = planes ? 1u : A.jpp;
     A.jslot = planes ? h->band_h * h->cfg.width : 1u;
+    if (!planes && motion) A.jpx = gi_job_slots(h);
     A.radius = h->reuse_radius;
     A.neighbors = h->reuse_neighbors;
     A.cap = h->temporal_cap;
-    A.hist_valid = h->hist_valid ? 1u : 0u;
+    // (a moved camera's history is only usable through the motion pass)
+    A.hist_valid = h->hist_valid && (motion || !h->hist_moved) ? 1u : 0u;
+    if (motion) {  // the previous frame's camera and G-buffer (motion_prepare), as motion_args
+        std::memcpy(A.vpinv_prev, h->hist_camera, sizeof A.vpinv_prev);
+        mat4_inverse(A.vpinv_prev, A.vp_prev);
+        A.pgbuf = (const uint4 *)h->d_psurf.p + (size_t)h->halo_top * h->cfg.width;
+        A.prev_row_lo = -(int32_t)h->halo_top;
+        A.prev_row_hi = (int32_t)(h->band_h + h->halo_bot);
+        A.clip = (unsigned long long *)h->d_counters.p + CNT_MOTION_CLIP;
+    }
     return A;
 }
 
@@ -634,13 +646,14 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
     if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {
         // GI passes: init = 3 logic rounds around 2 traces, spatial = start, trace, combine,
         // temporal / final = one per-pixel launch
-        const GiArgs A = gi_args(h);
-        const int gp = pass == PTX_PASS_INIT ? 0 : pass == PTX_PASS_TEMPORAL ? 1 : pass == PTX_PASS_SPATIAL ? 2 : 3;
-        const int rounds = gp == 0 ? kWaveRoundsGiInit : gp == 2 ? kWaveRoundsGiSpatial : 0;
+        const bool motion = is_motion_pass(pass);
+        const GiArgs A = gi_args(h, motion);
+        const int gp = motion ? 4 : pass == PTX_PASS_INIT ? 0 : pass == PTX_PASS_TEMPORAL ? 1 : pass == PTX_PASS_SPATIAL ? 2 : 3;
+        const int rounds = gp == 0 ? kWaveRoundsGiInit : gp == 2 || gp == 4 ? kWaveRoundsGiSpatial : 0;
         for (int r = 0; e == hipSuccess && r <= rounds; ++r) {
             if (r > 0) {
                 TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
-                e = wave_trace(sc, w, r - 1, 1, h->stack_depth, st, gp == 2);  // spatial: occlusion only
+                e = wave_trace(sc, w, r - 1, 1, h->stack_depth, st, gp >= 2);  // spatial / motion: occlusion only
                 event_end(t, st);
                 if (e != hipSuccess) break;
             }
@@ -993,8 +1006,14 @@ void mat4_inverse(const float *mf, float *out) {
 // Before a moved-camera frame's passes: the previous frame's surface records -> d_psurf, on the
 // stream of that frame (`st`, ordered after its PT_1; a pipelined frame's next G-buffer on that
 // stream comes after the copy).  DI reuse handles (a band's halo rows included: that frame's
-// summaries wrote them from the exchanged G-buffer rows).
+// summaries wrote them from the exchanged G-buffer rows); GI handles copy the G-buffer itself
+// (halo rows included: that frame's exchange).
 int motion_prepare(ptx_handle *h, hipStream_t st) {
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {
+        if (int rc = alloc_buf(h, h->d_psurf, h->d_gbuf.bytes)) return rc;
+        HIP_CHECK(h, hipMemcpyAsync(h->d_psurf.p, h->d_gbuf.p, h->d_gbuf.bytes, hipMemcpyDeviceToDevice, st));
+        return PTX_OK;
+    }
     if (!h->d_surf.p) {  // (no surface records yet: nothing to reproject)
         h->hist_valid = false;
         h->hist_moved = false;
@@ -1157,7 +1176,7 @@ static int timed_wave_frame(ptx_handle *h) {
     // shortening the chain; so PTX_AB=MOTION_SPLIT=1 (A/B) selects the split, the default runs
     // the whole pass after the wait.
     static const bool msplit_on = ab_knob("MOTION_SPLIT", 0) != 0;
-    bool moved = h->hist_valid && h->hist_moved && has_reuse(h) && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
+    bool moved = h->hist_valid && h->hist_moved && has_reuse(h);
     const bool msplit = moved && pipe && msplit_on && pipe_depth() == 2 && h->ev_surf_ok && h->d_surf.p;
     const DevBuf prev_surf = h->d_surf;  // (the previous frame's context, before the swap)
     if (moved && !msplit) {
@@ -1448,12 +1467,12 @@ int ptx_set_frame(ptx_handle *h, const uint32_t uniform[PTX_UNIFORM_WORDS]) {
     }
     std::memcpy(h->uniform, uniform, sizeof h->uniform);
     h->frame_set = true;
-    // temporal history: a DI reuse handle reprojects it when the camera moved (the motion
+    // temporal history: a reuse or GI handle reprojects it when the camera moved (the motion
     // temporal pass; a band through ptx_render with a communicator or ptx_render_bands, which
-    // bring the neighbours' rows of it); elsewhere it is reusable only for the camera that
-    // produced it (GI's temporal pass, and pass by pass: dropped)
+    // bring the neighbours' rows of it); pass by pass it is reusable only for the camera that
+    // produced it (reuse_args / gi_args)
     h->hist_moved = std::memcmp(h->hist_camera, uniform + 4, sizeof h->hist_camera) != 0;
-    if (h->hist_moved && h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) h->hist_valid = false;
+    if (h->hist_moved && !has_reuse(h)) h->hist_valid = false;
     if (h->scene_loaded && !h->layout_valid) return build_layout(h);
     return PTX_OK;
 }

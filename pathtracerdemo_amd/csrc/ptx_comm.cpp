@@ -215,8 +215,8 @@ BandSets band_sets(const ptx_handle *h, const WaveBufs &w) {
 // surface records, queues; shared: history, shift jobs, accumulation.  The previous frame's
 // sends read the other context's rows, and a context's next frame starts on its stream after
 // its back passes, which wait for that frame's exchange (ev_halo): nothing is overwritten in
-// flight.  A moved camera (DI reuse, history valid: `moved`) reprojects the history: the previous
-// frame's surface records are copied first (motion_prepare, before the context swap), and the
+// flight.  A moved camera (DI reuse or GI, history valid: `moved`) reprojects the history: the previous
+// frame's surface records (GI: G-buffer) are copied first (motion_prepare, before the context swap), and the
 // neighbours' rows of its spatial output arrive as the motion halo before the temporal pass.
 // ev_prev marks everything enqueued before this frame on the previous frame's stream (pipelined
 // or not: a neighbour's motion-halo copy waits for it).
@@ -227,7 +227,7 @@ BandSets band_sets(const ptx_handle *h, const WaveBufs &w) {
 // renders the frame without history (`moved` false), so no rank waits on a send its neighbour
 // never posts.
 bool motion_exchange(const ptx_handle *h) {
-    return h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && h->band_frames > 0 &&
+    return has_reuse(h) && h->band_frames > 0 &&
            std::memcmp(h->band_camera, h->uniform + 4, sizeof h->band_camera) != 0;
 }
 int band_prepare(ptx_handle *h, Scene &sc, WaveBufs &w, bool &pipe, bool &moved) {

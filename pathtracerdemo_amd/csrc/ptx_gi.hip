@@ -544,6 +544,159 @@ __global__ __launch_bounds__(WB) void wgis_combine(Scene sc, WaveBufs w, GiArgs 
     }
 }
 
+// ---------------------------------------------------------------- temporal, moved camera
+// The history of pixel p lives at the reprojection p' of its primary hit in the previous
+// frame, in that frame's domain (oracle gi_temporal_motion_pixel; the DI pass's lookup,
+// ptx_reuse.hip motion_hist, with the previous frame's G-buffer in place of its surface
+// records): the spatial pass's pairwise rule with M = 1 over two occlusion jobs -- slot 0 the
+// history sample shifted here, slot 1 this pixel's sample shifted to p' (its MIS weight).
+__device__ __forceinline__ f3 gi_x0_prev(const GiArgs &A, const Scene &sc, uint32_t x, uint32_t y) {
+    float u = ((float)x + 0.5f) / (float)sc.U[U_W];  // (x0_of with the previous frame's VP^-1)
+    float v = ((float)y + 0.5f) / (float)sc.U[U_H];
+    return xform_point(A.vpinv_prev, mk(2.0f * u - 1.0f, 2.0f * v - 1.0f, 0.0f));
+}
+struct GiMotion { bool ok; int32_t pp; uint32_t px, py, C; Compact x1p; };
+__device__ __forceinline__ GiMotion gi_motion(const Scene &sc, const GiArgs &A, const Surface &X1, uint32_t y) {
+    GiMotion m{false, 0, 0u, 0u, 0u, Compact{}};
+    if (!A.hist_valid) return m;
+    const float *vp = A.vp_prev;
+    const f3 P = X1.pos;
+    const float cx = ((vp[0] * P.x + vp[4] * P.y) + vp[8] * P.z) + vp[12];
+    const float cy = ((vp[1] * P.x + vp[5] * P.y) + vp[9] * P.z) + vp[13];
+    const float cw = ((vp[3] * P.x + vp[7] * P.y) + vp[11] * P.z) + vp[15];
+    if (!(cw > 0.0f)) return m;
+    const float W = (float)sc.width, H = (float)sc.height;
+    const float fx = ((cx / cw + 1.0f) * 0.5f) * W, fy = ((cy / cw + 1.0f) * 0.5f) * H;
+    if (!(fx >= 0.0f && fx < W && fy >= 0.0f && fy < H)) return m;
+    m.px = (uint32_t)fx;
+    m.py = (uint32_t)fy;
+    const int32_t ry = (int32_t)m.py - (int32_t)sc.row_begin;
+    if (abs((int32_t)m.py - (int32_t)y) > (int32_t)A.radius || ry < A.prev_row_lo || ry >= A.prev_row_hi) {
+        if (A.clip) atomicAdd(A.clip, 1ull);
+        return m;
+    }
+    m.pp = ry * (int32_t)sc.width + (int32_t)m.px;
+    m.x1p = gdecode(A.pgbuf[m.pp]);
+    if (!m.x1p.valid) return m;
+    const Surface Sp = get_surface(sc, m.x1p);
+    if (!(dot(Sp.nrm, X1.nrm) >= 0.9f)) return m;
+    const f3 x0p = gi_x0_prev(A, sc, m.px, m.py);
+    const float dp = length(Sp.pos - x0p), dc = length(P - x0p);
+    if (!(fabsf(dp - dc) <= 0.05f * dc)) return m;
+    m.C = min(A.hist[4 * (ptrdiff_t)m.pp + 2].w, A.cap);
+    m.ok = m.C != 0u;
+    return m;
+}
+
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(GIS_START_WAVES, 8)))
+void wgim_start(Scene sc, WaveBufs w, GiArgs A) {
+    __shared__ uint32_t lds[2];
+    const Seg g = seg_begin(w, 0u, lds);
+    const uint32_t np = padded_pixels(sc);
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {  // workgroup-uniform (wave_alloc below)
+        const uint32_t q = seg_pixel(w, g.j, k);
+        uint32_t x = 0u, y = 0u, pix = 0u;
+        Compact x1{};
+        if (q < np && tile_xy(sc, q, x, y)) {
+            pix = (y - sc.row_begin) * sc.width + x;
+            x1 = gdecode(A.gbuf[pix]);
+        }
+        const bool valid = x1.valid != 0u;
+        GiMotion mh{false, 0, 0u, 0u, 0u, Compact{}};
+        GiDomain D{};
+        if (valid) {
+            D.Y = get_surface(sc, x1);
+            mh = gi_motion(sc, A, D.Y, y);
+        }
+        for (uint32_t slot = 0; slot < 2u; ++slot) {
+            bool ray = false;
+            f3 f{}, o{}, dir{};
+            float qv = 0.0f, remain = 0.0f;
+            if (mh.ok && slot == 0u) {  // the history's sample in this pixel's domain
+                const uint4 *hs = A.hist + 4 * (ptrdiff_t)mh.pp;
+                if (luminance(ld3(hs[3])) > 0.0f) {
+                    D.Vy = normalize(x0_of(sc, x, y) - D.Y.pos);
+                    ray = gi_shift_begin(D, gi_sample(sc, hs), f, qv, o, dir, remain);
+                }
+            } else if (mh.ok) {  // this pixel's sample in the previous frame's domain at p'
+                const uint4 *rc = A.cur + 4u * (size_t)pix;
+                if (rc[2].w != 0u && luminance(ld3(rc[3])) > 0.0f) {
+                    GiDomain Dp;
+                    Dp.Y = get_surface(sc, mh.x1p);
+                    Dp.Vy = normalize(gi_x0_prev(A, sc, mh.px, mh.py) - Dp.Y.pos);
+                    ray = gi_shift_begin(Dp, gi_sample(sc, rc), f, qv, o, dir, remain);
+                }
+            }
+            const uint32_t idx = g.rbase + wave_alloc(g.l_ray, ray ? 1u : 0u);
+            if (ray) {
+                put_ray(g.rays, idx, o, dir, remain, Q_OCC);
+                g.res_out[2u * idx] = make_float4(0.0f, f.x, f.y, f.z);
+                g.res_out[2u * idx + 1u] = make_float4(qv, 0.0f, 0.0f, 0.0f);
+            }
+            if (valid) A.jray[gi_jid(A, pix, slot)] = ray ? idx : GI_NO_RAY;
+        }
+        if (valid) {
+            A.jray[gi_jid(A, pix, 2u)] = (uint32_t)mh.pp;
+            A.jray[gi_jid(A, pix, 3u)] = mh.ok ? mh.C : 0u;
+        }
+    }
+    seg_end(w, g);
+}
+
+__global__ __launch_bounds__(WB) void wgim_combine(Scene sc, WaveBufs w, GiArgs A) {
+    const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
+    const float4 *res = w.res[0];
+    for (uint32_t k = 0; k < w.seg_px; k += WB) {
+        const uint32_t q = seg_pixel(w, j, k);
+        uint32_t x, y;
+        if (q >= np || !tile_xy(sc, q, x, y)) continue;
+        const uint32_t pix = (y - sc.row_begin) * sc.width + x;
+        if (!gdecode(A.gbuf[pix]).valid) continue;
+        uint4 *cur = A.cur + 4u * (size_t)pix;
+        uint32_t seed = gi_seed(sc, x, y, SALT_GI_TEMPORAL);
+        const uint4 c1 = cur[1], c2 = cur[2], c3 = cur[3];
+        const f3 fc = ld3(c3);
+        const float pc = luminance(fc), qc = asf(c3.w), Wc = asf(c1.w);
+        const bool canon_ok = c2.w != 0u && pc > 0.0f;
+        const int32_t pp = (int32_t)A.jray[gi_jid(A, pix, 2u)];
+        const uint32_t Cp = A.jray[gi_jid(A, pix, 3u)];
+        const float cp = (float)Cp;
+        const uint4 *hs = A.hist + 4 * (ptrdiff_t)(Cp ? pp : 0);
+        float wh = 0.0f, qf = 0.0f;
+        f3 ff = mk(0.0f, 0.0f, 0.0f);
+        f3 F;
+        float qF;
+        if (Cp != 0u && gi_job(A, res, gi_jid(A, pix, 0u), F, qF)) {
+            const uint4 h1 = hs[1], h3 = hs[3];
+            const float ph = luminance(ld3(h3)), qh = asf(h3.w), Wh = asf(h1.w);
+            const float pF = luminance(F);
+            const float J = qh / qF;
+            const float pb = ph / J;
+            const float den = 1.0f * pF + cp * pb;
+            const float m = den > 0.0f ? (cp * pb) / den : 0.0f;
+            wh = m * pF * Wh * J;
+            ff = F;
+            qf = qF;
+        }
+        float Q = 1.0f;
+        f3 B;
+        float qB;
+        if (canon_ok && Cp != 0u && gi_job(A, res, gi_jid(A, pix, 1u), B, qB)) {
+            const float pbc = luminance(B) * qc / qB;
+            const float den = 1.0f * pc + cp * pbc;
+            Q = den > 0.0f ? (1.0f * pc) / den : 1.0f;
+        }
+        const float wc = canon_ok ? Q * pc * Wc : 0.0f;
+        float w_sum = 0.0f;
+        bool from_hist = false;
+        w_sum += wc;
+        if (rnd(seed) < wc / w_sum) from_hist = false;
+        w_sum += wh;
+        if (rnd(seed) < wh / w_sum) from_hist = true;
+        gi_write(cur, from_hist ? hs : cur, from_hist ? ff : fc, from_hist ? qf : qc, w_sum, 1u + Cp);
+    }
+}
+
 // ---------------------------------------------------------------- final
 __global__ __launch_bounds__(WB) void wgi_final(Scene sc, WaveBufs w, GiArgs A) {
     const uint32_t j = w.seg_base + blockIdx.x, np = padded_pixels(sc);
@@ -576,6 +729,10 @@ hipError_t wave_gi_round(const Scene &sc, const WaveBufs &w, int pass, int round
     case 2:  // spatial: rounds 0, 1
         if (round == 0) hipLaunchKernelGGL(wgis_start, grid, blk, 0, s, sc, w, A);
         else hipLaunchKernelGGL(wgis_combine, grid, blk, 0, s, sc, w, A);
+        break;
+    case 4:  // temporal under camera motion: rounds 0, 1
+        if (round == 0) hipLaunchKernelGGL(wgim_start, grid, blk, 0, s, sc, w, A);
+        else hipLaunchKernelGGL(wgim_combine, grid, blk, 0, s, sc, w, A);
         break;
     default: hipLaunchKernelGGL(wgi_final, grid, blk, 0, s, sc, w, A); break;
     }

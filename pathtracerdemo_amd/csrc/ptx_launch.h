@@ -183,7 +183,8 @@ hipError_t wave_reuse_summary(const Scene &sc, const uint4 *gbuf, const uint4 *r
 hipError_t wave_surface(const Scene &sc, const WaveBufs &w, const uint4 *gbuf, hipStream_t s);
 
 // ReSTIR GI (ptx_gi.hip; pipeline PTX_PIPELINE_RESTIR_GI): pass 0 init (logic rounds 0..2,
-// traces between), 1 temporal (one launch), 2 spatial (start, trace, combine), 3 final.
+// traces between), 1 temporal (one launch), 2 spatial (start, trace, combine), 3 final,
+// 4 temporal under camera motion (start, trace, combine).
 constexpr int kWaveRoundsGiInit = 2, kWaveRoundsGiSpatial = 1;
 constexpr uint32_t kGiResU4 = 4u;  // 64-byte GI reservoir (oracle/pt_oracle_gi.c)
 struct GiArgs {
@@ -197,7 +198,16 @@ struct GiArgs {
     uint32_t jpx, jslot;  // job (pixel, slot) at jray[pix * jpx + slot * jslot]: slot planes
                           // (jpx 1, jslot = band pixels) or pixel-major (jpx = jpp, jslot 1)
     uint32_t radius, neighbors, cap, hist_valid;
+    // temporal reuse under camera motion (pass 4; ReuseArgs' motion fields): the previous frame's
+    // VP^-1 and VP, its G-buffer (gbuf's addressing, rows [prev_row_lo, prev_row_hi) held:
+    // the band and its halo rows), history rows the same; a reprojection outside them counts in *clip.
+    // Jobs: slot 0 the history here, slot 1 this sample at p', slots 2 / 3 p' and its confidence.
+    float vpinv_prev[16], vp_prev[16];
+    const uint4 *pgbuf;
+    int32_t prev_row_lo, prev_row_hi;
+    unsigned long long *clip;
 };
+constexpr uint32_t kGiMotionSlots = 4u;
 hipError_t wave_gi_round(const Scene &sc, const WaveBufs &w, int pass, int round, const GiArgs &A, hipStream_t s);
 
 }  // namespace ptx

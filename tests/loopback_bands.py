@@ -65,8 +65,8 @@ def differs(a, b):
     return int(np.any(a != b, axis=-1).sum())
 
 
-def make(cs, W, H, R, a=0, b=0):
-    r = Renderer(W, H, device=0, pipeline="reuse", reuse_radius=R, row_begin=a, row_end=b)
+def make(cs, W, H, R, a=0, b=0, pipeline="reuse"):
+    r = Renderer(W, H, device=0, pipeline=pipeline, reuse_radius=R, row_begin=a, row_end=b)
     r.Initialize(cs)
     return r
 
@@ -112,6 +112,31 @@ def scenario_split(cs, out):
                     "clips_one": int(one.read_counters()["motion_clips"]),
                     "hist_used": float((one.read_reservoir()[..., 29] > 1).mean()),
                     "comm": [b.comm_info() for b in bands]}
+    for r in [one] + bands:
+        r.close()
+
+
+def scenario_gi_split(cs, out):
+    """ReSTIR GI as 3 communicator bands (R = 8) along PATH: the GI motion pass reads the motion
+    halo (previous spatial output) and the previous static halo (G-buffer rows)."""
+    W, H, R = 64, 96, 8
+    cuts = [0, 40, 70, 96]
+    one = make(cs, W, H, R, pipeline="gi")
+    bands = [make(cs, W, H, R, a, b, pipeline="gi") for a, b in zip(cuts, cuts[1:])]
+    connect(bands)
+    frames = []
+    for f, (loc, yaw, pitch) in enumerate(PATH, start=1):
+        pose(one, loc, yaw, pitch)
+        one.Render()
+        for b in bands:
+            pose(b, loc, yaw, pitch)
+        errs = run_threads([b.Render for b in bands])
+        assert not any(errs), errs
+        frames.append({"frame": f, **compare(one, bands)})
+    out["gi_split"] = {"frames": frames,
+                       "clips_bands": int(sum(b.read_counters()["motion_clips"] for b in bands)),
+                       "clips_one": int(one.read_counters()["motion_clips"]),
+                       "hist_used": float((one.read_reservoir()[..., 11] > 1).mean())}
     for r in [one] + bands:
         r.close()
 
@@ -174,6 +199,7 @@ def main():
     cs = compile_scene("c3_interior_32")
     out = {}
     scenario_split(cs, out)
+    scenario_gi_split(cs, out)
     scenario_reset_one_rank(cs, out)
     scenario_dead_peer(cs, out, stats)
     out["stub"] = dict(zip(["groups", "pairs", "bytes", "destroys", "aborts", "finalizes"], stats()))

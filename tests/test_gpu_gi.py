@@ -137,3 +137,49 @@ def test_full_hd_gi_window_bit_exact(scene3, oracle_mod):
     assert_same(r.read_image()[y0:y1], fr.accum[y0:y1], "radiance (window)")
     img = r.read_image()
     assert np.isfinite(img).all()
+
+
+# tests/test_gpu_bands.py's moving-camera path, then a pitch jump past the reuse radius
+GI_MOTION_PATH = [((0.0, 0.0, 6.0), 0.0, 0.0), ((0.083, 0.0, 6.0), 0.0, 0.0), ((0.166, 0.0, 5.95), 0.0, 0.0),
+                  ((0.25, 0.02, 5.9), 1.5, 0.0), ((0.25, 0.02, 5.9), 3.0, 0.0), ((0.2, 0.02, 5.85), 4.5, 0.0),
+                  ((0.2, 0.02, 5.85), 4.5, 0.0), ((0.12, 0.0, 5.8), 3.0, 9.0), ((0.12, 0.0, 5.8), 3.0, 9.0)]
+
+
+def gi_pose(r, loc, yaw, pitch):
+    c = r.GetCamera()
+    c.set_location(*loc)
+    c.set_yaw(yaw)
+    c.set_pitch(pitch)
+    r.Update()
+
+
+@pytest.mark.parametrize("scene,W,H,prm", [("scene3", 64, 48, (30, 3, 20)), ("scene1", 45, 38, (6, 2, 20)),
+                                           ("scene3", 80, 64, (8, 3, 5))])
+def test_gi_moving_camera_bit_exact(request, oracle_mod, scene, W, H, prm):
+    """GI temporal reuse under camera motion (wgim_start / wgim_combine: the history at the
+    reprojection of the primary hit, reconnection shifts both ways, pairwise MIS) along a moving
+    path with still frames and a pitch jump past the reuse radius: temporal output, spatial output
+    and radiance equal the oracle's (gi_temporal_motion_pixel) after every frame, and the
+    reprojected history carries most pixels on the moved frames."""
+    cs = request.getfixturevalue(scene)
+    O = oracle_mod
+    r = gi_renderer(cs, W, H, prm)
+    fr = oracle_frame(O, cs, W, H, prm)
+    used = []
+    for f, (loc, yaw, pitch) in enumerate(GI_MOTION_PATH, start=1):
+        gi_pose(r, loc, yaw, pitch)
+        moved = fr.hist_valid and bool(np.any(np.asarray(r.uniform)[4:23] != fr.prev_uniform[4:23]))
+        fr.set_camera(r.uniform)
+        fr.set_frame_index(int(r.uniform[23]))
+        fr.run_gi_frame(threads=8)
+        r.Render()
+        assert_same(r.read_reservoir(), fr.gi_res, f"temporal output, frame {f}")
+        assert_same(r.read_history(), fr.gi_hist, f"spatial output, frame {f}")
+        assert_same(r.read_image(), fr.accum, f"radiance, frame {f}")
+        if moved:
+            valid = (fr.gbuffer[..., 0] >> 31) == 1
+            used.append(float((fr.gi_res[..., 11][valid] > 1).mean()))
+    assert len(used) >= 5 and max(used) > 0.6, used
+    if (W, prm[0]) == (80, 8):  # the 9-degree pitch moves rows by more than R = 8 at this size
+        assert r.read_counters()["motion_clips"] > 0
+    r.close()

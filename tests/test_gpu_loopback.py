@@ -13,8 +13,9 @@ Checked: along the 8-frame moving-camera path plus a 12-degree pitch turn (past 
 halo: the motion rule clips those reprojections in every handle) and three frames through
 ptx_render_bands' communicator branch, the 4-band split equals one handle bit for bit (temporal
 output, spatial output, radiance) after every frame; both count the same clipped pixels; a rank
-that reset its history while the camera moves does not desynchronise the exchange; a rank whose
-peer never renders gets an error status within the deadline and its communicator is aborted.
+that reset its history while the camera moves does not desynchronise the exchange; ReSTIR GI's
+motion pass over three communicator bands equals one handle too; a rank whose peer never renders
+gets an error status within the deadline and its communicator is aborted.
 """
 import json
 import os
@@ -42,6 +43,11 @@ def test_loopback_communicator_bands():
     assert sp["clips_one"] > 0 and sp["clips_bands"] == sp["clips_one"]
     assert sp["hist_used"] > 0.2
     assert all(c["world"] == 4 and c["halo_bytes_sent"] > 0 for c in sp["comm"])
+    gi = out["gi_split"]
+    for fr in gi["frames"]:
+        assert fr["history"] == fr["temporal"] == fr["radiance"] == 0, fr
+    assert gi["clips_one"] > 0 and gi["clips_bands"] == gi["clips_one"]
+    assert gi["hist_used"] > 0.2
     rr = out["reset_one_rank"]
     assert all(not any(e) for e in rr["errors"]), rr
     assert rr["finite"]
