@@ -65,32 +65,48 @@ def _compose(t, q, s) -> np.ndarray:
             float(t[0]), float(t[1]), float(t[2]), 1.0]
 
 
+def _div(a: float, b: float) -> float:
+    """a / b with JavaScript's IEEE semantics (x / 0 = +-Infinity, 0 / 0 = NaN), where Python
+    raises: a zero-scale matrix decomposes to the same Infinity / NaN as three.js on the JS host."""
+    if b != 0.0:
+        return a / b
+    if a == 0.0 or math.isnan(a):
+        return math.nan
+    return math.copysign(math.inf, a) * math.copysign(1.0, b)
+
+
+def _sqrt(x: float) -> float:
+    """Math.sqrt: NaN for a negative argument (Python raises)."""
+    return math.sqrt(x) if x >= 0.0 else math.nan
+
+
 def _decompose(m) -> tuple:
     """three.js Matrix4.decompose(position, quaternion, scale) (f64, the library's order): column
     lengths as scale (the first negated when the determinant is negative), the columns scaled by
-    1 / s, Quaternion.setFromRotationMatrix of that 3x3."""
-    sx = math.sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2])
-    sy = math.sqrt(m[4] * m[4] + m[5] * m[5] + m[6] * m[6])
-    sz = math.sqrt(m[8] * m[8] + m[9] * m[9] + m[10] * m[10])
+    1 / s, Quaternion.setFromRotationMatrix of that 3x3.  A zero-length column gives the JS
+    host's Infinity / NaN (never an exception: ADVICE r4), so both hosts bake the same bits."""
+    sx = _sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2])
+    sy = _sqrt(m[4] * m[4] + m[5] * m[5] + m[6] * m[6])
+    sz = _sqrt(m[8] * m[8] + m[9] * m[9] + m[10] * m[10])
     if _determinant(m) < 0:
         sx = -sx
-    ix, iy, iz = 1 / sx, 1 / sy, 1 / sz
+    ix, iy, iz = _div(1.0, sx), _div(1.0, sy), _div(1.0, sz)
     m11, m21, m31 = m[0] * ix, m[1] * ix, m[2] * ix
     m12, m22, m32 = m[4] * iy, m[5] * iy, m[6] * iy
     m13, m23, m33 = m[8] * iz, m[9] * iz, m[10] * iz
     trace = m11 + m22 + m33
     if trace > 0:
-        s = 0.5 / math.sqrt(trace + 1.0)
-        q = ((m32 - m23) * s, (m13 - m31) * s, (m21 - m12) * s, 0.25 / s)
+        s = _div(0.5, _sqrt(trace + 1.0))
+        q = ((m32 - m23) * s, (m13 - m31) * s, (m21 - m12) * s, _div(0.25, s))
     elif m11 > m22 and m11 > m33:
-        s = 2.0 * math.sqrt(1.0 + m11 - m22 - m33)
-        q = (0.25 * s, (m12 + m21) / s, (m13 + m31) / s, (m32 - m23) / s)
+        s = 2.0 * _sqrt(1.0 + m11 - m22 - m33)
+        q = (0.25 * s, _div(m12 + m21, s), _div(m13 + m31, s), _div(m32 - m23, s))
     elif m22 > m33:
-        s = 2.0 * math.sqrt(1.0 + m22 - m11 - m33)
-        q = ((m12 + m21) / s, 0.25 * s, (m23 + m32) / s, (m13 - m31) / s)
+        s = 2.0 * _sqrt(1.0 + m22 - m11 - m33)
+        q = (_div(m12 + m21, s), 0.25 * s, _div(m23 + m32, s), _div(m13 - m31, s))
     else:
-        s = 2.0 * math.sqrt(1.0 + m33 - m11 - m22)
-        q = ((m13 + m31) / s, (m23 + m32) / s, 0.25 * s, (m21 - m12) / s)
+        s = 2.0 * _sqrt(1.0 + m33 - m11 - m22)
+        q = (_div(m13 + m31, s), _div(m23 + m32, s), 0.25 * s, _div(m21 - m12, s))
     return (m[12], m[13], m[14]), q, (sx, sy, sz)
 
 

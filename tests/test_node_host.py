@@ -271,8 +271,14 @@ def test_matrix_nodes_are_decomposed_and_recomposed_like_three():
             sc[k % 3] = -sc[k % 3]  # mirrored
         cases.append(G._compose(list(rng.normal(size=3) * 4), q, sc))
     cases.append([1.0, 0.0, 0.0, 0.0, 0.5, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 1.0, 2.0, 3.0, 1.0])  # shear
+    n_regular = len(cases)
+    # zero-scale columns (a collapsed node): JS divides by zero to Infinity / NaN, Python must too
+    cases.append([0.0, 0.0, 0.0, 0.0, 0.0, 2.0, 0.0, 0.0, 0.0, 0.0, 3.0, 0.0, 1.0, 2.0, 3.0, 1.0])
+    cases.append([0.0] * 12 + [4.0, 5.0, 6.0, 1.0])
     want = [G._node_local_matrix({"matrix": m}) for m in cases]
-    for m, w in zip(cases[:-1], want[:-1]):
+    for w in want[n_regular:]:
+        assert np.isnan(np.array(w, dtype=np.float64)[:12]).any()  # (three.js's result: NaN rotation)
+    for m, w in zip(cases[:n_regular - 1], want[:n_regular - 1]):
         np.testing.assert_allclose(w, m, rtol=0, atol=1e-12 * max(1.0, max(abs(v) for v in m)))
     src = ("const G = require('./pathtracerdemo_amd/js/gltf.js');"
            "const ms = JSON.parse(require('fs').readFileSync(0, 'utf8'));"
@@ -280,5 +286,9 @@ def test_matrix_nodes_are_decomposed_and_recomposed_like_three():
     p = subprocess.run([NODE, "-e", src], input=json.dumps(cases), capture_output=True, text=True, cwd=ROOT, timeout=60)
     assert p.returncode == 0, p.stderr
     got = json.loads(p.stdout)
-    for g, w in zip(got, want):  # (JSON carries -0 as 0: compared as values, which is exact here)
-        assert np.array_equal(np.array(g, dtype=np.float64), np.array(w, dtype=np.float64))
+    assert len(got) == len(want)
+    for g, w in zip(got, want):  # (JSON carries -0 as 0 and NaN / Infinity as null: compared as values)
+        w = np.array(w, dtype=np.float64)
+        w[~np.isfinite(w)] = np.nan
+        g = np.array([np.nan if v is None else v for v in g], dtype=np.float64)
+        assert np.array_equal(g, w, equal_nan=True)
