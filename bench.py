@@ -61,20 +61,6 @@ DEFAULT_SCENE = {"reuse": "c3_interior_32", "restir": "dummy_scene_1", "mcpt": "
                  "gi": "c3_interior_32"}
 
 
-def ab_knob(key, dflt):
-    """PTX_AB's value for `key` as the library reads it (ptx_api.cpp ab_knob): "K" -> 1, "K=v" ->
-    atoi(v) -- the leading decimal integer of v, 0 when there is none ("K=" included)."""
-    import re
-    for item in os.environ.get("PTX_AB", "").split(","):
-        k, eq, v = item.partition("=")
-        if k == key:
-            if not eq:
-                return 1
-            m = re.match(r"\s*([+-]?\d+)", v)
-            return int(m.group(1)) if m else 0
-    return dflt
-
-
 def usable_cpus() -> int:
     """CPUs this process can actually use: its affinity set, capped by the cgroup CPU quota
     (a container's share -- the GPU box shows 256 logical CPUs but allows 16)."""

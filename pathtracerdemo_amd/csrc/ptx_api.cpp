@@ -22,7 +22,7 @@
 namespace ptx {
 
 
-int ab_knob(const char *key, int dflt) {
+int env_knob(const char *key, int dflt) {
     static const std::string ab = getenv("PTX_AB") ? getenv("PTX_AB") : "";
     const size_t n = std::strlen(key);
     for (size_t pos = 0; pos < ab.size();) {
@@ -100,7 +100,7 @@ int alloc_buf(ptx_handle *h, DevBuf &b, size_t bytes) {
     b.bytes = bytes;
     // diagnostics: PTX_AB=DEBUG_FILL=<byte> fills every new buffer with that byte (an
     // uninitialised read then shows up as a parity failure)
-    static const int fill = ab_knob("DEBUG_FILL", -1);
+    static const int fill = env_knob("DEBUG_FILL", -1);
     if (fill >= 0) HIP_CHECK(h, memset_sync(h, b.p, fill & 0xff, bytes));
     return PTX_OK;
 }
@@ -570,12 +570,9 @@ static ReuseArgs reuse_args(ptx_handle *h, int pass) {
 }
 
 // The motion temporal pass (wtmotion_*): the frame context's temporal job buffers (three job
-// planes; so its first part may run before the previous frame's spatial pass, which owns the
-// spatial job buffers, is done), the history reprojected through the previous frame's camera.
-// `pass`: the whole pass, its jobs before the wait (slots 0 and 2, the reprojection test on
-// geometry only) or the rest after it (slot 1 and the combine).
+// planes), the history reprojected through the previous frame's camera.
 void mat4_inverse(const float *mf, float *out);
-static ReuseArgs motion_args(ptx_handle *h, int pass) {
+static ReuseArgs motion_args(ptx_handle *h) {
     ReuseArgs A = reuse_args(h, PTX_PASS_SPATIAL);
     A.jstate = (float4 *)h->d_tjstate.p;
     A.jres = (float4 *)h->d_tjres.p;
@@ -584,15 +581,11 @@ static ReuseArgs motion_args(ptx_handle *h, int pass) {
     static const bool planes = ab_knob("JOB_PLANES", 1) != 0;
     A.jpx = planes ? 1u : A.jpp;
     A.jslot = planes ? h->band_h * h->cfg.width : 1u;
-    A.motion_slots = pass == kPassTemporalMotionJobs ? 5u : pass == kPassTemporalMotionCombine ? 2u : 7u;
-    A.motion_geom = pass == kPassTemporalMotionJobs ? 1u : 0u;
     A.hist_valid = h->hist_valid ? 1u : 0u;
     A.use_init = h->init_state_valid ? 1u : 0u;
-    // light segments finished by the combine, as in the still passes -- in the part that ends
-    // with the combine (the split's early jobs finish in their steps: the later part's trace
-    // rounds reuse the result buffers).  PTX_AB=MOTION_FOLD=0 / FOLD_LAST_STEP=0: off.
-    static const bool fold_on = ab_knob("FOLD_LAST_STEP", 1) != 0 && ab_knob("MOTION_FOLD", 1) != 0;
-    A.fold_last = fold_on && pass != kPassTemporalMotionJobs ? 1u : 0u;
+    // light segments finished by the combine, as in the still passes (PTX_AB=FOLD_LAST_STEP=0: off)
+    static const bool fold_on = ab_knob("FOLD_LAST_STEP", 1) != 0;
+    A.fold_last = fold_on ? 1u : 0u;
     A.motion = 1u;
     std::memcpy(A.vpinv_prev, h->hist_camera, sizeof A.vpinv_prev);  // (words 4..19 of that frame)
     mat4_inverse(A.vpinv_prev, A.vp_prev);
@@ -666,7 +659,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
     if (pass == PTX_PASS_TEMPORAL || pass == PTX_PASS_SPATIAL || pass == kPassTemporalJobs ||
         pass == kPassTemporalCombine || is_motion_pass(pass)) {
         const bool temporal = pass != PTX_PASS_SPATIAL;
-        ReuseArgs A = is_motion_pass(pass) ? motion_args(h, pass)
+        ReuseArgs A = is_motion_pass(pass) ? motion_args(h)
                                            : reuse_args(h, temporal ? PTX_PASS_TEMPORAL : PTX_PASS_SPATIAL);
         WaveBufs wj = w;
         if (A.fold_last && wj.res[2]) wj.nres = 3;  // light segments finished by the combine
@@ -674,7 +667,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         const int nr = reuse_rounds(temporal, A);
         // (the temporal pass in parts: its jobs = rounds 0..nr, its combine = round nr + 1)
         const int r_first = pass == kPassTemporalCombine ? nr + 1 : 0;
-        const int r_last = pass == kPassTemporalJobs || pass == kPassTemporalMotionJobs ? nr : nr + 1;
+        const int r_last = pass == kPassTemporalJobs ? nr : nr + 1;
         for (int r = r_first; e == hipSuccess && r <= r_last; ++r) {
             if (r > 0 && r <= nr) {
                 TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_TRACE, st);
@@ -801,7 +794,6 @@ static hipError_t spatial_overlap_seq(ptx_handle *h, const Scene &sc, const Wave
         we.dyn = use_dyn ? (uint32_t *)h->d_wctr.p + dyn0 +
                                (size_t)(ptx_handle::kMaxSplit + q) * kWaveMaxRounds * kDynRoundWords
                          : nullptr;
-        wi.pool = we.pool = nullptr;
         if (fold) wi.nres = we.nres = 3;
         WaveBufs wt = wi;  // this sequence's trace launches: both shares' slots
         wt.seg_count = wi.seg_count + we.seg_count;
@@ -877,12 +869,11 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     bool surf_ok = h->surf_valid;
     for (int i = 0; i < npasses && i < 8; ++i) {
         if (passes[i] == PTX_PASS_GBUFFER) surf_ok = false;
-        else if (passes[i] == PTX_PASS_INIT && w.surf) surf_ok = true, h->ev_surf_ok = false;
+        else if (passes[i] == PTX_PASS_INIT && w.surf) surf_ok = true;
         else if ((passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalJobs || passes[i] == PTX_PASS_SPATIAL ||
                   is_motion_pass(passes[i])) &&
                  w.surf) {
             need_surf[i] = !surf_ok;
-            if (need_surf[i]) h->ev_surf_ok = false;
             surf_ok = true;
         }
     }
@@ -917,18 +908,6 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
             part.dyn = !use_dyn ? nullptr
                                : (uint32_t *)h->d_wctr.p + 2u * kWaveMaxRounds * ws.cnt_stride +
                                      (uint32_t)((set * ptx_handle::kMaxSplit + q) * kWaveMaxRounds) * kDynRoundWords;
-            // the launch sequence's restart pools (its dynamic-batch trace launches: <= kDynMaxGroups
-            // workgroups of WB / 64 waves; sequences run concurrently, so each has its own).
-            // PTX_AB=RESTART_POOL=0: every restart in place (A/B)
-            static const bool pool_on = ab_knob("RESTART_POOL", 1) != 0;
-            part.pool = nullptr;
-            if (PTX_RESTART_POOL && use_dyn && pool_on) {
-                const size_t per_set = (size_t)kDynMaxGroups * (kBlock / 64) * 2u * kRestartCap;  // float4s
-                if (!h->d_wpool.p && (e = hipMalloc(&h->d_wpool.p, kRestartPoolSets * per_set * 16u)) != hipSuccess)
-                    return e;
-                h->d_wpool.bytes = kRestartPoolSets * per_set * 16u;
-                part.pool = (float4 *)h->d_wpool.p + (size_t)(set * ptx_handle::kMaxSplit + q) * per_set;
-            }
             part.seg_base = (uint32_t)((uint64_t)ws.nseg * q / k);
             part.seg_count = (uint32_t)((uint64_t)ws.nseg * (q + 1) / k) - part.seg_base;
             if (!part.seg_count) continue;
@@ -957,8 +936,7 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     }
     // the temporal pass rewrote the reservoirs PT_1's state describes, and summarised them
     for (int i = 0; i < npasses; ++i)
-        if (passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalCombine || passes[i] == kPassTemporalMotion ||
-            passes[i] == kPassTemporalMotionCombine) {
+        if (passes[i] == PTX_PASS_TEMPORAL || passes[i] == kPassTemporalCombine || passes[i] == kPassTemporalMotion) {
             h->init_state_valid = false;
             h->nbr_valid = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
         }
@@ -1072,7 +1050,6 @@ static void swap_two(ptx_handle *h);
 // The next context (round robin over pipe_depth() contexts): the members become the next
 // context's, `alt` (and `alt2`) the ones after it.
 void swap_frame_ctx(ptx_handle *h) {
-    h->ev_surf_ok = false;  // (ev_surf describes the surface records of the context it was recorded on)
     swap_two(h);
     if (pipe_depth() == 3) std::swap(h->alt, h->alt2);
     h->ctx_idx = (h->ctx_idx + 1) % pipe_depth();
@@ -1094,7 +1071,6 @@ static void swap_two(ptx_handle *h) {
     std::swap(h->d_wact0, a.wact0);
     std::swap(h->d_wact1, a.wact1);
     std::swap(h->d_wctr, a.wctr);
-    std::swap(h->d_wpool, a.wpool);
     std::swap(h->wave_ray_cap, a.wave_ray_cap);
     std::swap(h->wave_slots, a.wave_slots);
     std::swap(h->stream, a.stream);
@@ -1146,12 +1122,6 @@ int leave_alt(ptx_handle *h) {
     return PTX_OK;
 }
 
-static int ensure_motion_events(ptx_handle *h) {
-    for (hipEvent_t *ev : {&h->ev_surf, &h->ev_psurf, &h->ev_motion})
-        if (!*ev) HIP_CHECK(h, hipEventCreateWithFlags(ev, hipEventDisableTiming));
-    return PTX_OK;
-}
-
 // A whole ReSTIR frame in wavefront form (G-buffer -> init -> final per segment group), timed
 // as one unit in stats slot PTX_STAT_FRAME.  Returns 1 if this path does not apply.
 static int timed_wave_frame(ptx_handle *h) {
@@ -1165,21 +1135,13 @@ static int timed_wave_frame(ptx_handle *h) {
     Scene sc = make_scene(h);
     if (!tables_fit_lds(sc)) return 1;
     const bool pipe = pipelined(h);
-    // a moved camera (whole-image DI reuse): the history is reprojected, from the previous
-    // frame's surface records.  Pipelined (two contexts), the motion pass runs in two parts
-    // like the still temporal pass (msplit): the previous frame's records are copied on THIS
-    // frame's stream once that frame's PT_1 is done (ev_surf) and its slot-0 / slot-2 jobs run
-    // before the wait for the previous frame; otherwise they are copied first on the previous
-    // frame's stream (the current one here) and the whole pass runs after the wait.
-    // Measured (moving-camera bench, same box, 2 reps): split 313.2 / 312.2 Msamples/s, whole
-    // 315.5 / 314.8 -- the early jobs compete with the previous frame's spatial pass instead of
-    // shortening the chain; so PTX_AB=MOTION_SPLIT=1 (A/B) selects the split, the default runs
-    // the whole pass after the wait.
-    static const bool msplit_on = ab_knob("MOTION_SPLIT", 0) != 0;
+    // a moved camera (DI reuse or GI): the history is reprojected, from the previous frame's
+    // surface records (GI: G-buffer), copied first on the previous frame's stream (the current
+    // one here); the whole motion pass runs after the wait for that frame.  (A split form --
+    // the canonical sample's jobs before the wait -- measured 313 vs 315 Msamples/s on the
+    // moving-camera bench: round 4)
     bool moved = h->hist_valid && h->hist_moved && has_reuse(h);
-    const bool msplit = moved && pipe && msplit_on && pipe_depth() == 2 && h->ev_surf_ok && h->d_surf.p;
-    const DevBuf prev_surf = h->d_surf;  // (the previous frame's context, before the swap)
-    if (moved && !msplit) {
+    if (moved) {
         if (int rc = motion_prepare(h, h->stream)) return rc;
         moved = h->hist_moved;
     }
@@ -1207,36 +1169,15 @@ static int timed_wave_frame(ptx_handle *h) {
         // the previous frame's spatial output)
         static const bool split = ab_knob("TEMPORAL_SPLIT", 1) != 0;
         static const int front[2] = {PTX_PASS_GBUFFER, PTX_PASS_INIT};
-        static const int jobs[1] = {kPassTemporalJobs}, jobs_m[1] = {kPassTemporalMotionJobs};
+        static const int jobs[1] = {kPassTemporalJobs};
         static const int temporal[1] = {PTX_PASS_TEMPORAL}, temporal_b[1] = {kPassTemporalCombine};
-        static const int temporal_m[1] = {kPassTemporalMotion}, temporal_mb[1] = {kPassTemporalMotionCombine};
+        static const int temporal_m[1] = {kPassTemporalMotion};
         static const int back[2] = {PTX_PASS_SPATIAL, PTX_PASS_FINAL};
-        if (int rc = ensure_motion_events(h)) return rc;
-        // (the frame after a split motion pass rewrites the surface records it copied)
-        if (h->psurf_wait) HIP_CHECK(h, hipStreamWaitEvent(h->stream, h->ev_psurf, 0));
-        h->psurf_wait = false;
         e = launch_wave_parts(h, sc, w, front, 2);
-        if (e == hipSuccess && msplit) {
-            // the previous frame's surface records, once its PT_1 is done and the motion combine
-            // before (which reads d_psurf) has finished
-            if (h->motion_wait) e = hipStreamWaitEvent(h->stream, h->ev_motion, 0);
-            if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_surf, 0);
-            if (e == hipSuccess && alloc_buf(h, h->d_psurf, prev_surf.bytes) != PTX_OK) e = hipErrorOutOfMemory;
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(h->d_psurf.p, prev_surf.p, prev_surf.bytes, hipMemcpyDeviceToDevice, h->stream);
-            if (e == hipSuccess) e = hipEventRecord(h->ev_psurf, h->stream);
-            h->psurf_wait = true;
-        }
-        // this frame's surface records are complete here (a moved next frame copies them)
-        if (e == hipSuccess) e = hipEventRecord(h->ev_surf, h->stream);
-        h->ev_surf_ok = e == hipSuccess;
-        if (e == hipSuccess && (msplit || (split && !moved)))
-            e = launch_wave_parts(h, sc, w, msplit ? jobs_m : jobs, 1);
+        if (e == hipSuccess && split && !moved) e = launch_wave_parts(h, sc, w, jobs, 1);
         if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
         if (e == hipSuccess)
-            e = launch_wave_parts(h, sc, w, msplit ? temporal_mb : moved ? temporal_m : split ? temporal_b : temporal, 1);
-        if (e == hipSuccess && msplit) e = hipEventRecord(h->ev_motion, h->stream);
-        h->motion_wait = msplit;
+            e = launch_wave_parts(h, sc, w, moved ? temporal_m : split ? temporal_b : temporal, 1);
         if (e == hipSuccess) e = launch_wave_parts(h, sc, w, back, 2);
         if (e == hipSuccess) mark_history(h);
     } else if (has_reuse(h)) {
@@ -1810,13 +1751,13 @@ int ptx_destroy(ptx_handle *h) {
     if (h->host_stage) (void)hipHostFree(h->host_stage);
     for (DevBuf *b : {&h->d_canvas, &h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
-                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wres2, &h->d_wact0, &h->d_wact1, &h->d_wctr, &h->d_wpool,
+                      &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wres2, &h->d_wact0, &h->d_wact1, &h->d_wctr,
                       &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_tjstate, &h->d_tjres, &h->d_nbr, &h->d_surf, &h->d_psurf, &h->d_direct, &h->d_census})
         free_buf(*b);
     for (ptx_handle::FrameCtx *ap : {&h->alt, &h->alt2}) {
         ptx_handle::FrameCtx &a = *ap;
         for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wres2, &a.wact0, &a.wact1,
-                          &a.wctr, &a.wpool, &a.tjstate, &a.tjres})
+                          &a.wctr, &a.tjstate, &a.tjres})
             free_buf(*b);
         if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
         for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {
@@ -1827,8 +1768,6 @@ int ptx_destroy(ptx_handle *h) {
     if (h->alt_stream) (void)hipStreamDestroy(h->alt_stream);
     if (h->alt2_stream) (void)hipStreamDestroy(h->alt2_stream);
     if (h->ev_prev) (void)hipEventDestroy(h->ev_prev);
-    for (hipEvent_t ev : {h->ev_surf, h->ev_psurf, h->ev_motion})
-        if (ev) (void)hipEventDestroy(ev);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {
         if (h->ev_join[q]) (void)hipEventDestroy(h->ev_join[q]);

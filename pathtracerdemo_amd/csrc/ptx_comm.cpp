@@ -116,7 +116,7 @@ const Rccl &rccl() {
 // failed inside it) thus gets an error status after `seconds` instead of hanging for ever, and
 // the communicator is aborted (PTX_AB=COMM_TIMEOUT_S=n overrides the 120 s default).
 int comm_timeout_s() {
-    static const int t = ab_knob("COMM_TIMEOUT_S", 120);
+    static const int t = env_knob("COMM_TIMEOUT_S", 120);
     return t > 0 ? t : 120;
 }
 ncclResult_t comm_wait(ncclComm_t c, int seconds) {

@@ -158,46 +158,10 @@ __device__ __forceinline__ f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y +
 __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ f3 operator*(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
-// f3 / s = three correctly rounded divisions by one s (normalize is v / length(v)).  The
-// compiler expands each `x / s` on its own (v_div_scale x2, v_rcp, 6 FMA/MUL, v_div_fmas,
-// v_div_fixup, plus VCC hazard pads); PTX_SHARED_DIV shares the refined reciprocal over the
-// three and drops the scale steps where they are identities: with s's exponent in [-40, 40]
-// and every component's in [-50, 50] (zero, inf and NaN give 0), v_div_scale leaves both
-// operands unscaled with VCC = 0 (the quotient far from overflow and denormals, the numerator
-// far above 2^-103), so the compiler's sequence is exactly the rcp / FMA chain below with
-// v_div_fmas a plain FMA, and the same v_div_fixup settles zeros, signs, inf and NaN from the
-// operands alone.  Same bits.  Any other operand (in any lane of the wave) and any constant s
-// (whose reciprocal the compiler would fold) take the compiler's divisions.  Off: bit-exact
-// (GPU suite green with it on) but not faster -- a third fewer division issue slots left the
-// logic kernels within +-3 % and the headline -0.6 %, so they are not
-// bound by the divisions' issue.
-#ifndef PTX_SHARED_DIV
-#define PTX_SHARED_DIV 0
-#endif
-__device__ __forceinline__ float div_by_rcp(float a, float s, float y) {
-    float q = a * y;
-    float r = __builtin_fmaf(-s, q, a);
-    q = __builtin_fmaf(r, y, q);
-    r = __builtin_fmaf(-s, q, a);
-    q = __builtin_fmaf(r, y, q);
-    return __builtin_amdgcn_div_fixupf(q, s, a);
-}
-__device__ __forceinline__ f3 operator/(f3 a, float s) {
-    if constexpr (PTX_SHARED_DIV) {
-        if (!__builtin_constant_p(s)) {
-            const int es = __builtin_amdgcn_frexp_expf(s);
-            const int ex = __builtin_amdgcn_frexp_expf(a.x), ey = __builtin_amdgcn_frexp_expf(a.y),
-                      ez = __builtin_amdgcn_frexp_expf(a.z);
-            const bool ok = (uint32_t)(es + 40) <= 80u && min(min(ex, ey), ez) >= -50 && max(max(ex, ey), ez) <= 50;
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) == 0ull, 1)) {
-                const float y0 = __builtin_amdgcn_rcpf(s);
-                const float y = __builtin_fmaf(__builtin_fmaf(-s, y0, 1.0f), y0, y0);
-                return f3{div_by_rcp(a.x, s, y), div_by_rcp(a.y, s, y), div_by_rcp(a.z, s, y)};
-            }
-        }
-    }
-    return f3{a.x / s, a.y / s, a.z / s};
-}
+// f3 / s = three correctly rounded divisions by one s (normalize is v / length(v)).  (Sharing one
+// refined reciprocal over the three, same bits, left the logic kernels within +-3 % and the
+// headline -0.6 %: they are not bound by the divisions' issue -- round 4)
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return f3{a.x / s, a.y / s, a.z / s}; }
 __device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {

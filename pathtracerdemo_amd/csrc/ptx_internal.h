@@ -30,14 +30,11 @@ using namespace ptx;
 // previous frame's spatial output) -- so a pipelined frame runs the jobs before waiting for
 // the previous frame.
 constexpr int kPassTemporalJobs = 0x100, kPassTemporalCombine = 0x101;
-// the temporal pass of a frame whose camera moved since the history's (wtmotion_*), whole, or
-// in two parts like the still one: the jobs that read only this frame's PT_1 output and the
-// previous frame's surface records (slot 0: the canonical sample at home, slot 2: the canonical
-// sample in the previous frame's domain), then -- after the wait for the previous frame -- the
-// history sample's job (slot 1, it reads that frame's spatial output) and the combine
-constexpr int kPassTemporalMotion = 0x102, kPassTemporalMotionJobs = 0x103, kPassTemporalMotionCombine = 0x104;
+// the temporal pass of a frame whose camera moved since the history's (wtmotion_* / wgim_*),
+// run whole after the wait for the previous frame (a split form measured slower: DESIGN §4)
+constexpr int kPassTemporalMotion = 0x102;
 inline bool is_motion_pass(int p) {
-    return p == kPassTemporalMotion || p == kPassTemporalMotionJobs || p == kPassTemporalMotionCombine;
+    return p == kPassTemporalMotion;
 }
 
 struct ptx_handle {
@@ -128,13 +125,6 @@ struct ptx_handle {
     int ctx_idx = 0;              // which context the members above hold (0: own_stream's)
     hipStream_t alt_stream = nullptr, alt2_stream = nullptr;  // the other contexts' streams (owned)
     hipEvent_t ev_prev = nullptr;
-    // split motion pass (pipelined whole-image frames): ev_surf after each frame's PT_1 (its surface
-    // records are complete: the next frame's copy into d_psurf waits for it), ev_psurf after that
-    // copy (the frame after, which rewrites those records, waits for it), ev_motion after the
-    // motion combine (the next copy into d_psurf waits for it)
-    hipEvent_t ev_surf = nullptr, ev_psurf = nullptr, ev_motion = nullptr;
-    bool psurf_wait = false, motion_wait = false;
-    bool ev_surf_ok = false;  // ev_surf marks the latest PT_1's surface records (reset by any other pass)
     // multi-GPU (ptx_comm.cpp): the RCCL communicator this handle owns (ncclComm_t), its
     // rank and world; the halo exchange stream and its fork / done events
     void *comm = nullptr;

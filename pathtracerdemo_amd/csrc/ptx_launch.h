@@ -10,11 +10,19 @@ namespace ptx {
 constexpr int kTile = 16;
 constexpr int kBlock = 256;
 
-// A/B and diagnostic switches: every one is read from ONE environment variable, PTX_AB, a
-// comma-separated list of KEY or KEY=int (e.g. PTX_AB=TRACE_DYN=0,SEG_PX=512); a key that is
-// absent gives `dflt`.  Without PTX_AB every launch runs the product configuration, and
-// bench.py echoes PTX_AB (and any other PTX_* variable) in its line.  Defined in ptx_api.cpp.
-int ab_knob(const char *key, int dflt);
+// Runtime switches are read from ONE environment variable, PTX_AB, a comma-separated list of
+// KEY or KEY=int; a key that is absent gives `dflt`.  env_knob (ptx_api.cpp): the few the
+// shipped library honours, each covered by a test -- COMM_TIMEOUT_S (test_gpu_loopback.py),
+// DEBUG_FILL (test_gpu_debug_fill.py).  ab_knob: the A/B and diagnostic switches of the measurement builds
+// (make variant NAME=x ALT_DEFS=-DPTX_AB_BUILD, make wgt; selected with PTX_LIB_PATH) -- in the
+// shipped library every one is its default, a compile-time constant, and the losing branches
+// fold away.  bench.py echoes PTX_AB (and any other PTX_* variable) in its line.
+int env_knob(const char *key, int dflt);
+#ifdef PTX_AB_BUILD
+inline int ab_knob(const char *key, int dflt) { return env_knob(key, dflt); }
+#else
+constexpr int ab_knob(const char *, int dflt) { return dflt; }
+#endif
 
 // dynamic LDS bytes for a traversal stack of `depth` entries per thread
 inline size_t stack_lds_bytes(uint32_t depth) { return (size_t)depth * kBlock * sizeof(uint32_t); }
@@ -85,21 +93,7 @@ struct WaveBufs {
     // DI reuse pipeline: primary-hit surface records (2 uint4 per pixel, first band row; halo
     // rows at negative / >= npix indices), written by winit_start; nullptr otherwise
     uint4 *surf;
-    // Visibility restart pools of a dynamic-batch trace launch (trace_lanes): per wave of the
-    // launch, kRestartCap entries of 2 float4; nullptr = every restart continues in place
-    float4 *pool;
 };
-// A Visibility query whose closest hit is transmissive restarts from the hit (up to 5
-// segments, SH/PT_1_InitPass.wgsl:774-802).  When fewer than kRestartInPlace lanes of a wave's
-// batch restart, their continuations go to the wave's pool instead (origin, remaining distance,
-// transmittance, segment, query slot) and the wave walks them later as one batch of >=
-// kRestartRun restarts (or at the end): the same per-query walks, without 60+ idle lanes each.
-// PTX_RESTART_POOL=1 builds this form (A/B: -7.5 % on the headline; default off).
-#ifndef PTX_RESTART_POOL
-#define PTX_RESTART_POOL 0
-#endif
-constexpr uint32_t kRestartCap = 64u, kRestartInPlace = 32u, kRestartRun = 32u;
-constexpr size_t kRestartPoolSets = 8u;  // (tile set, launch sequence) pairs of a frame context
 // dynamic trace batches: one workgroup per slot, at most kDynMaxGroups (the chip holds ~1024 trace
 // workgroups; later ones find the list drained and leave)
 constexpr uint32_t kDynMaxGroups = 1024u, kDynMaxSlots = 4096u;
@@ -155,11 +149,6 @@ struct ReuseArgs {
     const uint4 *psurf;
     int32_t prev_row_lo, prev_row_hi;
     unsigned long long *clip;  // nullptr: not counted
-    // the start kernel's job slots (bit k: slot k) and, for the part that runs before the
-    // previous frame's spatial output is complete, the reprojection test without the history's
-    // confidence (motion_geom: slot 2 is created wherever the geometry passes; the combine uses
-    // its result only where that confidence is nonzero)
-    uint32_t motion_slots, motion_geom;
 };
 // the motion temporal pass's jobs per pixel: the canonical sample at home, the reprojected
 // history sample here, the canonical sample in the previous frame's domain

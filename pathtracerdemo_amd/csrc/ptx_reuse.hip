@@ -608,10 +608,6 @@ __device__ __forceinline__ MotionHist motion_hist(const Scene &sc, const ReuseAr
     const f3 x0p = x0_prev(A, sc, m.px, m.py);
     const float dp = length(pp - x0p), dc = length(P - x0p);
     if (!(fabsf(dp - dc) <= 0.05f * dc)) return m;
-    if (A.motion_geom) {  // (the history itself is not complete yet: geometry only)
-        m.ok = true;
-        return m;
-    }
     m.C = min(A.hist[8 * (ptrdiff_t)m.pp + 7].y, A.cap);
     m.ok = m.C != 0u;
     return m;
@@ -641,12 +637,10 @@ void wtmotion_start(Scene sc, WaveBufs w, ReuseArgs A) {
         const uint4 r5c = valid ? rv[5] : make_uint4(0u, 0u, 0u, 0u);
         const uint32_t cC = valid ? rv[7].y : 0u, clen = r5c.w, ck = r5c.x & 0xffu;
         const bool canon = valid && cC != 0u && clen >= 2u;
-        const bool count = (A.motion_slots & 2u) != 0u;  // (once per pixel: with slot 1)
-        const MotionHist mh = valid ? motion_hist(sc, A, X1, y, count) : MotionHist{false, 0, 0u, 0u, 0u};
+        const MotionHist mh = valid ? motion_hist(sc, A, X1, y, true) : MotionHist{false, 0, 0u, 0u, 0u};
         // the pixel's jobs through ONE job_emit site (three inlined copies needed 256 VGPRs)
 #pragma unroll 1
         for (uint32_t slot = 0; slot < kMotionJobs; ++slot) {  // (uniform)
-            if (!(A.motion_slots & (1u << slot))) continue;
             const uint32_t jid = job_id(A, pix, slot);
             Job s;
             bool act = false;

@@ -64,13 +64,12 @@ constexpr uint32_t kFlatMinInstances = 3u;
 // The queries of one wave: lane state {ray, kind, transmittance T, remaining distance, segment}
 // for query slot gi (its result at res[2 gi]).  Visibility (SH/PT_1_InitPass.wgsl:774-802) walks
 // through transmissive hits: one trace site, looped, so the traversal code is emitted once.
-// pool (dynamic batches): after the first segment, a few restarting lanes leave their
-// continuation in the wave's pool (kRestartInPlace, trace_restarts) instead of walking again here.
+// (A form that parked a wave's few restarting lanes in a per-wave pool and walked them later as
+// one batch measured -7.5 % on the headline, 442 vs 477 Msamples/s: round 4)
 template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES, bool FLAT>
 __device__ __forceinline__ void trace_lanes(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
                                             uint32_t *stack, CoopLds coop, Ray r, uint32_t kind, float T, float remain,
-                                            uint32_t seg, bool active, float4 *res, uint32_t gi, float4 *pool,
-                                            uint32_t &pool_n, uint32_t *dbg) {
+                                            uint32_t seg, bool active, float4 *res, uint32_t gi, uint32_t *dbg) {
     const bool vis = kind != Q_CLOSEST;
     for (;;) {
         const float t_max = !active ? __builtin_nanf("") : vis ? fminf(remain, 1e10f) : 1e10f;
@@ -107,20 +106,6 @@ __device__ __forceinline__ void trace_lanes(const Scene &sc, const SubRoot *subs
                 active = false;
             }
         }
-        if (pool) {  // (wave-uniform) lanes that just finished their first segment
-            const unsigned long long rs = wballot(active && seg == 1u);
-            const uint32_t nr = (uint32_t)__popcll(rs);
-            if (nr != 0u && nr < kRestartInPlace && pool_n + nr <= kRestartCap) {
-                if (active && seg == 1u) {
-                    const uint32_t slot =
-                        pool_n + __builtin_amdgcn_mbcnt_hi((uint32_t)(rs >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rs, 0u));
-                    pool[2u * slot] = make_float4(r.o.x, r.o.y, r.o.z, remain);
-                    pool[2u * slot + 1u] = make_float4(T, asf(seg), asf(gi), 0.0f);
-                    active = false;
-                }
-                pool_n += nr;
-            }
-        }
         if (wballot(active) == 0ull) break;
     }
 }
@@ -129,8 +114,7 @@ __device__ __forceinline__ void trace_lanes(const Scene &sc, const SubRoot *subs
 template <bool COUNT, bool PROF, bool OCC, bool LDS_TABLES = false, bool FLAT = false>
 __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
                                             uint32_t *stack, CoopLds coop, float4 *res_all, const float4 *rays_all,
-                                            uint32_t gbase, uint32_t i, bool active, float4 *pool, uint32_t &pool_n,
-                                            uint32_t *dbg = nullptr) {
+                                            uint32_t gbase, uint32_t i, bool active, uint32_t *dbg = nullptr) {
     const uint32_t gi = gbase + i;
     float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
     if (active) {
@@ -138,7 +122,7 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
         b = rays_all[2u * gi + 1u];
     }
     trace_lanes<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop, Ray{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)},
-                                                    asu(b.w), 1.0f, a.w, 0u, active, res_all, gi, pool, pool_n, dbg);
+                                                    asu(b.w), 1.0f, a.w, 0u, active, res_all, gi, dbg);
 }
 // Dynamic batches (WaveBufs::dyn): the launch's rays -- every slot of the launch's segment
 // range -- are one list of 64-query batches (a slot's batch k = its queries 64k .. 64k+63,
@@ -195,11 +179,6 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         uint32_t *heads = w.dyn + round * kDynRoundWords;
         const uint32_t lane = __lane_id();
         float4 *res_all = res_buf(w, round);
-        // this wave's restart pool (none in the counting / profiling builds: same work, in place)
-        float4 *pool = (!COUNT && !PROF && w.pool)
-                           ? w.pool + ((size_t)blockIdx.x * (WB / 64u) + (threadIdx.x >> 6)) * (2u * kRestartCap)
-                           : nullptr;
-        uint32_t pool_n = 0u;
         uint32_t x = blockIdx.x % kDynHeads, visited = 0u;
         uint32_t c0 = (uint32_t)((uint64_t)total * x / kDynHeads), c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
         // each dequeue takes G consecutive batches (WaveBufs::trace_split in this mode): one
@@ -207,102 +186,22 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         const uint32_t G = w.trace_split;
         uint32_t bnext = 0u;
         if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
-        if constexpr (!PTX_RESTART_POOL) {
-            // One trace_batch per dequeued batch, every restart in place.  (The pooled loop
-            // below, one trace site fed by batches and pooled restarts, measured -7.5 % on the
-            // headline against this form: 442 vs 477 Msamples/s, tools/cl/r4_libs_ab.sh,
-            // r4_bis_ab.sh.)
-            uint32_t no_pool = 0u;
-            uint32_t bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
-            for (;;) {  // wave-uniform
-                if (bi >= c1) {  // this chunk is drained: the next head
-                    if (++visited == kDynHeads) break;
-                    x = (x + 1u) % kDynHeads;
-                    c0 = (uint32_t)((uint64_t)total * x / kDynHeads);
-                    c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
-                    if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
-                    bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
-                    continue;
-                }
-                if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);  // the next dequeue, fetched ahead
-                const uint32_t bend = min(bi + G, c1);
-                uint32_t lo = 0u;
-                for (; bi < bend; ++bi) {
-                    uint32_t hi = w.seg_count;  // last slot with pref <= bi (batches ascend: search from lo)
-                    while (hi - lo > 1u) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (pref[mid] <= bi) lo = mid;
-                        else hi = mid;
-                    }
-                    const uint32_t j = w.seg_phys + w.seg_base + lo;
-                    const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
-                    const uint32_t i = (bi - pref[lo]) * 64u + lane;
-#ifdef PTX_WG_TIMES
-                    const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
-                    uint32_t dbg[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-#else
-                    uint32_t *dbg = nullptr;
-#endif
-                    trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
-                                                                     res_all + 2u * (size_t)j * w.ray_stride,
-                                                                     w.rays + 2u * (size_t)j * w.ray_stride, 0u, i,
-                                                                     i < n, nullptr, no_pool, dbg);
-#ifdef PTX_WG_TIMES
-                    batch_record(sc.wgt, tb0, bi, round, dbg);
-#endif
-                }
+        // one trace_batch per dequeued batch, every Visibility restart in place
+        uint32_t bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
+        for (;;) {  // wave-uniform
+            if (bi >= c1) {  // this chunk is drained: the next head
+                if (++visited == kDynHeads) break;
+                x = (x + 1u) % kDynHeads;
+                c0 = (uint32_t)((uint64_t)total * x / kDynHeads);
+                c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
+                if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
                 bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
+                continue;
             }
-            return;
-        }
-        uint32_t bi = 0u, bend = 0u, lo = 0u;
-        bool drained = false;
-        // One unit of work per iteration -- the next batch, or (once kRestartRun restarts are
-        // pooled, and at the end) the pooled restarts -- through ONE trace site (wave-uniform).
-        for (;;) {
-            bool restart = pool_n >= kRestartRun;
-            while (!restart && !drained && bi >= bend) {  // the next dequeue (its successor fetched ahead)
-                const uint32_t nb = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
-                if (nb < c1) {
-                    bi = nb;
-                    bend = min(nb + G, c1);
-                    lo = 0u;
-                    if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
-                } else if (++visited == kDynHeads) {
-                    drained = true;
-                } else {  // this chunk is drained: the next head
-                    x = (x + 1u) % kDynHeads;
-                    c0 = (uint32_t)((uint64_t)total * x / kDynHeads);
-                    c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
-                    if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
-                }
-            }
-            if (drained && !restart) {
-                if (pool_n == 0u) break;
-                restart = true;  // the wave's last restarts
-            }
-#ifdef PTX_WG_TIMES
-            const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
-            uint32_t dbg[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-            const uint32_t rec_bi = restart ? 0xFFFFFFFFu : bi;
-#else
-            uint32_t *dbg = nullptr;
-#endif
-            float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = make_float4(0.0f, 0.0f, 1.0f, 0.0f), c = a;
-            bool active;
-            uint32_t gi = 0u;
-            if (restart) {  // pooled restart `lane`: {origin, remain}, {T, segment, query slot}
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (the wave's own pool stores)
-                active = lane < pool_n;
-                c = make_float4(1.0f, 0.0f, 0.0f, 0.0f);
-                if (active) {
-                    a = pool[2u * lane];
-                    c = pool[2u * lane + 1u];
-                    gi = asu(c.z);
-                    b = w.rays[2u * gi + 1u];  // the query's direction and kind
-                }
-                pool_n = 0u;
-            } else {
+            if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);  // the next dequeue, fetched ahead
+            const uint32_t bend = min(bi + G, c1);
+            uint32_t lo = 0u;
+            for (; bi < bend; ++bi) {
                 uint32_t hi = w.seg_count;  // last slot with pref <= bi (batches ascend: search from lo)
                 while (hi - lo > 1u) {
                     const uint32_t mid = (lo + hi) >> 1;
@@ -312,22 +211,20 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
                 const uint32_t j = w.seg_phys + w.seg_base + lo;
                 const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
                 const uint32_t i = (bi - pref[lo]) * 64u + lane;
-                active = i < n;
-                gi = j * w.ray_stride + i;
-                c = make_float4(1.0f, 0.0f, 0.0f, 0.0f);  // T = 1, segment 0
-                if (active) {
-                    a = w.rays[2u * gi];
-                    b = w.rays[2u * gi + 1u];
-                }
-                ++bi;
-            }
-            trace_lanes<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
-                                                            Ray{mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)}, asu(b.w), c.x, a.w,
-                                                            asu(c.y), active, res_all, gi, restart ? nullptr : pool, pool_n,
-                                                            dbg);
 #ifdef PTX_WG_TIMES
-            batch_record(sc.wgt, tb0, rec_bi, round, dbg);
+                const unsigned long long tb0 = __builtin_amdgcn_s_memrealtime();
+                uint32_t dbg[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+#else
+                uint32_t *dbg = nullptr;
 #endif
+                trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop,
+                                                                 res_all + 2u * (size_t)j * w.ray_stride,
+                                                                 w.rays + 2u * (size_t)j * w.ray_stride, 0u, i, i < n, dbg);
+#ifdef PTX_WG_TIMES
+                batch_record(sc.wgt, tb0, bi, round, dbg);
+#endif
+            }
+            bi = c0 + G * (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
         }
         return;
     }
@@ -347,11 +244,10 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     const Inst *insts = T.insts;
     if (COUNT && sc.census)  // row census: this slot's queries count into its own block
         sc.counters = sc.census + (size_t)kCensusWords * ((sc.row_end - sc.row_begin + 7u) / 8u + j);
-    uint32_t no_pool = 0u;
     for (uint32_t i0 = share * WB; i0 < n; i0 += K * WB) {  // workgroup-uniform
         const uint32_t i = i0 + threadIdx.x;
         trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop, res_buf(w, round), w.rays,
-                                                         j * w.ray_stride, i, i < n, nullptr, no_pool);
+                                                         j * w.ray_stride, i, i < n);
     }
 }
 
@@ -1082,9 +978,7 @@ void wfinal_one(Scene sc, WaveBufs w, const uint4 *gbuf, const uint4 *reservoir,
                 }
             }
             // the traversal kernel's walk, every lane of the wave (idle ones with a NaN bound)
-            uint32_t no_pool = 0u;
-            trace_batch<false, false, false, true, FLAT>(sc, T.subs, T.insts, eps, stack, coop, res, rays, 0u, slot, active,
-                                                         nullptr, no_pool);
+            trace_batch<false, false, false, true, FLAT>(sc, T.subs, T.insts, eps, stack, coop, res, rays, 0u, slot, active);
             if (active) {  // wfinal_step
                 if (s.phase == 0u) {
                     const Hit h = get_hit(res, slot);
@@ -1309,7 +1203,8 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
                                (uint32_t)round, eps);
         return hipGetLastError();
     }
-    static const bool refill = ab_knob("TRACE_REFILL", 0) != 0;  // A/B switch for profiling
+    // (PTX_AB=TRACE_REFILL: the lane-refill kernel of ptx_trace on the queues -- A/B builds)
+    static const bool refill = ab_knob("TRACE_REFILL", 0) != 0;
     if (refill) {
         const uint32_t pb = w.seg_phys + w.seg_base;
         const uint32_t *cnt = w.cnt + (2u * round + 1u) * w.cnt_stride + pb;
@@ -1349,8 +1244,10 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
         static const bool no_lds = ab_knob("TRACE_NOLDS", 0) != 0;
         const bool tables_fit = tables_fit_lds(sc) && !no_lds;
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
+#ifdef PTX_AB_BUILD
                  : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
                  : occ == 6  ? trace_queue<false, 6>
+#endif
                  : occ == 5  ? (flat ? trace_queue<false, 5, false, true, false, true> : trace_queue<false, 5>)
                              : (flat ? trace_queue<false, 4, false, true, false, true> : trace_queue<false, 4>);
         hipLaunchKernelGGL(k, dim3(trace_grid(w)), dim3(WB), lds, s, sc, w, (uint32_t)round, eps);
