@@ -56,8 +56,10 @@ namespace ptx {
 #define PTX_FLAT_INST 1  // the instance loop flattened into the lanes (trace_core_flat) for scenes
 #endif                   // of >= kFlatMinInstances instances (host side, wave_trace)
 // Measured same box (1080p): furnished C3 (13 instances) +9.7 %, GI on C3 (3) +3.2 %, reuse on
-// C3 +0.6 %, TEST_MCPT on C1 (2 instances) -3.2 %: flattened from 3 instances up.
-constexpr uint32_t kFlatMinInstances = 3u;
+// C3 +0.6 %, TEST_MCPT on C1 (2 instances) -3.2 % (round 3, batch walk).  With the streamed lanes
+// (trace_stream, flat walk only) C1 gains too -- TEST_MCPT 1448 -> 1512, ReSTIR 1388 -> 1417
+// Msamples/s (round 5) -- so every scene takes the flat walk.
+constexpr uint32_t kFlatMinInstances = 1u;
 #ifndef PTX_LDS_TRANS
 #define PTX_LDS_TRANS 1  // the restart test's transmission from the LDS root table (A/B: 0 = Scene::mats)
 #endif
@@ -136,26 +138,29 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
 // lanes' new queries.  Lanes whose query is over are finalised (result written, or the
 // Visibility walk continued from the transmissive hit) and given new queries once at least
 // kStreamRefill of them wait, or when no lane is still walking (the result write and the ray
-// load then serve many lanes at once).  The stream: the launch's 64-query batches (WaveBufs::dyn
-// chunk heads, as trace_queue), taken by the wave as its lanes need them.
+// load then serve many lanes at once).  The stream (DYN): the launch's 64-query batches
+// (WaveBufs::dyn chunk heads, as trace_queue), taken by the wave as its lanes need them; or
+// (static slots) the workgroup's segment `sj` (`sn` queries), its 64-query batches taken by the
+// workgroup's waves through an LDS counter.
 #ifndef PTX_STREAM_REFILL
-#define PTX_STREAM_REFILL 16
+#define PTX_STREAM_REFILL 32
 #endif
 #ifndef PTX_TRACE_STREAM
 #define PTX_TRACE_STREAM 1
 #endif
-template <bool PROF, bool OCC>
+template <bool PROF, bool OCC, bool DYN>
 __device__ __forceinline__ void trace_stream(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
                                              uint32_t *stack, CoopLds coop, const WaveBufs &w, uint32_t round,
-                                             const uint32_t *pref, uint32_t *heads, float4 *res_all) {
+                                             const uint32_t *pref, uint32_t *heads, float4 *res_all,
+                                             uint32_t *l_next = nullptr, uint32_t sj = 0u, uint32_t sn = 0u) {
     constexpr uint32_t stride = WB;
     const uint32_t lane = __lane_id();
     // ---- the batch stream (wave-uniform)
-    const uint32_t total = pref[w.seg_count];
+    const uint32_t total = DYN ? pref[w.seg_count] : 0u;
     uint32_t x = blockIdx.x % kDynHeads, visited = 0u;
     uint32_t c0 = (uint32_t)((uint64_t)total * x / kDynHeads), c1 = (uint32_t)((uint64_t)total * (x + 1u) / kDynHeads);
     uint32_t bnext = 0u;
-    if (lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
+    if (DYN && lane == 0u) bnext = atomicAdd(heads + x * kDynStride, 1u);
     bool src_done = false;
     uint32_t qbase = 0u, qleft = 0u;  // the current batch's untaken queries: ray slots qbase ..
     // ---- this lane's query
@@ -239,7 +244,18 @@ __device__ __forceinline__ void trace_stream(const Scene &sc, const SubRoot *sub
             // new queries for the free lanes, in lane order from the stream
             unsigned long long want = wballot(!has);
             while (want != 0ull && !src_done) {  // wave-uniform
-                if (qleft == 0u) {
+                if (!DYN && qleft == 0u) {  // the workgroup's next batch of its segment
+                    uint32_t b = 0u;
+                    if (lane == 0u) b = __hip_atomic_fetch_add(l_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+                    if (b * 64u >= sn) {
+                        src_done = true;
+                        break;
+                    }
+                    qbase = sj * w.ray_stride + b * 64u;
+                    qleft = min(64u, sn - b * 64u);
+                }
+                if (DYN && qleft == 0u) {
                     for (;;) {  // the next batch of this wave's chunk, or of the next chunk
                         const uint32_t bi = c0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)bnext);
                         if (bi < c1) {
@@ -491,7 +507,7 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         const uint32_t lane = __lane_id();
         float4 *res_all = res_buf(w, round);
         if constexpr (PTX_TRACE_STREAM && LDS_TABLES && FLAT && !COUNT) {  // lane refill (trace_stream)
-            trace_stream<PROF, OCC>(sc, subs, insts, eps, stack, coop, w, round, pref, heads, res_all);
+            trace_stream<PROF, OCC, true>(sc, subs, insts, eps, stack, coop, w, round, pref, heads, res_all);
             return;
         }
         uint32_t x = blockIdx.x % kDynHeads, visited = 0u;
@@ -554,9 +570,18 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
     const uint32_t j = w.seg_phys + w.seg_base + local;  // physical queue slot
     const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
     if (share * WB >= n) return;  // (workgroup-uniform) nothing for this share
+    __shared__ uint32_t l_next;   // (trace_stream's batch counter)
+    if (threadIdx.x == 0u) l_next = 0u;  // (ordered by stage_tables' barrier)
     const LdsTables T = LDS_TABLES ? stage_tables(sc, wstack) : LdsTables{sc.subs, sc.insts};
     const SubRoot *subs = T.subs;
     const Inst *insts = T.insts;
+    if constexpr (PTX_TRACE_STREAM && LDS_TABLES && FLAT && !COUNT) {  // lane refill over the segment
+        if (K == 1u) {
+            trace_stream<PROF, OCC, false>(sc, subs, insts, eps, stack, coop, w, round, nullptr, nullptr,
+                                           res_buf(w, round), &l_next, j, n);
+            return;
+        }
+    }
     if (COUNT && sc.census)  // row census: this slot's queries count into its own block
         sc.counters = sc.census + (size_t)kCensusWords * ((sc.row_end - sc.row_begin + 7u) / 8u + j);
     for (uint32_t i0 = share * WB; i0 < n; i0 += K * WB) {  // workgroup-uniform
