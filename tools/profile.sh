@@ -12,6 +12,10 @@ cd /tmp && export TMPDIR=/tmp
 # pipeline's whole-band sequences use the dynamic trace batches (EXTRA_AB=TRACE_DYN=1 makes
 # the production region run the same kernel mode as bench.py's launch-timed region)
 export PTX_AB="WAVE_STREAMS=1,PIPELINE_FRAMES=0${EXTRA_AB:+,$EXTRA_AB}"
+# (the shipped libptx.so compiles these switches to their defaults since round 5: the profile
+# runs the measurement build of the same sources, make -C pathtracerdemo_amd/csrc ab)
+export PTX_LIB_PATH="${PTX_LIB_PATH:-$R/pathtracerdemo_amd/libptx_ab.so}"
+[ -f "$PTX_LIB_PATH" ] || { echo "missing $PTX_LIB_PATH (make -C pathtracerdemo_amd/csrc ab)"; exit 1; }
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
