@@ -423,7 +423,7 @@ __device__ __forceinline__ bool inst_may_hit(const Inst &I, f3 o, f3 winv, float
 #define PTX_INST_CULL 1
 #endif
 #ifndef PTX_EARLY_LEAF_K  // trace_core_flat's early leaf phase (0 = off)
-#define PTX_EARLY_LEAF_K 8
+#define PTX_EARLY_LEAF_K 16
 #endif
 #ifndef PTX_EARLY_LEAF_L
 #define PTX_EARLY_LEAF_L 4
