@@ -148,9 +148,6 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
 #ifndef PTX_TRACE_STREAM
 #define PTX_TRACE_STREAM 1
 #endif
-#ifndef PTX_STREAM_NODE_BREAK
-#define PTX_STREAM_NODE_BREAK 0
-#endif
 template <bool PROF, bool OCC, bool DYN>
 __device__ __forceinline__ void trace_stream(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
                                              uint32_t *stack, CoopLds coop, const WaveBufs &w, uint32_t round,
@@ -345,8 +342,7 @@ __device__ __forceinline__ void trace_stream(const Scene &sc, const SubRoot *sub
                 }
             }
         }
-        // ---- node loop (trace_core_flat's, with its early leaf phase; PTX_STREAM_NODE_BREAK = K:
-        // also left once at most K lanes descend while enough lanes wait for new queries)
+        // ---- node loop (trace_core_flat's, with its early leaf phase)
         for (;;) {
             const bool want = has && leaf == 0u && (sp >= 0 || mask != 0u);
             const unsigned long long wm = wballot(want);
@@ -354,11 +350,6 @@ __device__ __forceinline__ void trace_stream(const Scene &sc, const SubRoot *sub
             if constexpr (PTX_EARLY_LEAF_K > 0) {
                 if (__builtin_popcountll(wm) <= PTX_EARLY_LEAF_K &&
                     __builtin_popcountll(wballot(leaf != 0u)) >= PTX_EARLY_LEAF_L)
-                    break;
-            }
-            if constexpr (PTX_STREAM_NODE_BREAK > 0) {
-                if (!src_done && __builtin_popcountll(wm) <= PTX_STREAM_NODE_BREAK &&
-                    __builtin_popcountll(wballot(!(has && !done))) >= PTX_STREAM_REFILL)
                     break;
             }
             if (PROF && want) pf.hit(PROF_NODE);
