@@ -1026,7 +1026,10 @@ bool pipelined(const ptx_handle *h) {
     // unpipelined, 474.9 pipelined.)  PTX_AB=PIPE_MAX_KPX=<n>: A/B
     static const size_t max_px = (size_t)ab_knob("PIPE_MAX_KPX", 16384) << 10;
     const size_t px = (size_t)h->band_h * h->cfg.width;
-    return !off && !(band && bands_off) && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE &&
+    // (ReSTIR GI: whole-image handles; its band frames stay one frame at a time)
+    const bool pipe_kind = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ||
+                           (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI && !band);
+    return !off && !(band && bands_off) && pipe_kind &&
            px <= max_px &&
            !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK |
                    PTX_FLAG_TIME_LAUNCHES | PTX_FLAG_SINGLE_STREAM | PTX_FLAG_ROW_CENSUS)) &&
@@ -1068,6 +1071,7 @@ static void swap_two(ptx_handle *h) {
     std::swap(h->d_wres2, a.wres2);
     std::swap(h->d_tjstate, a.tjstate);
     std::swap(h->d_tjres, a.tjres);
+    std::swap(h->d_direct, a.direct);  // (GI: the direct light PT_1's init writes and the shade reads)
     std::swap(h->d_wact0, a.wact0);
     std::swap(h->d_wact1, a.wact1);
     std::swap(h->d_wctr, a.wctr);
@@ -1111,6 +1115,14 @@ int ensure_alt(ptx_handle *h) {
             if (int rc = alloc_buf(h, *rs[c], rbytes)) return rc;
             HIP_CHECK(h, memset_sync(h, rs[c]->p, 0, rs[c]->bytes));
         }
+    }
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {  // GI: each context's direct light too
+        DevBuf *ds[3] = {&h->d_direct, &h->alt.direct, &h->alt2.direct};
+        for (int c = 0; c < pipe_depth(); ++c)
+            if (!ds[c]->p) {
+                if (int rc = alloc_buf(h, *ds[c], h->d_direct.bytes)) return rc;
+                HIP_CHECK(h, memset_sync(h, ds[c]->p, 0, ds[c]->bytes));
+            }
     }
     return PTX_OK;
 }
@@ -1167,7 +1179,9 @@ static int timed_wave_frame(ptx_handle *h) {
         // wait, its combine after; PTX_AB=TEMPORAL_SPLIT=0: the whole pass after the wait)
         // (a moved camera: the whole motion temporal pass after the wait -- its history jobs read
         // the previous frame's spatial output)
-        static const bool split = ab_knob("TEMPORAL_SPLIT", 1) != 0;
+        // (GI: its temporal pass is one per-pixel launch without rays -- never split)
+        static const bool split_on = ab_knob("TEMPORAL_SPLIT", 1) != 0;
+        const bool split = split_on && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE;
         static const int front[2] = {PTX_PASS_GBUFFER, PTX_PASS_INIT};
         static const int jobs[1] = {kPassTemporalJobs};
         static const int temporal[1] = {PTX_PASS_TEMPORAL}, temporal_b[1] = {kPassTemporalCombine};
@@ -1757,7 +1771,7 @@ int ptx_destroy(ptx_handle *h) {
     for (ptx_handle::FrameCtx *ap : {&h->alt, &h->alt2}) {
         ptx_handle::FrameCtx &a = *ap;
         for (DevBuf *b : {&a.gbuf, &a.res, &a.nbr, &a.surf, &a.wstate, &a.wrays, &a.wres0, &a.wres1, &a.wres2, &a.wact0, &a.wact1,
-                          &a.wctr, &a.tjstate, &a.tjres})
+                          &a.wctr, &a.tjstate, &a.tjres, &a.direct})
             free_buf(*b);
         if (a.ev_fork) (void)hipEventDestroy(a.ev_fork);
         for (int q = 0; q < ptx_handle::kMaxSplit; ++q) {

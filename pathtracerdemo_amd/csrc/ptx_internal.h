@@ -113,7 +113,7 @@ struct ptx_handle {
     // ptx_render swaps the members above with `alt` per frame, so everything else always sees
     // the latest frame's buffers; the shared ones (accumulation, history, jobs, scene) never move.
     struct FrameCtx {
-        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wres2, wact0, wact1, wctr, wpool, tjstate, tjres;
+        DevBuf gbuf, res, nbr, surf, wstate, wrays, wres0, wres1, wres2, wact0, wact1, wctr, tjstate, tjres, direct;
         size_t wave_ray_cap = 0;
         uint32_t wave_slots = 0;
         hipStream_t stream = nullptr;
