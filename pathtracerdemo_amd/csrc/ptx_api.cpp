@@ -742,6 +742,16 @@ hipError_t spatial_summaries(ptx_handle *h, hipStream_t st) {
 }
 
 static bool whole_band_sequences(const ptx_handle *h);
+// Dynamic trace batches (trace_queue's launch-wide batch stream) for the whole-band launch
+// sequences of a whole-image handle; a band handle (halo rows or a communicator) keeps one slot per
+// workgroup -- measured at the streamed walk on configs[3]'s 8 re-cut bands, each alone with the
+// exchange proxy: static 2.34-2.50 ms against dynamic 2.45-2.56 (the headline: dynamic 515 against
+// static 506-510 Msamples/s; tools/cl/r5_bands2.sh).  PTX_AB=TRACE_DYN=0 / 1 forces it off / on.
+static bool use_dyn_batches(const ptx_handle *h) {
+    static const int dyn_env = ab_knob("TRACE_DYN", -1);
+    const bool band = h->comm || h->halo_top || h->halo_bot;
+    return dyn_env == 1 || (dyn_env != 0 && whole_band_sequences(h) && !band);
+}
 // A band's spatial pass + PT_4 with the halo in flight (PTX_FLAG_HALO_OVERLAP): only the start
 // kernel runs per tile set -- the interior rows' shift jobs (their neighbourhood lies inside the
 // band) while the halo is in flight, the edge rows' once it has landed (`halo`) -- and every
@@ -760,8 +770,7 @@ static hipError_t spatial_overlap_seq(ptx_handle *h, const Scene &sc, const Wave
     int k = env_bk > 0 && h->alt_stream && pipelined(h) ? env_bk : 1;
     if (h->cfg.flags & PTX_FLAG_SINGLE_STREAM) k = 1;
     k = std::max(1, std::min<int>({k, ptx_handle::kMaxSplit, (int)interior.nseg, (int)edge.nseg}));
-    static const int dyn_env = ab_knob("TRACE_DYN", -1);
-    const bool use_dyn = dyn_env == 1 || (dyn_env != 0 && whole_band_sequences(h));
+    const bool use_dyn = use_dyn_batches(h);
     const size_t dyn0 = 2u * kWaveMaxRounds * (size_t)interior.cnt_stride;
     ReuseArgs A = reuse_args(h, PTX_PASS_SPATIAL);
     const bool fold = A.fold_last && interior.res[2];
@@ -903,8 +912,7 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
             // already fill a launch's tail and the per-workgroup prefix costs more than it
             // saves (1080p, static vs dynamic: ReSTIR 1240 vs 1081, GI 675 vs 625, TEST_MCPT
             // 1264 vs 1229 Msamples/s).  PTX_AB=TRACE_DYN=0 / 1 forces it off / on.
-            static const int dyn_env = ab_knob("TRACE_DYN", -1);
-            const bool use_dyn = dyn_env == 1 || (dyn_env != 0 && whole_band_sequences(h));
+            const bool use_dyn = use_dyn_batches(h);
             part.dyn = !use_dyn ? nullptr
                                : (uint32_t *)h->d_wctr.p + 2u * kWaveMaxRounds * ws.cnt_stride +
                                      (uint32_t)((set * ptx_handle::kMaxSplit + q) * kWaveMaxRounds) * kDynRoundWords;
