@@ -1018,7 +1018,8 @@ static bool whole_band_sequences(const ptx_handle *h) {
     const uint32_t fl = h->cfg.flags;
     const bool timed_alone = (fl & PTX_FLAG_TIME_LAUNCHES) && (fl & PTX_FLAG_SINGLE_STREAM);
     return (h->alt_stream && pipelined(h)) ||
-           (timed_alone && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !h->comm && !h->halo_top && !h->halo_bot &&
+           (timed_alone && (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE || h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) &&
+            !h->comm && !h->halo_top && !h->halo_bot &&
             (size_t)h->band_h * h->cfg.width <= ((size_t)4u << 20));
 }
 bool pipelined(const ptx_handle *h) {

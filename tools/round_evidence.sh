@@ -7,7 +7,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
 ROUND=${ROUND:-r1}
 for WL in ${WORKLOADS:-reuse restir mcpt}; do
-  DYN=""; [ "$WL" = "reuse" ] && DYN=TRACE_DYN=1
+  DYN=""; { [ "$WL" = "reuse" ] || [ "$WL" = "gi" ]; } && DYN=TRACE_DYN=1
   EXTRA_AB=$DYN TAG=${ROUND}_$WL BENCH_ARGS="--workload $WL" bash tools/profile.sh || { echo "profile $WL failed"; exit 1; }
   timeout -k 10 400 python3 bench.py --workload "$WL" --steps 20 --warmup 3 > "gpurun_out/bench_${ROUND}_$WL.log" 2>&1 \
     || { echo "bench $WL failed"; exit 1; }
