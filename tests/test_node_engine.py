@@ -12,8 +12,9 @@ methods equal the Python host's restatement bit for bit.
 GPU: along a scripted path (WASD + Q/E moves, a mouse turn, still frames, a resize) every
 uniform the JS host writes equals the Python restatement of the same loop, and the accumulated
 image after several ticks is bit-identical to the oracle rendering the same uniforms -- the
-reuse pipeline on C3 (its temporal pass reprojecting the history under the motion) and the
-reference pipeline on C1; after the resize the frames come out at the new size.
+reuse pipeline on C3 (its temporal pass reprojecting the history under the motion), ReSTIR GI
+on C3 (the same for its GI history) and the reference pipeline on C1; after the resize the
+frames come out at the new size.
 """
 import json
 import os
@@ -136,7 +137,8 @@ def test_native_renderer_constructor_forms():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("which,pipeline,W,H", [("scene3", "reuse", 96, 64), ("scene1", "restir", 64, 48)])
+@pytest.mark.parametrize("which,pipeline,W,H", [("scene3", "reuse", 96, 64), ("scene1", "restir", 64, 48),
+                                                ("scene3", "gi", 64, 48)])
 def test_engine_loop_bit_exact(request, oracle_mod, tmp_path, which, pipeline, W, H):
     from pathtracerdemo_amd.scene.export import export_compiled
     cs = request.getfixturevalue(which)
@@ -165,6 +167,8 @@ def test_engine_loop_bit_exact(request, oracle_mod, tmp_path, which, pipeline, W
             fr.set_frame_index(int(u[23]))
         if pipeline == "reuse":
             fr.run_reuse_frame(threads=16)
+        elif pipeline == "gi":
+            fr.run_gi_frame(threads=16)
         else:
             fr.run(oracle_mod.PASS_RESTIR, threads=16)
         if t in DUMP:
@@ -173,5 +177,5 @@ def test_engine_loop_bit_exact(request, oracle_mod, tmp_path, which, pipeline, W
             img = np.fromfile(f"{out}.{t}", dtype=np.float32).reshape(h, w, 4)
             np.testing.assert_array_equal(img.view(np.uint32), fr.accum.view(np.uint32), f"radiance, tick {t}")
     assert [t["uniform"][23] for t in ticks] == [1, 1, 1, 1, 1, 1, 2, 3, 1, 1, 2]
-    if pipeline == "reuse":
+    if pipeline in ("reuse", "gi"):
         assert moved_frames >= 4  # the temporal pass reprojected its history on the moved frames
