@@ -4,7 +4,9 @@ one handle, its own streams), each timed alone on the idle GPU with bench.calibr
 (the band path a rank runs, pipelined, without the exchange: PTX_FLAG_HALO_SKIP).
 `tools/band_timing.py` times all bands from one process, where 9 handles' streams share the
 process's hardware queues.  usage: python tools/band_alone.py [--world 8] [--bands census|calibrated]
-prints one JSON line: bands, per-band ms, max/mean, implied speedup over the one-GPU frame."""
+prints one JSON line: bands, per-band ms, max/mean, implied speedup over the one-GPU frame.
+(The exchange proxy, PTX_AB=HALO_PROXY_US=<us>, is an A/B switch: run it with
+PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so, the measurement build.)"""
 import argparse
 import json
 import os

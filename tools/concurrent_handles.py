@@ -1,7 +1,10 @@
 """Throughput of H whole-frame handles rendering concurrently (each on its own streams) vs one:
 an upper-bound experiment for pipelining consecutive frames.
 
-usage: PTX_AB=WAVE_STREAMS=2 python tools/concurrent_handles.py --handles 2 [--steps 20]"""
+usage: PTX_AB=WAVE_STREAMS=2 PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so \
+           python tools/concurrent_handles.py --handles 2 [--steps 20]
+(WAVE_STREAMS is an A/B switch: only the measurement build, make -C pathtracerdemo_amd/csrc ab,
+reads it)"""
 import argparse
 import json
 import os

@@ -18,6 +18,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ["PTX_AB"] = ",".join(v for v in (os.environ.get("PTX_AB", ""), "TRACE_PROF") if v)
+# (TRACE_PROF is an A/B switch: only the measurement build reads it -- make -C pathtracerdemo_amd/csrc ab)
+os.environ.setdefault("PTX_LIB_PATH", os.path.join(ROOT, "pathtracerdemo_amd", "libptx_ab.so"))
+if not os.path.exists(os.environ["PTX_LIB_PATH"]):
+    sys.exit(f"{os.environ['PTX_LIB_PATH']} missing: make -C pathtracerdemo_amd/csrc ab")
 
 from pathtracerdemo_amd import _native as N  # noqa: E402
 from pathtracerdemo_amd.renderer import Renderer  # noqa: E402
