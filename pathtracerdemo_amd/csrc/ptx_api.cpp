@@ -121,6 +121,14 @@ uint4 *hist_band(ptx_handle *h) { return (uint4 *)h->d_hist.p + h->res_u4 * (siz
 bool has_reuse(const ptx_handle *h) {
     return h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE || h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI;
 }
+// ReSTIR without reuse pipelines its frames too: frame N + 1's G-buffer + PT_1 beside frame N's
+// PT_4 (C1 1080p, one sequence per context at 768-pixel segments: 1536-1543 Msamples/s against
+// 1406-1414 one frame at a time; PTX_AB=PIPE_RESTIR=0: A/B).  Its timed-alone region keeps static
+// slots, as its pipelined frames do (use_dyn_batches).
+static bool restir_pipe() {
+    static const bool on = ab_knob("PIPE_RESTIR", 1) != 0;
+    return on;
+}
 
 static inline float as_f32(uint32_t u) {
     float f;
@@ -416,8 +424,16 @@ void resolve_event(TimedLaunch &t, ptx_handle *h) {
 static uint32_t seg_pixels(const ptx_handle *h) {
     static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);
     if (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) return env_px;
-    if (h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) return kWaveSegPixels;
     const size_t npx = (size_t)h->band_h * h->cfg.width;
+    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR && restir_pipe()) {
+        // ReSTIR (pipelined frames, and the same segments timed alone): ~1150 segments (static
+        // trace slots, one workgroup each).  C1 1080p, 2 sequences per context: 1536 / 1792 /
+        // 2048 / 2560 px 1695 / 1717 / 1703 / 1697 Msamples/s, the trace launches 0.538 / 0.563 /
+        // 0.550 / 0.531 of the roofline (tools/cl/r5_piperestir5.sh); 768 below 1 Mpx
+        const size_t p = (npx / 1152u + 128u) / 256u * 256u;
+        return (uint32_t)std::min<size_t>(4096u, std::max<size_t>(kWaveSegPixels, p));
+    }
+    if (h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) return kWaveSegPixels;
     uint32_t p = 512u;
     while (p < 4096u && (size_t)(2u * p) * 1500u <= npx) p *= 2u;
     return p;
@@ -750,7 +766,11 @@ static bool whole_band_sequences(const ptx_handle *h);
 static bool use_dyn_batches(const ptx_handle *h) {
     static const int dyn_env = ab_knob("TRACE_DYN", -1);
     const bool band = h->comm || h->halo_top || h->halo_bot;
-    return dyn_env == 1 || (dyn_env != 0 && whole_band_sequences(h) && !band);
+    // (ReSTIR without reuse keeps static slots in its pipelined frames: C1 1080p 1536-1543
+    // Msamples/s against 1431-1443 with dynamic batches, 1406-1414 one frame at a time;
+    // tools/cl/r5_piperestir2.sh)
+    return dyn_env == 1 ||
+           (dyn_env != 0 && whole_band_sequences(h) && !band && h->cfg.pipeline != PTX_PIPELINE_RESTIR);
 }
 // A band's spatial pass + PT_4 with the halo in flight (PTX_FLAG_HALO_OVERLAP): only the start
 // kernel runs per tile set -- the interior rows' shift jobs (their neighbourhood lies inside the
@@ -847,8 +867,11 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     // sequence (whole-band launches, dynamic trace batches); measured at 1080p C3 reuse: 1
     // stream per context 338 Msamples/s, 2 streams 308, unpipelined 3 streams 320
     // (PTX_AB=PIPE_STREAMS=k: A/B)
+    // (ReSTIR without reuse: 2 per context, C1 1080p at 1792-pixel segments 1717 against 1620
+    // with one; three 1294 -- tools/cl/r5_piperestir4.sh, r5_piperestir5.sh)
     static const int env_pk = ab_knob("PIPE_STREAMS", 0);
-    int k = h->alt_stream && pipelined(h) ? (env_pk > 0 ? env_pk : 1) : env_k > 0 ? env_k : 3;
+    const int pipe_k = env_pk > 0 ? env_pk : h->cfg.pipeline == PTX_PIPELINE_RESTIR ? 2 : 1;
+    int k = h->alt_stream && pipelined(h) ? pipe_k : env_k > 0 ? env_k : 3;
     // a pipelined frame's spatial pass + PT_4 (the serial back half every frame waits for) as
     // two launch sequences: one half's trace rounds overlap the other's logic kernels.  Same
     // box, 1080p C3 reuse: 1 sequence 387.2, 2: 396.1, 3: 369.7 Msamples/s (3 contexts' streams
@@ -1037,7 +1060,8 @@ bool pipelined(const ptx_handle *h) {
     const size_t px = (size_t)h->band_h * h->cfg.width;
     // (ReSTIR GI: whole-image handles; its band frames stay one frame at a time)
     const bool pipe_kind = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ||
-                           (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI && !band);
+                           (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI && !band) ||
+                           (h->cfg.pipeline == PTX_PIPELINE_RESTIR && !band && restir_pipe());
     return !off && !(band && bands_off) && pipe_kind &&
            px <= max_px &&
            !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK |
@@ -1180,7 +1204,14 @@ static int timed_wave_frame(ptx_handle *h) {
     resolve_event(t, h);
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
     hipError_t e;
-    if (pipe) {
+    if (pipe && !has_reuse(h)) {
+        // ReSTIR: G-buffer + PT_1 of this frame overlap the previous frame's PT_4, whose
+        // accumulation this frame's PT_4 follows (ev_prev)
+        static const int front[2] = {PTX_PASS_GBUFFER, PTX_PASS_INIT}, back[1] = {PTX_PASS_FINAL};
+        e = launch_wave_parts(h, sc, w, front, 2);
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
+        if (e == hipSuccess) e = launch_wave_parts(h, sc, w, back, 1);
+    } else if (pipe) {
         // G-buffer + PT_1 of this frame overlap the previous frame's spatial pass + PT_4; the
         // temporal pass reads that frame's spatial output (d_hist) and shares its job buffers
         if (int rc = reuse_buffers(h)) return rc;

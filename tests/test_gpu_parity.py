@@ -138,6 +138,31 @@ def test_mcpt_full_hd_window_bit_exact(scene1, oracle_mod):
     assert np.isfinite(img).all()
 
 
+def test_restir_full_hd_pipelined_window_bit_exact(scene1, oracle_mod, native):
+    """configs[0]'s pipeline at 1920x1080 through Render(): ReSTIR frames two in flight (frame
+    N + 1's G-buffer + PT_1 beside frame N's PT_4) with the large segments and two launch
+    sequences per context that size takes; FrameIndex 1..3 accumulated, then 3 row windows of
+    the image and of the last frame's reservoirs against the oracle, bit for bit (ReSTIR
+    without reuse is per pixel)."""
+    W, H = 1920, 1080
+    r = make_renderer(scene1, W, H)
+    fr = oracle_frame(oracle_mod, scene1, W, H)
+    windows = [(0, 10), (536, 546), (1070, 1080)]
+    for f in (1, 2, 3):
+        r.Update()
+        r.Render()
+        fr.set_frame_index(f)
+        for y0, y1 in windows:
+            fr.run(oracle_mod.PASS_RESTIR, 16, (0, y0, W, y1))
+    img = r.read_image()
+    res = r.read_reservoir()
+    for y0, y1 in windows:
+        np.testing.assert_array_equal(img[y0:y1].view(np.uint32), fr.accum[y0:y1].view(np.uint32))
+        np.testing.assert_array_equal(res[y0:y1], fr.reservoir[y0:y1])
+    assert np.isfinite(img).all()
+    assert r.stats()["frames"] == 3
+
+
 @pytest.mark.parametrize("variant", ["simple"])
 def test_alternate_variants(scene1, oracle_mod, native, variant):
     """The A/B kernel variants obey the same bars as the default wavefront path."""
