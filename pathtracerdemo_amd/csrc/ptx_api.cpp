@@ -129,6 +129,20 @@ static bool restir_pipe() {
     static const bool on = ab_knob("PIPE_RESTIR", 1) != 0;
     return on;
 }
+// The DI reuse pipeline's whole-image frames on the same launch shape as the others' (static
+// trace slots, ~1150 segments, 2 front sequences per context) instead of dynamic batches over
+// 1024-pixel segments (PTX_AB=REUSE_STATIC=0: A/B); its bands keep their own segments
+static bool reuse_static() {
+    static const bool on = ab_knob("REUSE_STATIC", 1) != 0;
+    return on;
+}
+// TEST_MCPT likewise: frame N + 1's paths beside frame N's, each frame's colours mixed into the
+// accumulation after the previous frame's (C1 1080p at 1792-pixel segments, 2 sequences per
+// context: 1744-1758 Msamples/s against 1509-1515 one frame at a time; PTX_AB=PIPE_MCPT=0: A/B)
+static bool mcpt_pipe() {
+    static const bool on = ab_knob("PIPE_MCPT", 1) != 0;
+    return on;
+}
 
 static inline float as_f32(uint32_t u) {
     float f;
@@ -425,11 +439,16 @@ static uint32_t seg_pixels(const ptx_handle *h) {
     static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);
     if (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) return env_px;
     const size_t npx = (size_t)h->band_h * h->cfg.width;
-    if (h->cfg.pipeline == PTX_PIPELINE_RESTIR && restir_pipe()) {
-        // ReSTIR (pipelined frames, and the same segments timed alone): ~1150 segments (static
-        // trace slots, one workgroup each).  C1 1080p, 2 sequences per context: 1536 / 1792 /
-        // 2048 / 2560 px 1695 / 1717 / 1703 / 1697 Msamples/s, the trace launches 0.538 / 0.563 /
-        // 0.550 / 0.531 of the roofline (tools/cl/r5_piperestir5.sh); 768 below 1 Mpx
+    const bool band = h->comm || h->halo_top || h->halo_bot || (h->cfg.flags & PTX_FLAG_HALO_SKIP);
+    if ((h->cfg.pipeline == PTX_PIPELINE_RESTIR && restir_pipe()) || (h->cfg.pipeline == PTX_PIPELINE_MCPT && mcpt_pipe()) ||
+        h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI || (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !band && reuse_static())) {
+        // ReSTIR, TEST_MCPT and GI: ~1150 segments (1792 px at 1080p), 768 below 1 Mpx; the
+        // pipelined frames and the same segments timed alone.  C1 1080p, static trace slots (one
+        // workgroup per segment), 2 sequences per context -- ReSTIR: 1536 / 1792 / 2048 / 2560 px
+        // 1695 / 1717 / 1703 / 1697 Msamples/s, the trace launches 0.538 / 0.563 / 0.550 / 0.531
+        // of the roofline (tools/cl/r5_piperestir5.sh); TEST_MCPT: 1024 / 1792 px 1715-1722 /
+        // 1744-1758, 0.88 / 0.92 (r5_pipemcpt2.sh).  GI C3 1080p: 768 / 1280 / 1536 / 1792 / 2048 px
+        // 1033-1043 / 1052-1060 / 1061-1076 / 1078-1083 / 1059-1061 (r5_segall.sh, r5_giseg.sh)
         const size_t p = (npx / 1152u + 128u) / 256u * 256u;
         return (uint32_t)std::min<size_t>(4096u, std::max<size_t>(kWaveSegPixels, p));
     }
@@ -457,14 +476,14 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     // a band's spatial pass: ceil(a/s) + ceil(b/s) <= ceil((a+b)/s) + 1)
     const size_t slots = nseg + 1u;
     const size_t cap = per_px * seg_px * slots;
-    if (!h->d_wstate.p) {
-        if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wact0, slots * seg_px * jpp * 4u)) return rc;
-        if (int rc = alloc_buf(h, h->d_wact1, slots * seg_px * jpp * 4u)) return rc;
-        // counts per round and slot, then the dynamic-batch counters of trace_queue: one per
-        // (tile set, launch sequence, round) -- kDynCounters words
-        if (int rc = alloc_buf(h, h->d_wctr, (2u * kWaveMaxRounds * slots + kDynCounters) * 4u)) return rc;
-    }
+    // (sized by the segment size, which depends on the handle's band state: re-checked every call,
+    // alloc_buf keeps a buffer of the right size)
+    if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
+    if (int rc = alloc_buf(h, h->d_wact0, slots * seg_px * jpp * 4u)) return rc;
+    if (int rc = alloc_buf(h, h->d_wact1, slots * seg_px * jpp * 4u)) return rc;
+    // counts per round and slot, then the dynamic-batch counters of trace_queue: one per
+    // (tile set, launch sequence, round) -- kDynCounters words
+    if (int rc = alloc_buf(h, h->d_wctr, (2u * kWaveMaxRounds * slots + kDynCounters) * 4u)) return rc;
     if (cap > h->wave_ray_cap) {
         free_buf(h->d_wrays);
         free_buf(h->d_wres0);
@@ -724,7 +743,7 @@ static hipError_t launch_wave_seq(ptx_handle *h, const Scene &sc, const WaveBufs
         TimedLaunch *t = event_begin(h, PTX_STAT_WAVE_LOGIC, st);
         e = pass == PTX_PASS_INIT    ? wave_init_round(sc, w, r, gb, res, st)
             : pass == PTX_PASS_FINAL ? wave_final_round(sc, w, r, gb, fres, acc, st)
-                                     : wave_mcpt_round(sc, w, r, acc, st);
+                                     : wave_mcpt_round(sc, w, r, acc, h->mcpt_color, st);
         event_end(t, st);
     }
     return e;
@@ -766,11 +785,14 @@ static bool whole_band_sequences(const ptx_handle *h);
 static bool use_dyn_batches(const ptx_handle *h) {
     static const int dyn_env = ab_knob("TRACE_DYN", -1);
     const bool band = h->comm || h->halo_top || h->halo_bot;
-    // (ReSTIR without reuse keeps static slots in its pipelined frames: C1 1080p 1536-1543
-    // Msamples/s against 1431-1443 with dynamic batches, 1406-1414 one frame at a time;
-    // tools/cl/r5_piperestir2.sh)
+    // (ReSTIR without reuse, TEST_MCPT and GI keep static slots in their pipelined frames: C1
+    // 1080p ReSTIR 1536-1543 Msamples/s against 1431-1443 with dynamic batches, 1406-1414 one
+    // frame at a time (tools/cl/r5_piperestir2.sh); TEST_MCPT 1663-1668 against 1598-1609,
+    // 1509-1515 (r5_pipemcpt.sh); GI C3 at 1792-pixel segments 1104-1107 against 1082
+    // (r5_pipemcpt3.sh))
     return dyn_env == 1 ||
-           (dyn_env != 0 && whole_band_sequences(h) && !band && h->cfg.pipeline != PTX_PIPELINE_RESTIR);
+           (dyn_env != 0 && whole_band_sequences(h) && !band && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE &&
+            !reuse_static());
 }
 // A band's spatial pass + PT_4 with the halo in flight (PTX_FLAG_HALO_OVERLAP): only the start
 // kernel runs per tile set -- the interior rows' shift jobs (their neighbourhood lies inside the
@@ -867,10 +889,12 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     // sequence (whole-band launches, dynamic trace batches); measured at 1080p C3 reuse: 1
     // stream per context 338 Msamples/s, 2 streams 308, unpipelined 3 streams 320
     // (PTX_AB=PIPE_STREAMS=k: A/B)
-    // (ReSTIR without reuse: 2 per context, C1 1080p at 1792-pixel segments 1717 against 1620
-    // with one; three 1294 -- tools/cl/r5_piperestir4.sh, r5_piperestir5.sh)
+    // (ReSTIR without reuse, TEST_MCPT and GI: 2 per context -- C1 1080p ReSTIR at 1792-pixel
+    // segments 1717 against 1620 with one, three 1294 (tools/cl/r5_piperestir4.sh,
+    // r5_piperestir5.sh); TEST_MCPT 1744-1758 against 1706-1714 (r5_pipemcpt2.sh); GI on static
+    // slots 1111-1113 against 1104-1107 (r5_pipemcpt3.sh))
     static const int env_pk = ab_knob("PIPE_STREAMS", 0);
-    const int pipe_k = env_pk > 0 ? env_pk : h->cfg.pipeline == PTX_PIPELINE_RESTIR ? 2 : 1;
+    const int pipe_k = env_pk > 0 ? env_pk : h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !reuse_static() ? 1 : 2;
     int k = h->alt_stream && pipelined(h) ? pipe_k : env_k > 0 ? env_k : 3;
     // a pipelined frame's spatial pass + PT_4 (the serial back half every frame waits for) as
     // two launch sequences: one half's trace rounds overlap the other's logic kernels.  Same
@@ -1061,7 +1085,8 @@ bool pipelined(const ptx_handle *h) {
     // (ReSTIR GI: whole-image handles; its band frames stay one frame at a time)
     const bool pipe_kind = h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE ||
                            (h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI && !band) ||
-                           (h->cfg.pipeline == PTX_PIPELINE_RESTIR && !band && restir_pipe());
+                           (h->cfg.pipeline == PTX_PIPELINE_RESTIR && !band && restir_pipe()) ||
+                           (h->cfg.pipeline == PTX_PIPELINE_MCPT && !band && mcpt_pipe());
     return !off && !(band && bands_off) && pipe_kind &&
            px <= max_px &&
            !(fl & (PTX_FLAG_SIMPLE_KERNELS | PTX_FLAG_COUNT_WORK |
@@ -1204,7 +1229,21 @@ static int timed_wave_frame(ptx_handle *h) {
     resolve_event(t, h);
     HIP_CHECK(h, hipEventRecord(t.start, h->stream));
     hipError_t e;
-    if (pipe && !has_reuse(h)) {
+    if (pipe && h->cfg.pipeline == PTX_PIPELINE_MCPT) {
+        // TEST_MCPT: this frame's paths overlap the previous frame's; their colours are kept per
+        // pixel (this context's d_direct) and mixed in after the previous frame's mix (ev_prev)
+        if (int rc = alloc_buf(h, h->d_direct, (size_t)h->band_h * h->cfg.width * 16u)) return rc;
+        static const int mcpt[1] = {PTX_PASS_MCPT};
+        h->mcpt_color = (float4 *)h->d_direct.p;
+        e = launch_wave_parts(h, sc, w, mcpt, 1);
+        h->mcpt_color = nullptr;
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_prev, 0);
+        if (e == hipSuccess) {
+            TimedLaunch *tl = event_begin(h, PTX_STAT_WAVE_LOGIC, h->stream);
+            e = wave_mix_frame(sc, (const float4 *)h->d_direct.p, (float4 *)h->d_accum.p, h->stream);
+            event_end(tl, h->stream);
+        }
+    } else if (pipe && !has_reuse(h)) {
         // ReSTIR: G-buffer + PT_1 of this frame overlap the previous frame's PT_4, whose
         // accumulation this frame's PT_4 follows (ev_prev)
         static const int front[2] = {PTX_PASS_GBUFFER, PTX_PASS_INIT}, back[1] = {PTX_PASS_FINAL};
@@ -1326,7 +1365,7 @@ static bool buffer_view(ptx_handle *h, int which, DevBuf &v) {
     switch (which) {
     case PTX_BUF_GBUFFER: v.p = gbuf_band(h); v.bytes = px * 16u; return true;
     case PTX_BUF_RESERVOIR: v.p = res_band(h); v.bytes = px * 16u * h->res_u4; return true;
-    case PTX_BUF_DIRECT: v = h->d_direct; return v.p != nullptr;
+    case PTX_BUF_DIRECT: v = h->d_direct; return v.p != nullptr && h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI;
     case PTX_BUF_ACCUM: v = h->d_accum; return true;
     case PTX_BUF_COUNTERS: v = h->d_counters; return true;
     case PTX_BUF_RESERVOIR_HIST: v.p = h->d_hist.p ? hist_band(h) : nullptr; v.bytes = px * 16u * h->res_u4; return v.p != nullptr;
@@ -1600,6 +1639,10 @@ int ptx_render(ptx_handle *h, float *rgba_out) {
         if (rc == 1)  // counting builds: pass by pass
             for (int p : {PTX_PASS_GBUFFER, PTX_PASS_INIT, PTX_PASS_TEMPORAL, PTX_PASS_SPATIAL, PTX_PASS_FINAL})
                 if ((rc = timed_launch(h, p))) return rc;
+    } else if (pipelined(h)) {  // TEST_MCPT frames two in flight
+        int rc = timed_wave_frame(h);
+        if (rc < 0) return rc;
+        if (rc == 1 && (rc = timed_launch(h, PTX_PASS_MCPT))) return rc;
     } else {
         if (int rc = timed_launch(h, PTX_PASS_MCPT)) return rc;
     }

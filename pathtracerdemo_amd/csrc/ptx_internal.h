@@ -81,6 +81,9 @@ struct ptx_handle {
     DevBuf d_surf;
     bool surf_valid = false;
     uint32_t reuse_radius = 0, reuse_neighbors = 0, temporal_cap = 0;
+    // set while a pipelined TEST_MCPT frame's pass is enqueued: its path colours go to this
+    // context's d_direct, mixed into d_accum after the previous frame's (wave_mix_frame)
+    float4 *mcpt_color = nullptr;
     bool hist_valid = false;           // d_hist holds the previous frame of this camera/scene
     uint32_t hist_camera[19] = {0};    // uniform words 4..22 of the frame that wrote d_hist
     // the camera moved since d_hist's frame (whole-image DI reuse handles): ptx_render reprojects

@@ -110,7 +110,11 @@ hipError_t wave_final_round(const Scene &sc, const WaveBufs &w, int round, const
 hipError_t wave_gbuffer(const Scene &sc, const WaveBufs &w, uint4 *gbuf, uint32_t stack_depth, hipStream_t s);
 hipError_t launch_trace_rays_sm(const Scene &sc, const float4 *rays, float4 *hits, uint32_t n, int eps_mode,
                                 uint32_t stack_depth, hipStream_t s);
-hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, hipStream_t s);
+// color: nullptr mixes every finished path into accum (WriteColor); else the path colours go to
+// color (a pipelined frame) and wave_mix_frame mixes them in after the previous frame's
+hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, float4 *color,
+                           hipStream_t s);
+hipError_t wave_mix_frame(const Scene &sc, const float4 *color, float4 *accum, hipStream_t s);
 
 // reuse passes (ptx_reuse.hip): round 0 start, 1..kWaveRoundsReuse step, then combine
 constexpr int kWaveRoundsReuse = 3;

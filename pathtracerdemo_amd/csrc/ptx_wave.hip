@@ -1426,6 +1426,12 @@ __device__ __forceinline__ void wmcpt_vertex(const Scene &sc, const Seg &g, bool
     }
 }
 
+// a finished path's colour: WriteColor into the accumulation, or (a pipelined frame, `color`
+// set) kept per pixel for wmix_frame, which mixes it in after the previous frame's
+__device__ __forceinline__ void mcpt_out(const Scene &sc, float4 *accum, float4 *color, uint32_t pix, f3 c) {
+    if (color) color[pix] = make_float4(c.x, c.y, c.z, 1.0f);
+    else mix_color(sc, accum, pix, c);
+}
 __global__ __launch_bounds__(WB) void wmcpt_start(Scene sc, WaveBufs w) {
     __shared__ uint32_t lds[2];
     const Seg g = seg_begin(w, 0u, lds);
@@ -1457,7 +1463,7 @@ __global__ __launch_bounds__(WB) void wmcpt_start(Scene sc, WaveBufs w) {
 }
 
 template <int FIRST>
-__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wmcpt_step(Scene sc, WaveBufs w, uint32_t round, float4 *accum) {
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES, 8))) void wmcpt_step(Scene sc, WaveBufs w, uint32_t round, float4 *accum, float4 *color) {
     __shared__ uint32_t lds[3];
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
@@ -1490,12 +1496,12 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
                 }
             }
             if (!(s.flags & 1u)) {
-                mix_color(sc, accum, pix, s.color);  // RR ended the path or 3 bounces done
+                mcpt_out(sc, accum, color, pix, s.color);  // RR ended the path or 3 bounces done
             } else {
                 const Hit h = get_hit(res_in, s.pidx);
                 if (!h.valid) {  // escaped: environment (TEST_MCPT:1340-1344)
                     s.color = s.color + (s.f / s.p) * ENV_C;
-                    mix_color(sc, accum, pix, s.color);
+                    mcpt_out(sc, accum, color, pix, s.color);
                 } else {
                     X = surface_at(sc, h.s, h.pos);
                     emit = true;
@@ -1661,13 +1667,29 @@ hipError_t wave_final_one(const Scene &sc, const WaveBufs &w, const uint4 *gbuf,
     return hipGetLastError();
 }
 
-hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, hipStream_t s) {
+hipError_t wave_mcpt_round(const Scene &sc, const WaveBufs &w, int round, float4 *accum, float4 *color,
+                           hipStream_t s) {
     if (round == 0)
         hipLaunchKernelGGL(wmcpt_start, dim3(w.seg_count), dim3(WB), 0, s, sc, w);
     else if (round == 1)
-        hipLaunchKernelGGL(wmcpt_step<1>, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, accum);
+        hipLaunchKernelGGL(wmcpt_step<1>, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, accum, color);
     else
-        hipLaunchKernelGGL(wmcpt_step<0>, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, accum);
+        hipLaunchKernelGGL(wmcpt_step<0>, dim3(w.seg_count), dim3(WB), 0, s, sc, w, (uint32_t)round, accum, color);
+    return hipGetLastError();
+}
+
+// A pipelined TEST_MCPT frame's WriteColor, after the previous frame's: each band pixel's path
+// colour (wmcpt_step wrote it to `color`) mixed into the accumulation, the same mix_color
+__global__ __launch_bounds__(WB) void wmix_frame(Scene sc, const float4 *color, float4 *accum, uint32_t npx) {
+    const uint32_t i = blockIdx.x * WB + threadIdx.x;
+    if (i >= npx) return;
+    const float4 c = color[i];
+    mix_color(sc, accum, i, mk(c.x, c.y, c.z));
+}
+hipError_t wave_mix_frame(const Scene &sc, const float4 *color, float4 *accum, hipStream_t s) {
+    const uint32_t npx = (sc.row_end - sc.row_begin) * sc.width;
+    if (npx == 0u) return hipSuccess;
+    hipLaunchKernelGGL(wmix_frame, dim3((npx + WB - 1u) / WB), dim3(WB), 0, s, sc, color, accum, npx);
     return hipGetLastError();
 }
 
