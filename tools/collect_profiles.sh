@@ -17,11 +17,9 @@ for WL in ${WORKLOADS:-reuse restir mcpt gi}; do
   cp "$src/pmc_WRITE_SIZE/run_counter_collection.csv" "$dst/pmc_WRITE_SIZE/counter_collection.csv"
   cp "$src/bench_trace.log" "$dst/bench_under_rocprof.log"
   tail -n 1 "gpurun_out/bench_${ROUND}_$WL.log" > "$dst/bench_line.json"
-  # the timed roofline symbol only (GI: the closest-hit instance, not the any-hit one)
-  # (the closest-hit instance; prefix: the flattened variant adds ", true" -- scenes of >= 3 instances)
-  KN="trace_queue<false, 4, false, true, false"
-  # the flattened walk (C3 scenes: reuse, GI) runs at 5 waves per SIMD since round 3
-  case "$WL" in reuse|gi) KN="trace_queue<false, 5, false, true, false" ;; esac
+  # the timed roofline symbol only (GI: the closest-hit instance, not the any-hit one); the
+  # flattened walk at 5 waves per SIMD runs every scene since round 5 (kFlatMinInstances = 1)
+  KN="trace_queue<false, 5, false, true, false"
   python3 tools/hbm_traffic.py "$dst" "$WL:${SCENE[$WL]}:trace_queue:1920x1080" "$KN" > /dev/null
   # the bench line carries the PMC traffic of THIS build's passes (the bench ran first and
   # looked up the previous entry)

@@ -8,9 +8,9 @@ cd /tmp && export TMPDIR=/tmp
 # one launch sequence per pass: per-kernel durations then match bench.py's launch-timing
 # region (PTX_FLAG_SINGLE_STREAM); the two-stream production overlap is measured by the
 # bench's headline value, not by per-kernel averages
-# and one frame in flight (frame pipelining overlaps consecutive frames' kernels); the reuse
-# pipeline's whole-band sequences use the dynamic trace batches (EXTRA_AB=TRACE_DYN=1 makes
-# the production region run the same kernel mode as bench.py's launch-timed region)
+# and one frame in flight (frame pipelining overlaps consecutive frames' kernels); EXTRA_AB
+# adds switches (e.g. TRACE_DYN=1: the dynamic trace batches, the reuse pipeline's default
+# before late round 5)
 export PTX_AB="WAVE_STREAMS=1,PIPELINE_FRAMES=0${EXTRA_AB:+,$EXTRA_AB}"
 # (the shipped libptx.so compiles these switches to their defaults since round 5: the profile
 # runs the measurement build of the same sources, make -C pathtracerdemo_amd/csrc ab)
