@@ -894,7 +894,12 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     // r5_piperestir5.sh); TEST_MCPT 1744-1758 against 1706-1714 (r5_pipemcpt2.sh); GI on static
     // slots 1111-1113 against 1104-1107 (r5_pipemcpt3.sh))
     static const int env_pk = ab_knob("PIPE_STREAMS", 0);
-    const int pipe_k = env_pk > 0 ? env_pk : h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !reuse_static() ? 1 : 2;
+    // (a band handle keeps one: a configs[3] band alone with the exchange proxy 2.38 ms against 2.88
+    // with two -- tools/cl/r5_bandps.sh)
+    const bool band_h = h->comm || h->halo_top || h->halo_bot || (h->cfg.flags & PTX_FLAG_HALO_SKIP);
+    const int pipe_k = env_pk > 0 ? env_pk
+                       : band_h || (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !reuse_static()) ? 1
+                                                                                                        : 2;
     int k = h->alt_stream && pipelined(h) ? pipe_k : env_k > 0 ? env_k : 3;
     // a pipelined frame's spatial pass + PT_4 (the serial back half every frame waits for) as
     // two launch sequences: one half's trace rounds overlap the other's logic kernels.  Same
