@@ -163,6 +163,33 @@ def test_restir_full_hd_pipelined_window_bit_exact(scene1, oracle_mod, native):
     assert r.stats()["frames"] == 3
 
 
+@pytest.mark.parametrize("pipeline", ["restir", "mcpt"])
+def test_pipelined_frames_with_host_writes_bit_exact(scene1, oracle_mod, native, pipeline):
+    """Frames in flight (ReSTIR: PT_1 of frame N + 1 beside PT_4 of frame N; TEST_MCPT: paths of
+    frame N + 1 beside frame N's, colours mixed in after it) with host operations between them:
+    an accumulation reset after frame 2 and an accumulation write after frame 3.  Every image
+    must equal the oracle's, which applies the same operations in order."""
+    W, H = 640, 360
+    r = make_renderer(scene1, W, H, pipeline=pipeline)
+    fr = oracle_frame(oracle_mod, scene1, W, H)
+    pid = oracle_mod.PASS_RESTIR if pipeline == "restir" else oracle_mod.PASS_MCPT
+    seed = np.random.default_rng(5).random((H, W, 4), dtype=np.float32)
+    for f in range(1, 6):
+        r.Update()
+        r.Render()
+        fr.set_frame_index(f)
+        fr.run(pid, 16)
+        if f == 2:
+            r.reset_accumulation()
+            fr.accum[:] = 0.0
+        if f == 3:
+            np.testing.assert_array_equal(r.read_image().view(np.uint32), fr.accum.view(np.uint32))
+            r.write_buffer(native.PTX_BUF_ACCUM, seed)
+            fr.accum[:] = seed
+    np.testing.assert_array_equal(r.read_image().view(np.uint32), fr.accum.view(np.uint32))
+    assert r.stats()["frames"] == 5
+
+
 @pytest.mark.parametrize("variant", ["simple"])
 def test_alternate_variants(scene1, oracle_mod, native, variant):
     """The A/B kernel variants obey the same bars as the default wavefront path."""
