@@ -889,17 +889,21 @@ hipError_t launch_wave_parts(ptx_handle *h, const Scene &sc, const WaveBufs &w, 
     // sequence (whole-band launches, dynamic trace batches); measured at 1080p C3 reuse: 1
     // stream per context 338 Msamples/s, 2 streams 308, unpipelined 3 streams 320
     // (PTX_AB=PIPE_STREAMS=k: A/B)
-    // (ReSTIR without reuse, TEST_MCPT and GI: 2 per context -- C1 1080p ReSTIR at 1792-pixel
-    // segments 1717 against 1620 with one, three 1294 (tools/cl/r5_piperestir4.sh,
-    // r5_piperestir5.sh); TEST_MCPT 1744-1758 against 1706-1714 (r5_pipemcpt2.sh); GI on static
-    // slots 1111-1113 against 1104-1107 (r5_pipemcpt3.sh))
+    // (ReSTIR without reuse, TEST_MCPT and the reuse pipeline's whole-image frames: 2 per context
+    // -- C1 1080p ReSTIR at 1792-pixel segments 1717 against 1620 with one, three 1294
+    // (tools/cl/r5_piperestir4.sh, r5_piperestir5.sh); TEST_MCPT 1744-1758 against 1706-1714
+    // (r5_pipemcpt2.sh); reuse still 509-514 against 509-513, moving 334 against 329 (r5_gicam2.sh))
     static const int env_pk = ab_knob("PIPE_STREAMS", 0);
     // (a band handle keeps one: a configs[3] band alone with the exchange proxy 2.38 ms against 2.88
     // with two -- tools/cl/r5_bandps.sh)
     const bool band_h = h->comm || h->halo_top || h->halo_bot || (h->cfg.flags & PTX_FLAG_HALO_SKIP);
+    // (GI keeps one too: its moving camera 779-784 Msamples/s against 753-759 with two, still
+    // 1104-1107 against 1111-1113 -- tools/cl/r5_gicam2.sh, r5_pipemcpt3.sh)
     const int pipe_k = env_pk > 0 ? env_pk
-                       : band_h || (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !reuse_static()) ? 1
-                                                                                                        : 2;
+                       : band_h || h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI ||
+                                 (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !reuse_static())
+                           ? 1
+                           : 2;
     int k = h->alt_stream && pipelined(h) ? pipe_k : env_k > 0 ? env_k : 3;
     // a pipelined frame's spatial pass + PT_4 (the serial back half every frame waits for) as
     // two launch sequences: one half's trace rounds overlap the other's logic kernels.  Same
