@@ -129,9 +129,9 @@ static bool restir_pipe() {
     static const bool on = ab_knob("PIPE_RESTIR", 1) != 0;
     return on;
 }
-// The DI reuse pipeline's whole-image frames on the same launch shape as the others' (static
-// trace slots, ~1150 segments, 2 front sequences per context) instead of dynamic batches over
-// 1024-pixel segments (PTX_AB=REUSE_STATIC=0: A/B); its bands keep their own segments
+// The DI reuse pipeline's whole-image frames on static trace slots with 2 front sequences per
+// context, as ReSTIR's and TEST_MCPT's, instead of dynamic batches with one (PTX_AB=REUSE_STATIC=0:
+// A/B); its segments stay seg_pixels' reuse rule (1024 px at 1080p)
 static bool reuse_static() {
     static const bool on = ab_knob("REUSE_STATIC", 1) != 0;
     return on;
@@ -439,9 +439,8 @@ static uint32_t seg_pixels(const ptx_handle *h) {
     static const uint32_t env_px = (uint32_t)ab_knob("SEG_PX", 0);
     if (env_px >= 256u && env_px <= 8192u && env_px % 256u == 0u) return env_px;
     const size_t npx = (size_t)h->band_h * h->cfg.width;
-    const bool band = h->comm || h->halo_top || h->halo_bot || (h->cfg.flags & PTX_FLAG_HALO_SKIP);
     if ((h->cfg.pipeline == PTX_PIPELINE_RESTIR && restir_pipe()) || (h->cfg.pipeline == PTX_PIPELINE_MCPT && mcpt_pipe()) ||
-        h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI || (h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE && !band && reuse_static())) {
+        h->cfg.pipeline == PTX_PIPELINE_RESTIR_GI) {
         // ReSTIR, TEST_MCPT and GI: ~1150 segments (1792 px at 1080p), 768 below 1 Mpx; the
         // pipelined frames and the same segments timed alone.  C1 1080p, static trace slots (one
         // workgroup per segment), 2 sequences per context -- ReSTIR: 1536 / 1792 / 2048 / 2560 px
@@ -453,6 +452,10 @@ static uint32_t seg_pixels(const ptx_handle *h) {
         return (uint32_t)std::min<size_t>(4096u, std::max<size_t>(kWaveSegPixels, p));
     }
     if (h->cfg.pipeline != PTX_PIPELINE_RESTIR_REUSE) return kWaveSegPixels;
+    // DI reuse (whole image and bands): 512 px at 1 Mpx .. 4096 at 8.3 Mpx.  Its whole-image frames
+    // on static slots measured 1024 / 1280 / 1536 / 1792 px at 1080p: still 516.7 / 499-502 /
+    // 511-512 / 515 Msamples/s (trace frac 0.627 / 0.60 / 0.62 / 0.663), moving camera 355.5-355.7
+    // / 340-342 / 343-344 / 342-343 (tools/cl/r5_cam4.sh): 1024 keeps both frames fastest
     uint32_t p = 512u;
     while (p < 4096u && (size_t)(2u * p) * 1500u <= npx) p *= 2u;
     return p;
