@@ -479,8 +479,7 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     // a band's spatial pass: ceil(a/s) + ceil(b/s) <= ceil((a+b)/s) + 1)
     const size_t slots = nseg + 1u;
     const size_t cap = per_px * seg_px * slots;
-    // (sized by the segment size, which depends on the handle's band state: re-checked every call,
-    // alloc_buf keeps a buffer of the right size)
+    // (sized by the segment size: re-checked every call, alloc_buf keeps a buffer of the right size)
     if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
     if (int rc = alloc_buf(h, h->d_wact0, slots * seg_px * jpp * 4u)) return rc;
     if (int rc = alloc_buf(h, h->d_wact1, slots * seg_px * jpp * 4u)) return rc;
@@ -788,11 +787,11 @@ static bool whole_band_sequences(const ptx_handle *h);
 static bool use_dyn_batches(const ptx_handle *h) {
     static const int dyn_env = ab_knob("TRACE_DYN", -1);
     const bool band = h->comm || h->halo_top || h->halo_bot;
-    // (ReSTIR without reuse, TEST_MCPT and GI keep static slots in their pipelined frames: C1
-    // 1080p ReSTIR 1536-1543 Msamples/s against 1431-1443 with dynamic batches, 1406-1414 one
-    // frame at a time (tools/cl/r5_piperestir2.sh); TEST_MCPT 1663-1668 against 1598-1609,
-    // 1509-1515 (r5_pipemcpt.sh); GI C3 at 1792-pixel segments 1104-1107 against 1082
-    // (r5_pipemcpt3.sh))
+    // (every pipeline keeps static slots in its pipelined frames since late round 5: C1 1080p
+    // ReSTIR 1536-1543 Msamples/s against 1431-1443 with dynamic batches, 1406-1414 one frame at a
+    // time (tools/cl/r5_piperestir2.sh); TEST_MCPT 1663-1668 against 1598-1609, 1509-1515
+    // (r5_pipemcpt.sh); GI C3 at 1792-pixel segments 1104-1107 against 1082 (r5_pipemcpt3.sh);
+    // the reuse headline through REUSE_STATIC (reuse_static))
     return dyn_env == 1 ||
            (dyn_env != 0 && whole_band_sequences(h) && !band && h->cfg.pipeline == PTX_PIPELINE_RESTIR_REUSE &&
             !reuse_static());
