@@ -1,7 +1,8 @@
 #!/usr/bin/env bash
 # Per-kernel A/B: rocprofv3 --kernel-trace --stats of a short single-sequence bench per library
 # (PTX_AB=PIPELINE_FRAMES=0: kernels do not share the chip with a second frame), then the
-# average duration of every kernel side by side.  usage: LIBS="libptx_a.so libptx.so" bash tools/ab_kernels.sh
+# average duration of every kernel side by side (static trace slots, the production mode since late
+# round 5; EXTRA_AB=TRACE_DYN=1 for the dynamic batches).  usage: LIBS="libptx_a.so libptx.so" bash tools/ab_kernels.sh
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 P=$R/pathtracerdemo_amd
@@ -10,7 +11,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for L in $LIBS; do
-  PTX_LIB_PATH=$P/$L PTX_AB=PIPELINE_FRAMES=0,TRACE_DYN=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$L" -o run --output-format csv -- \
+  PTX_LIB_PATH=$P/$L PTX_AB=PIPELINE_FRAMES=0${EXTRA_AB:+,$EXTRA_AB} timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$L" -o run --output-format csv -- \
       python3 "$R/bench.py" --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/$L.log" 2>&1 || { echo "$L rc=$?"; tail -5 "$OUT/$L.log"; exit 1; }
 done
 python3 - "$OUT" $LIBS <<'PY'
