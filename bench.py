@@ -41,6 +41,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
+L2_PEAK_GBS = 34500.0  # MI355X L2, all 8 XCDs (MI355X_MICROARCH.md §L2: ~34.5 TB/s)
+# the wavefront queue's own IO per traced query (32 B ray record read + 32 B hit record
+# written): layout-specific, so NOT in SURVEY §8(d)'s B_ray -- reported beside the roofline
+QUEUE_IO_PER_RAY = 64
 # algorithmic bytes: 32 per slab test, 36 per triangle test, 48 per
 # instance transform, 48 per hit reconstruction; per-pixel pass IO below.
 B_AABB, B_TRI, B_INST, B_HIT = 32, 36, 48, 48
@@ -129,6 +133,10 @@ def parse():
                          "temporal pass reprojects its history (the interactive case behind the UI)")
     ap.add_argument("--variant", choices=["wave", "simple"], default="wave",
                     help="kernel variant (A/B): wavefront queues, or 1 thread/pixel")
+    ap.add_argument("--profile-region", action="store_true",
+                    help="run ONLY the launch-timed region (one launch sequence, one frame in flight) on the "
+                         "shipped library: what rocprofv3 profiles, so its per-kernel averages are the line's "
+                         "(tools/profile.sh); no headline region, no CPU baseline")
     return ap.parse_args()
 
 
@@ -319,7 +327,9 @@ def main():
             drv = ReuseBand(r, rank, world, device=f"cuda:{device}" if backend == "nccl" else "cpu")
         return r, drv
 
-    r, band_drv = make()
+    if args.profile_region:
+        args.no_cpu_baseline = args.no_configs3 = True
+    r, band_drv = (None, None) if args.profile_region else make()
 
     steps_done = {}
 
@@ -346,37 +356,47 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        frame(r, band_drv)
-    r.synchronize()
-    r.reset_stats()
-    barrier()
-    r.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        frame(r, band_drv)
-    r.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    own_elapsed = elapsed
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}" if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    st = r.stats()
-    img = r.read_image()
-    nonfinite = int((~np.isfinite(img[..., :3])).sum())
+    def timed(rr, drv):
+        """W untimed warmup frames, then K frames between barriers + synchronize: seconds."""
+        for _ in range(args.warmup):
+            frame(rr, drv)
+        rr.synchronize()
+        rr.reset_stats()
+        barrier()
+        rr.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            frame(rr, drv)
+        rr.synchronize()
+        barrier()
+        return time.perf_counter() - t0
+
+    band_digest = comm = None
+    motion_clips = None
     frames_rendered = args.warmup + args.steps
-    # multi-rank self-check: each rank's band (radiance + spatial output after every frame it
-    # rendered) is hashed here and compared on rank 0 with the same rows of ONE handle of the
-    # whole frame rendered the same number of frames (bands are bit-identical by design)
-    band_digest = None
-    if reuse and world > 1 and strong:
-        import hashlib
-        band_digest = hashlib.sha256(img.tobytes() + r.read_history().tobytes()).hexdigest()
-    comm = r.comm_info() if use_comm else None
-    r.close()
+    if r is not None:
+        elapsed = timed(r, band_drv)
+        own_elapsed = elapsed
+        if dist is not None:
+            import torch
+            t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}" if backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        st = r.stats()
+        img = r.read_image()
+        nonfinite = int((~np.isfinite(img[..., :3])).sum())
+        if args.camera_path and reuse:
+            # pixels of the timed frames whose reprojection fell outside the rows the handle holds
+            # (the global motion row rule: more than reuse_radius rows from the pixel's own row)
+            motion_clips = r.read_counters()["motion_clips"]
+        # multi-rank self-check: each rank's band (radiance + spatial output after every frame it
+        # rendered) is hashed here and compared on rank 0 with the same rows of ONE handle of the
+        # whole frame rendered the same number of frames (bands are bit-identical by design)
+        if reuse and world > 1 and strong:
+            import hashlib
+            band_digest = hashlib.sha256(img.tobytes() + r.read_history().tobytes()).hexdigest()
+        comm = r.comm_info() if use_comm else None
+        r.close()
 
     # Second timed region, same K steps, with HIP events around every wavefront launch
     # (PTX_FLAG_TIME_LAUNCHES costs ~5% of a frame, so the headline region above runs
@@ -387,16 +407,14 @@ def main():
     st_k = None
     if args.variant == "wave":
         rk, drv_k = make(time_launches=True, single_stream=True)
-        for _ in range(max(1, args.warmup)):
-            frame(rk, drv_k)
-        rk.synchronize()
-        rk.reset_stats()
-        barrier()
-        for _ in range(args.steps):
-            frame(rk, drv_k)
-        rk.synchronize()
-        barrier()
+        args.warmup = max(1, args.warmup)
+        el_k = timed(rk, drv_k)
         st_k = rk.stats()
+        if r is None:  # --profile-region: this region is the run
+            elapsed = own_elapsed = el_k
+            st = st_k
+            img = rk.read_image()
+            nonfinite = int((~np.isfinite(img[..., :3])).sum())
         rk.close()
 
     # per-rank band times, communicators and band digests (rank 0 reports them all)
@@ -452,11 +470,18 @@ def main():
             traced = [p for p in traced if p != "final"]
         work = {k: sum(counts[p][k] for p in traced) for k in counts[traced[0]]}
         per_frame = n_trace / args.steps
-        dom_bytes = (ray_bytes(work) + 64 * work["rays"]) / per_frame
+        # SURVEY §8(d)'s B_ray only (layout-neutral); the queue's 64 B per query beside it
+        dom_bytes = ray_bytes(work) / per_frame
+        queue_io = QUEUE_IO_PER_RAY * work["rays"] / per_frame
         dom_ms = st_k["kernel_ms_total"][N.PTX_STAT_WAVE_TRACE] / n_trace
         logic_ms = (st_k["kernel_ms_total"][N.PTX_STAT_WAVE_LOGIC]
                     / max(1, st_k["kernel_launches"][N.PTX_STAT_WAVE_LOGIC]))
-        extra = {"launches_per_frame": per_frame, "logic_kernel_avg_ms": round(logic_ms, 4)}
+        extra = {"launches_per_frame": per_frame, "logic_kernel_avg_ms": round(logic_ms, 4),
+                 "queue_io_bytes_per_launch": int(queue_io),
+                 "frac_with_queue_io": round((dom_bytes + queue_io) / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                 "bytes_note": "alg_bytes_per_launch = SURVEY §8(d) B_ray (32 per AABB test + 36 per triangle test "
+                               "+ 48 per instance transform + 48 per hit reconstruction) / trace launches per frame; "
+                               "the wavefront queue's own ray / hit records (64 B per query) are NOT counted in frac"}
     else:
         dom = max(kms, key=lambda p: kms[p])
         work = counts[dom]
@@ -465,15 +490,34 @@ def main():
         extra = {}
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
-    # (profiles/hbm_traffic.json travels to the GPU box: .gpurunignore excludes only the
-    # per-round profile directories)
+    limiters = None
+    # (profiles/hbm_traffic.json and profiles/limiters.json travel to the GPU box: .gpurunignore
+    # excludes only the per-round profile directories)
+    key = f"{pipeline}:{args.scene}:{dom}:{W}x{Hb}"
     prof = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     if os.path.exists(prof):
         try:
-            entry = json.load(open(prof)).get(f"{pipeline}:{args.scene}:{dom}:{W}x{Hb}")
+            entry = json.load(open(prof)).get(key)
             traffic = entry["bytes_per_launch"] if isinstance(entry, dict) else entry
         except Exception:
             traffic = None
+    lim = os.path.join(ROOT, "profiles", "limiters.json")
+    if os.path.exists(lim) and n_trace:
+        try:
+            entry = json.load(open(lim)).get(key)
+        except Exception:
+            entry = None
+        if entry:
+            # what bounds the kernel: the L2's request bytes against its peak, and the
+            # lanes the traversal's node loop keeps busy (the simd_util build)
+            limiters = dict(entry)
+            l2 = entry.get("l2_bytes_per_launch")
+            if l2:
+                limiters["l2_achieved_gbs"] = round(l2 / (dom_ms * 1e-3) / 1e9, 1)
+                limiters["l2_peak_gbs"] = L2_PEAK_GBS
+                limiters["l2_frac"] = round(l2 / (dom_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4)
+            if traffic:
+                limiters["hbm_traffic_frac"] = round(traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     cpu = ts_cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(cs, W, Hb, pipeline, args.cpu_threads or usable_cpus(), device=device,
@@ -515,7 +559,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "avg_launch_ms": round(dom_ms, 4), "alg_bytes_per_launch": int(dom_bytes),
-                     "work_per_frame": work, **extra,
+                     "work_per_frame": work, **extra, "limiters": limiters,
                      "frame": {"alg_bytes": int(frame_bytes), "alg_bytes_per_sample": round(frame_bytes / px, 1),
                                "kernel_ms": round(frame_kernel_s * 1e3, 4),
                                "frac": round(frame_bytes / frame_kernel_s / (HBM_PEAK_GBS * 1e9), 4)}},
@@ -524,6 +568,13 @@ def main():
     }
     if cpu is not None and "parity" in cpu:
         line["parity"] = cpu.pop("parity")
+    if motion_clips is not None:
+        line["motion_clip_px"] = {"pixels": int(motion_clips), "of": W * Hb * args.steps,
+                                  "note": "timed frames' pixels whose reprojected history lay more than reuse_radius "
+                                          "rows away (no history there: the global motion row rule, DESIGN §4.3)"}
+    if args.profile_region:
+        line["profile_region"] = ("launch-timed region only (one launch sequence, one frame in flight): value is "
+                                  "NOT the headline throughput")
     if world == 1:
         line["scaling_note"] = ("one GPU: configs[2]'s frame; `--gpus N` splits configs[3]'s 3840x2160 frame into N "
                                 "row bands (strong); configs3_one_gpu is that frame on this one GPU")
@@ -541,6 +592,11 @@ def main():
             line["parity_check"] = parity
     # any PTX_* switch in the environment (PTX_AB selects A/B kernel variants: unset = product)
     line["env"] = {k: v for k, v in sorted(os.environ.items()) if k.startswith("PTX_")}
+    # which libptx.so ran (product / measurement build), and PTX_AB keys it ignored
+    line["library"] = N.build_info()
+    if line["library"].get("ptx_ab_ignored"):
+        line["env_warning"] = (f"PTX_AB keys {line['library']['ptx_ab_ignored']} are not honoured by this "
+                               f"{line['library']['build']} build: the line measures its defaults")
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

@@ -37,13 +37,14 @@
 extern "C" {
 #endif
 
-#define PTX_ABI_VERSION 4
+#define PTX_ABI_VERSION 5
 
 #define PTX_OK 0
 #define PTX_E_INVALID (-1)  /* bad argument / state                  */
 #define PTX_E_HIP (-2)      /* HIP runtime error                     */
 #define PTX_E_SCENE (-3)    /* scene arrays inconsistent/unsupported */
 #define PTX_E_NOMEM (-4)    /* allocation failure                    */
+#define PTX_E_PENDING (-5)  /* ptx_present_poll: the present is still in flight (not an error) */
 
 #define PTX_UNIFORM_WORDS 33
 #define PTX_GBUFFER_WORDS 4     /* rgba32 texel: flags|inst|mat, prim, bary.x, bary.y */
@@ -216,6 +217,24 @@ int ptx_device_pointer(ptx_handle *h, int which, void **dev_ptr, size_t *bytes);
  * (bgra = 0, a 2D canvas's ImageData) or BGRA (bgra = 1, a bgra8unorm WebGPU canvas); blocking.
  * Whole-image handles (a split frame is presented from its gathered rows by the host). */
 int ptx_present(ptx_handle *h, uint32_t canvas_w, uint32_t canvas_h, int bgra, uint8_t *out);
+/* The same render pass without blocking the caller (the reference's Render() ends by drawing into
+ * the canvas, GC/Renderer_TEST.ts:233-258, and WebGPUEngine's loop calls nothing else,
+ * GC/service/WebGPUEngine.ts:199-200): ptx_present_async enqueues it for the frame last rendered,
+ * with the copy into handle-owned pinned memory, on the handle's stream, and returns at once;
+ * ptx_present_poll copies the bytes into `out` (canvas_w * canvas_h * 4) and returns PTX_OK once
+ * that copy has landed, PTX_E_PENDING while it is in flight (hipEventQuery: never waits).  One
+ * present may be in flight per handle (a second ptx_present_async before its poll returned
+ * PTX_OK fails).  A later frame's accumulation waits for it on the GPU, so the bytes are exactly
+ * the frame it was enqueued after. */
+int ptx_present_async(ptx_handle *h, uint32_t canvas_w, uint32_t canvas_h, int bgra);
+int ptx_present_poll(ptx_handle *h, uint8_t *out, size_t bytes);
+/* What this libptx.so is, as one JSON object in `out` (NUL-terminated, truncated to `bytes`):
+ * {"abi": 5, "build": "product" | "ab" (every PTX_AB switch live: the measurement build) | "wgt"
+ *  (per-wave timing), "arch": "gfx950", "ptx_ab": <PTX_AB as read>, "ptx_ab_ignored": [keys this
+ *  build does not honour], "rccl": <the communicator library loaded, "" before ptx_comm_*>}.
+ * Returns the full length (like snprintf).  A benchmark line carries it, so a run made on the wrong
+ * library, or with switches the shipped library ignores, is labelled as such. */
+int ptx_build_info(char *out, size_t bytes);
 /* Closest-hit queries (TraceRay, SH/PT_1_InitPass.wgsl:605-715) for arbitrary rays.
  * rays: n x {o.x,o.y,o.z,d.x, d.y,d.z,-,-} f32 (32 B); hits: n x {t, flags|inst|mat (u32 bits),
  * prim (u32 bits), bary.x, bary.y, pos.x, pos.y, pos.z} (32 B; flags bit31 = valid).

@@ -13,7 +13,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTX_LIB_PATH") or os.path.join(PKG_DIR, "libptx.so")
 
 PTX_OK = 0
-PTX_ABI_VERSION = 4
+PTX_E_PENDING = -5  # ptx_present_poll: still in flight
+PTX_ABI_VERSION = 5
 PTX_PIPELINE_RESTIR, PTX_PIPELINE_MCPT, PTX_PIPELINE_RESTIR_REUSE, PTX_PIPELINE_RESTIR_GI = 0, 1, 2, 3
 PIPELINES = {"restir": PTX_PIPELINE_RESTIR, "mcpt": PTX_PIPELINE_MCPT, "reuse": PTX_PIPELINE_RESTIR_REUSE,
              "gi": PTX_PIPELINE_RESTIR_GI}
@@ -42,7 +43,8 @@ EXPORTED = ["ptx_abi_version", "ptx_create", "ptx_upload_scene", "ptx_set_frame"
             "ptx_write_buffer", "ptx_device_pointer", "ptx_set_stream", "ptx_destroy", "ptx_last_error",
             "ptx_trace", "ptx_trace_device", "ptx_run_passes", "ptx_halo_rows", "ptx_halo_pack",
             "ptx_halo_unpack", "ptx_comm_unique_id", "ptx_comm_init", "ptx_comm_init_all", "ptx_render_bands",
-            "ptx_row_census", "ptx_comm_info", "ptx_present"]
+            "ptx_row_census", "ptx_comm_info", "ptx_present", "ptx_present_async", "ptx_present_poll",
+            "ptx_build_info"]
 
 
 class PtxConfig(ctypes.Structure):
@@ -111,6 +113,9 @@ def load(path: str = LIB_PATH):
     lib.ptx_trace.argtypes = [H, P, P, ctypes.c_size_t, ctypes.c_int]
     lib.ptx_trace_device.argtypes = [H, P, P, ctypes.c_size_t, ctypes.c_int]
     lib.ptx_present.argtypes = [H, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P]
+    lib.ptx_present_async.argtypes = [H, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+    lib.ptx_present_poll.argtypes = [H, P, ctypes.c_size_t]
+    lib.ptx_build_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
     lib.ptx_run_passes.argtypes = [H, P, ctypes.c_int]
     lib.ptx_halo_rows.argtypes = [H, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                   ctypes.POINTER(ctypes.c_size_t)]
@@ -133,6 +138,18 @@ def load(path: str = LIB_PATH):
         raise PtxError(f"{path}: ABI {lib.ptx_abi_version()} != {PTX_ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
+
+
+def build_info(lib=None) -> dict:
+    """ptx_build_info as a dict: which build this libptx.so is ("product", "ab", "wgt"), the PTX_AB
+    keys it ignores, the communicator library it opened (include/ptx.h)."""
+    import json
+    lib = lib or load()
+    buf = ctypes.create_string_buffer(2048)
+    lib.ptx_build_info(buf, len(buf))
+    out = json.loads(buf.value.decode())
+    out["path"] = getattr(lib, "_name", LIB_PATH)
+    return out
 
 
 def check(lib, handle, rc: int, what: str):

@@ -22,8 +22,49 @@
 namespace ptx {
 
 
+// The keys of PTX_AB, and those this build does not honour: the shipped library reads only
+// kShippedKnobs (every other switch is compiled to its default, ab_knob in ptx_launch.h), so a
+// PTX_AB meant for the measurement build would silently measure the product.  Warned once on
+// stderr and listed by ptx_build_info (bench.py puts that in its line).
+[[maybe_unused]] static const char *const kShippedKnobs[] = {"COMM_TIMEOUT_S", "DEBUG_FILL", "HALO_PROXY_US"};
+#if defined(PTX_WG_TIMES)
+static const char *const kBuildKind = "wgt";
+#elif defined(PTX_AB_BUILD)
+static const char *const kBuildKind = "ab";
+#else
+static const char *const kBuildKind = "product";
+#endif
+static std::vector<std::string> ignored_knobs() {
+    std::vector<std::string> out;
+#ifndef PTX_AB_BUILD
+    const char *ab = getenv("PTX_AB");
+    for (const char *p = ab ? ab : ""; *p;) {
+        const char *end = std::strchr(p, ',');
+        if (!end) end = p + std::strlen(p);
+        const char *eq = static_cast<const char *>(std::memchr(p, '=', (size_t)(end - p)));
+        const std::string key(p, eq ? eq : end);
+        bool known = key.empty();
+        for (const char *k : kShippedKnobs) known = known || key == k;
+        if (!known) out.push_back(key);
+        p = *end ? end + 1 : end;
+    }
+#endif
+    return out;
+}
+static void warn_ignored_knobs() {
+    static const bool once = [] {
+        for (const std::string &k : ignored_knobs())
+            std::fprintf(stderr, "libptx (%s build): PTX_AB key %s is not honoured here -- A/B switches need the "
+                                 "measurement build (make -C pathtracerdemo_amd/csrc ab; PTX_LIB_PATH=.../libptx_ab.so)\n",
+                         kBuildKind, k.c_str());
+        return true;
+    }();
+    (void)once;
+}
+
 int env_knob(const char *key, int dflt) {
     static const std::string ab = getenv("PTX_AB") ? getenv("PTX_AB") : "";
+    warn_ignored_knobs();
     const size_t n = std::strlen(key);
     for (size_t pos = 0; pos < ab.size();) {
         size_t end = ab.find(',', pos);
@@ -480,12 +521,24 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t slots = nseg + 1u;
     const size_t cap = per_px * seg_px * slots;
     // (sized by the segment size: re-checked every call, alloc_buf keeps a buffer of the right size)
-    if (int rc = alloc_buf(h, h->d_wstate, (size_t)kWaveStateSlots * npix * 16u)) return rc;
-    if (int rc = alloc_buf(h, h->d_wact0, slots * seg_px * jpp * 4u)) return rc;
-    if (int rc = alloc_buf(h, h->d_wact1, slots * seg_px * jpp * 4u)) return rc;
+    const size_t state_b = (size_t)kWaveStateSlots * npix * 16u, act_b = slots * seg_px * jpp * 4u;
     // counts per round and slot, then the dynamic-batch counters of trace_queue: one per
     // (tile set, launch sequence, round) -- kDynCounters words
-    if (int rc = alloc_buf(h, h->d_wctr, (2u * kWaveMaxRounds * slots + kDynCounters) * 4u)) return rc;
+    const size_t ctr_b = (2u * kWaveMaxRounds * slots + kDynCounters) * 4u;
+    const bool resize = (h->d_wstate.p && h->d_wstate.bytes != state_b) || (h->d_wact0.p && h->d_wact0.bytes != act_b) ||
+                        (h->d_wact1.p && h->d_wact1.bytes != act_b) || (h->d_wctr.p && h->d_wctr.bytes != ctr_b) ||
+                        (h->wave_ray_cap && cap > h->wave_ray_cap);
+    // a buffer is only replaced when its size changes; the other frame context (and this one's
+    // last frame) may still run on it, so everything in flight finishes first
+    if (resize)
+        if (int rc = quiesce(h)) return rc;
+    if (int rc = alloc_buf(h, h->d_wstate, state_b)) return rc;
+    if (int rc = alloc_buf(h, h->d_wact0, act_b)) return rc;
+    if (int rc = alloc_buf(h, h->d_wact1, act_b)) return rc;
+    const void *ctr_before = h->d_wctr.p;
+    if (int rc = alloc_buf(h, h->d_wctr, ctr_b)) return rc;
+    // a new counter buffer starts from zero (the dynamic-batch heads count from it)
+    if (h->d_wctr.p != ctr_before) HIP_CHECK(h, memset_sync(h, h->d_wctr.p, 0, h->d_wctr.bytes));
     if (cap > h->wave_ray_cap) {
         free_buf(h->d_wrays);
         free_buf(h->d_wres0);
@@ -1111,6 +1164,8 @@ int pipe_depth() {
 int quiesce(ptx_handle *h) {
     for (hipStream_t q : {h->stream, h->alt.stream, h->alt2.stream})
         if (q) HIP_CHECK(h, hipStreamSynchronize(q));
+    for (hipStream_t q : h->hp)
+        if (q) HIP_CHECK(h, hipStreamSynchronize(q));
     for (int k = 1; k < ptx_handle::kMaxSplit; ++k) {
         if (h->sub[k]) HIP_CHECK(h, hipStreamSynchronize(h->sub[k]));
         if (h->alt.sub[k]) HIP_CHECK(h, hipStreamSynchronize(h->alt.sub[k]));
@@ -1391,7 +1446,33 @@ extern "C" {
 
 int ptx_abi_version(void) { return PTX_ABI_VERSION; }
 
+int ptx_build_info(char *out, size_t bytes) {
+    auto esc = [](const std::string &v) {
+        std::string o;
+        for (char c : v) {
+            if (c == '"' || c == '\\') o += '\\';
+            if ((unsigned char)c >= 0x20) o += c;
+        }
+        return o;
+    };
+    const char *ab = getenv("PTX_AB");
+    std::string ign;
+    for (const std::string &k : ignored_knobs()) ign += (ign.empty() ? "\"" : ",\"") + esc(k) + "\"";
+    char buf[1024];
+    const int n = std::snprintf(buf, sizeof buf,
+                                "{\"abi\": %d, \"build\": \"%s\", \"arch\": \"gfx950\", \"ptx_ab\": \"%s\", "
+                                "\"ptx_ab_ignored\": [%s], \"rccl\": \"%s\"}",
+                                PTX_ABI_VERSION, kBuildKind, esc(ab ? ab : "").c_str(), ign.c_str(),
+                                esc(comm_library()).c_str());
+    if (out && bytes) {
+        std::memcpy(out, buf, std::min<size_t>((size_t)std::max(n, 0), bytes - 1));
+        out[std::min<size_t>((size_t)std::max(n, 0), bytes - 1)] = 0;
+    }
+    return n;
+}
+
 int ptx_create(const ptx_config *cfg, ptx_handle **out) {
+    warn_ignored_knobs();  // (once per process: PTX_AB keys this build ignores)
     if (!cfg || !out) return PTX_E_INVALID;
     *out = nullptr;
     if (cfg->width == 0 || cfg->height == 0 || cfg->pipeline > PTX_PIPELINE_RESTIR_GI) return PTX_E_INVALID;
@@ -1798,6 +1879,53 @@ int ptx_present(ptx_handle *h, uint32_t canvas_w, uint32_t canvas_h, int bgra, u
     return read_to_host(h, out, h->d_canvas.p, bytes);
 }
 
+int ptx_present_async(ptx_handle *h, uint32_t canvas_w, uint32_t canvas_h, int bgra) {
+    if (!h) return PTX_E_INVALID;
+    if (h->present_pending) return fail(h, PTX_E_INVALID, "ptx_present_async: a present is in flight (poll it first)");
+    if (canvas_w == 0 || canvas_h == 0 || (uint64_t)canvas_w * canvas_h > (1ull << 28))
+        return fail(h, PTX_E_INVALID, "ptx_present_async: canvas %ux%u", canvas_w, canvas_h);
+    if (h->cfg.row_begin != 0 || h->band_h != h->cfg.height)
+        return fail(h, PTX_E_INVALID, "ptx_present_async: a band handle holds part of the texture");
+    if (!h->d_accum.p) return fail(h, PTX_E_INVALID, "ptx_present_async: nothing rendered");
+    HIP_CHECK(h, hipSetDevice(h->device));
+    const size_t bytes = (size_t)canvas_w * canvas_h * 4u;
+    if (int rc = alloc_buf(h, h->d_canvas_async, bytes)) return rc;
+    if (bytes > h->present_host_bytes) {
+        if (h->present_host) (void)hipHostFree(h->present_host);
+        h->present_host = nullptr;
+        h->present_host_bytes = 0;
+        HIP_CHECK(h, hipHostMalloc(&h->present_host, bytes, hipHostMallocDefault));
+        h->present_host_bytes = bytes;
+    }
+    if (!h->ev_present) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_present, hipEventDisableTiming));
+    // on the current frame's stream, after it: a pipelined handle's next frame records ev_prev
+    // on this stream before it enqueues anything, and its accumulation waits for ev_prev
+    const hipError_t e = launch_present((const float4 *)h->d_accum.p, h->cfg.width, h->cfg.height, canvas_w, canvas_h,
+                                        bgra != 0, (uint32_t *)h->d_canvas_async.p, h->stream);
+    if (e != hipSuccess) return fail(h, PTX_E_HIP, "ptx_present_async: %s", hipGetErrorString(e));
+    HIP_CHECK(h, hipMemcpyAsync(h->present_host, h->d_canvas_async.p, bytes, hipMemcpyDeviceToHost, h->stream));
+    HIP_CHECK(h, hipEventRecord(h->ev_present, h->stream));
+    h->present_bytes = bytes;
+    h->present_pending = true;
+    return PTX_OK;
+}
+
+int ptx_present_poll(ptx_handle *h, uint8_t *out, size_t bytes) {
+    if (!h || !out) return PTX_E_INVALID;
+    if (!h->present_pending) return fail(h, PTX_E_INVALID, "ptx_present_poll: no present in flight");
+    if (bytes < h->present_bytes)
+        return fail(h, PTX_E_INVALID, "ptx_present_poll: %zu bytes; the canvas needs %zu", bytes, h->present_bytes);
+    const hipError_t e = hipEventQuery(h->ev_present);
+    if (e == hipErrorNotReady) return PTX_E_PENDING;
+    if (e != hipSuccess) {
+        h->present_pending = false;
+        return fail(h, PTX_E_HIP, "ptx_present_poll: %s", hipGetErrorString(e));
+    }
+    std::memcpy(out, h->present_host, h->present_bytes);
+    h->present_pending = false;
+    return PTX_OK;
+}
+
 int ptx_trace_device(ptx_handle *h, const void *rays_dev, void *hits_dev, size_t n, int eps_mode) {
     if (!h || (n && (!rays_dev || !hits_dev)) || n > 0xffffffffu || (eps_mode != 0 && eps_mode != 1))
         return fail(h, PTX_E_INVALID, "ptx_trace: bad arguments");
@@ -1857,7 +1985,12 @@ int ptx_destroy(ptx_handle *h) {
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
     if (h->host_stage) (void)hipHostFree(h->host_stage);
-    for (DevBuf *b : {&h->d_canvas, &h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
+    if (h->ev_present) {
+        (void)hipEventSynchronize(h->ev_present);
+        (void)hipEventDestroy(h->ev_present);
+    }
+    if (h->present_host) (void)hipHostFree(h->present_host);
+    for (DevBuf *b : {&h->d_canvas, &h->d_canvas_async, &h->d_scene, &h->d_geometry, &h->d_tris, &h->d_nodes, &h->d_subs, &h->d_insts, &h->d_mats, &h->d_tverts, &h->d_gbuf,
                       &h->d_res, &h->d_accum, &h->d_counters, &h->d_queue, &h->d_qrays, &h->d_qhits,
                       &h->d_wstate, &h->d_wrays, &h->d_wres0, &h->d_wres1, &h->d_wres2, &h->d_wact0, &h->d_wact1, &h->d_wctr,
                       &h->d_hist, &h->d_jstate, &h->d_jres, &h->d_tjstate, &h->d_tjres, &h->d_nbr, &h->d_surf, &h->d_psurf, &h->d_direct, &h->d_census})
@@ -1873,6 +2006,13 @@ int ptx_destroy(ptx_handle *h) {
             if (a.sub[q]) (void)hipStreamDestroy(a.sub[q]);
         }
     }
+    for (hipStream_t &q : h->hp)
+        if (q) {
+            (void)hipStreamSynchronize(q);
+            (void)hipStreamDestroy(q);
+        }
+    if (h->ev_hp_in) (void)hipEventDestroy(h->ev_hp_in);
+    if (h->ev_hp_out) (void)hipEventDestroy(h->ev_hp_out);
     if (h->alt_stream) (void)hipStreamDestroy(h->alt_stream);
     if (h->alt2_stream) (void)hipStreamDestroy(h->alt2_stream);
     if (h->ev_prev) (void)hipEventDestroy(h->ev_prev);

@@ -27,9 +27,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -57,6 +59,9 @@ struct Rccl {
     std::string why;
 };
 
+// the library rccl() opened (ptx_build_info reports it: a PTX_RCCL_LIB stand-in is never silent)
+std::string g_comm_library;
+
 const Rccl &rccl() {
     static Rccl r;
     static std::once_flag once;
@@ -64,6 +69,8 @@ const Rccl &rccl() {
         const char *path = std::getenv("PTX_RCCL_LIB");
         void *lib = nullptr;
         if (path && *path) {
+            // a test hook (tests/loopback/): said on stderr, and in ptx_build_info's "rccl"
+            std::fprintf(stderr, "libptx: PTX_RCCL_LIB=%s replaces RCCL as the communicator library\n", path);
             lib = dlopen(path, RTLD_NOW | RTLD_LOCAL);
         } else {
             path = "librccl.so.1";
@@ -73,8 +80,10 @@ const Rccl &rccl() {
         if (!lib) {
             const char *e = dlerror();
             r.why = std::string("dlopen ") + path + ": " + (e ? e : "not found");
+            g_comm_library = std::string("(not loaded: ") + r.why + ")";
             return;
         }
+        g_comm_library = path;
         bool all = true;
         auto sym = [&](auto &fn, const char *name) {
             fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
@@ -445,6 +454,46 @@ int check_neighbours(ptx_handle *h) {
 
 }  // namespace
 
+// The back chain of a band frame -- temporal combine, exchange, summaries, spatial pass, PT_4 --
+// is the frame's critical path: the next frame's front (G-buffer + PT_1) runs beside it with slack
+// (a configs[3] band: front 1.96 ms against a 2.45 ms back chain, profiles/r5/bands/kernel_trace.csv).
+// PTX_AB=BAND_PRIO=1 (A/B) enqueues that chain on high-priority streams so the front fills what it
+// leaves; prio_leave joins it back into the frame context's stream (ev_prev and the frame's stop event
+// come after it there).
+static bool band_prio() {
+    static const bool on = ab_knob("BAND_PRIO", 0) != 0;
+    return on;
+}
+int prio_enter(ptx_handle *h) {
+    if (!band_prio() || h->hp_active) return PTX_OK;
+    int lo = 0, hi = 0;
+    HIP_CHECK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    for (int q = 0; q < ptx_handle::kMaxSplit; ++q)
+        if (!h->hp[q]) HIP_CHECK(h, hipStreamCreateWithPriority(&h->hp[q], hipStreamNonBlocking, hi));
+    if (!h->ev_hp_in) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_hp_in, hipEventDisableTiming));
+    if (!h->ev_hp_out) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_hp_out, hipEventDisableTiming));
+    HIP_CHECK(h, hipEventRecord(h->ev_hp_in, h->stream));
+    HIP_CHECK(h, hipStreamWaitEvent(h->hp[0], h->ev_hp_in, 0));
+    h->hp_saved_stream = h->stream;
+    h->stream = h->hp[0];
+    for (int q = 1; q < ptx_handle::kMaxSplit; ++q) {
+        h->hp_saved_sub[q] = h->sub[q];
+        h->sub[q] = h->hp[q];
+    }
+    h->hp_active = true;
+    return PTX_OK;
+}
+int prio_leave(ptx_handle *h) {
+    if (!h->hp_active) return PTX_OK;
+    h->hp_active = false;
+    for (int q = 1; q < ptx_handle::kMaxSplit; ++q) h->sub[q] = h->hp_saved_sub[q];
+    hipStream_t hp0 = h->stream;
+    h->stream = h->hp_saved_stream;
+    HIP_CHECK(h, hipEventRecord(h->ev_hp_out, hp0));
+    HIP_CHECK(h, hipStreamWaitEvent(h->stream, h->ev_hp_out, 0));
+    return PTX_OK;
+}
+
 // ptx_render of a band handle that owns a communicator: one whole frame, exchange included.
 int render_band_nccl(ptx_handle *h) {
     if (int rc = comm_health(h)) return rc;
@@ -455,6 +504,7 @@ int render_band_nccl(ptx_handle *h) {
     if (int rc = band_prepare(h, sc, w, pipe, moved)) return rc;
     TimedLaunch *ft = nullptr;
     if (int rc = band_front(h, sc, w, ft, pipe, moved)) return rc;
+    if (int rc = prio_enter(h)) return rc;
     if (xchg) {
         NCCL_CHECK(h, rccl().group_start());
         const int rc = nccl_motion_halo(h);
@@ -477,11 +527,12 @@ int render_band_nccl(ptx_handle *h) {
     if (h->halo_top) h->halo_bytes_sent += send_up(h).gb + send_up(h).rb;
     if (h->halo_bot) h->halo_bytes_sent += send_down(h).gb + send_down(h).rb;
     if (int r2 = halo_landed(h, xs)) return r2;
-    return band_back(h, sc, w, ft);
+    if (int r2 = band_back(h, sc, w, ft)) return r2;
+    return prio_leave(h);
 }
 
 // The exchange's proxy on one GPU (PTX_AB=HALO_PROXY_US=n, with PTX_FLAG_HALO_SKIP: timing
-// only): the band's edge rows copied into its own halo rows on the exchange stream (the same
+// only; the shipped library honours it): the band's edge rows copied into its own halo rows on the exchange stream (the same
 // bytes an exchange moves, device to device), then a one-workgroup wait of n microseconds
 // standing for the xGMI transfer (2 x 16.6 MB per direction at 153 GB/s: ~110 us), so the
 // band's frame time shows where the exchange sits on its critical chain.
@@ -517,14 +568,17 @@ int render_band_solo(ptx_handle *h) {
     if (int rc = band_prepare(h, sc, w, pipe, moved)) return rc;
     TimedLaunch *ft = nullptr;
     if (int rc = band_front(h, sc, w, ft, pipe, moved)) return rc;
+    if (int rc = prio_enter(h)) return rc;
     if (int rc = band_temporal(h, sc, w, pipe, moved)) return rc;  // (a motion halo keeps what it holds)
     hipStream_t xs;
     if (int rc = exchange_stream(h, xs)) return rc;
-    static const int proxy_us = ab_knob("HALO_PROXY_US", 0);
+    // (honoured by the shipped library: it only acts on a HALO_SKIP handle, a band timed alone)
+    static const int proxy_us = env_knob("HALO_PROXY_US", 0);
     if (proxy_us > 0 && proxy_us <= 100000)
         if (int rc = halo_proxy(h, xs, (uint32_t)proxy_us)) return rc;
     if (int rc = halo_landed(h, xs)) return rc;
-    return band_back(h, sc, w, ft);
+    if (int rc = band_back(h, sc, w, ft)) return rc;
+    return prio_leave(h);
 }
 
 }  // namespace ptx
@@ -583,6 +637,10 @@ int ptx_comm_init(ptx_handle *h, const void *unique_id, size_t bytes, int rank, 
     h->rank = rank;
     h->world = world;
     h->comm_broken = false;
+    // every rank calls this collectively: the motion-halo decision's shared state (motion_exchange)
+    // restarts in lockstep, whatever frames a rank rendered before
+    h->band_frames = 0;
+    std::memset(h->band_camera, 0, sizeof h->band_camera);
     if (int rc = check_neighbours(h)) {
         h->comm_broken = true;  // (the peers' view of this exchange is unknown: abort, never flush)
         comm_destroy(h);
@@ -623,6 +681,8 @@ int ptx_comm_init_all(ptx_handle *const *hs, int n) {
         hs[i]->comm = comms[i];
         hs[i]->rank = i;
         hs[i]->world = n;
+        hs[i]->band_frames = 0;
+        std::memset(hs[i]->band_camera, 0, sizeof hs[i]->band_camera);
     }
     return PTX_OK;
 }
@@ -772,12 +832,13 @@ int ptx_render_bands(ptx_handle *const *hs, int n, float *rgba_out) {
 }  // extern "C"
 
 namespace ptx {
+const char *comm_library() { return g_comm_library.c_str(); }
 // A communicator that timed out or reported an error is aborted: ncclCommDestroy would flush
 // operations a dead or absent peer never matches.  A healthy non-blocking one is finalized
 // against the deadline first (an abort if that does not complete), then destroyed.
 void comm_destroy(ptx_handle *h) {
-    const Rccl &R = rccl();
-    if (h->comm && R.ok) {
+    if (h->comm && rccl().ok) {  // (no communicator: RCCL is never opened)
+        const Rccl &R = rccl();
         ncclComm_t c = (ncclComm_t)h->comm;
         bool gone = false;
         if (h->comm_broken && R.abort) {

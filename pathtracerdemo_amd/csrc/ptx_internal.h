@@ -146,10 +146,24 @@ struct ptx_handle {
     // words (uniform 4..22) of the last one
     uint64_t band_frames = 0;
     uint32_t band_camera[19] = {0};
+    // band frames' back chain (temporal combine -> exchange -> spatial -> PT_4) on high-priority
+    // streams (prio_enter / prio_leave, ptx_comm.cpp): h->stream and h->sub are swapped for hp[]
+    // while it is enqueued, then the frame context's stream waits for it
+    hipStream_t hp[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_hp_in = nullptr, ev_hp_out = nullptr;
+    hipStream_t hp_saved_stream = nullptr, hp_saved_sub[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
+    bool hp_active = false;
     // ptx_present's canvas on the device; the pinned staging buffer of read_to_host
     DevBuf d_canvas;
     void *host_stage = nullptr;
     size_t host_stage_bytes = 0;
+    // ptx_present_async: its own device canvas and pinned host copy (a blocking ptx_present may
+    // run while it is in flight), the event after its copy, and what is in flight
+    DevBuf d_canvas_async;
+    void *present_host = nullptr;
+    size_t present_host_bytes = 0, present_bytes = 0;
+    hipEvent_t ev_present = nullptr;
+    bool present_pending = false;
     // stats
     TimedLaunch ring[kEventRing];
     int ring_pos = 0;
@@ -207,4 +221,6 @@ int leave_alt(ptx_handle *h);
 int render_band_nccl(ptx_handle *h);
 int render_band_solo(ptx_handle *h);
 void comm_destroy(ptx_handle *h);
+// the communicator library ptx_comm.cpp opened ("" before the first ptx_comm_* call), for ptx_build_info
+const char *comm_library();
 }  // namespace ptx

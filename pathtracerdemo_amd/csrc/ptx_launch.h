@@ -13,7 +13,9 @@ constexpr int kBlock = 256;
 // Runtime switches are read from ONE environment variable, PTX_AB, a comma-separated list of
 // KEY or KEY=int; a key that is absent gives `dflt`.  env_knob (ptx_api.cpp): the few the
 // shipped library honours, each covered by a test -- COMM_TIMEOUT_S (test_gpu_loopback.py),
-// DEBUG_FILL (test_gpu_debug_fill.py).  ab_knob: the A/B and diagnostic switches of the measurement builds
+// DEBUG_FILL (test_gpu_debug_fill.py), HALO_PROXY_US (a band timed alone with PTX_FLAG_HALO_SKIP:
+// the exchange's one-GPU stand-in, test_gpu_bands.py).  Any other key in PTX_AB is named on stderr
+// and in ptx_build_info.  ab_knob: the A/B and diagnostic switches of the measurement builds
 // (make variant NAME=x ALT_DEFS=-DPTX_AB_BUILD, make wgt; selected with PTX_LIB_PATH) -- in the
 // shipped library every one is its default, a compile-time constant, and the losing branches
 // fold away.  bench.py echoes PTX_AB (and any other PTX_* variable) in its line.

@@ -5,12 +5,18 @@
  *
  * Same surface: constructor, async Initialize(world), Update(), Render(), GetCamera(),
  * ResetFrameCount(); WebGPUEngine's loop (GC/service/WebGPUEngine.ts:199-200) calls
- * Update() then Render() per tick exactly as before.  Instead of a canvas it renders into
- * the accumulated RGBA f32 image (ReadImage / RenderAsync(out)); Present(canvasW, canvasH)
- * runs the reference's render pass on the GPU (the fullscreen quad + FragmentShader.wgsl's fixed
- * 600 x 450 texel window, unorm8) into bytes a canvas takes as they are: RGBA for a 2D canvas's
- * putImageData, BGRA for a bgra8unorm WebGPU canvas.  presentImage does the same on the host for
- * a frame gathered from row bands (renderBands).
+ * Update() then Render() per tick exactly as before, and nothing else.  Like Renderer_TEST.Render
+ * (Renderer_TEST.ts:233-258, which ends by drawing into the canvas it was constructed with),
+ * Render() paints the canvas it was given: when the canvas offers getContext('2d'), the reference's
+ * render pass (the fullscreen quad + FragmentShader.wgsl's fixed 600 x 450 texel window, unorm8)
+ * runs on the GPU behind the frame (ptx_present_async) and its bytes go to putImageData once they
+ * have landed -- polled off the event loop, never waited for; while one present is in flight a
+ * newer frame is presented after it, so the canvas always ends on the newest finished frame
+ * (PresentedSerial: the Render() call it shows; PresentIdle(): a promise for "nothing in flight").
+ * ReadImage / RenderAsync(out) give the accumulated RGBA f32 image; Present(canvasW, canvasH)
+ * is the same render pass, blocking, into RGBA (putImageData) or BGRA (a bgra8unorm WebGPU
+ * canvas) bytes.  presentImage does it on the host for a frame gathered from row bands
+ * (renderBands).
  *
  * `world` is the reference's own World (./world.js: World.LoadFromScene over the Scene JSON,
  * meshes in ResourceManager.MeshPool), serialized here by SerializeWorldData exactly as
@@ -59,6 +65,9 @@ function isCanvas(x) {
   return !!x && typeof x === 'object' && typeof x.width === 'number' && typeof x.height === 'number';
 }
 
+// the next turn of the event loop (Node: setImmediate; a browser: a zero timeout)
+const soon = typeof setImmediate === 'function' ? setImmediate : (fn) => setTimeout(fn, 0);
+
 class NativeRenderer {
   /**
    * Three call forms:
@@ -102,6 +111,14 @@ class NativeRenderer {
     this.Camera = null;
     this.FrameCount = 0;
     this.Uniform = null;
+    // canvas painting (Render): the 2D context, the present in flight, its waiters
+    this.Context2D = undefined;
+    this.RenderSerial = 0;
+    this.PresentedSerial = 0;
+    this.PresentInFlight = null;
+    this.PresentWanted = false;
+    this.PresentWaiters = [];
+    this.PresentError = null;
   }
 
   /** A handle for this.Width x this.Height (rows rowBegin..rowEnd of it). */
@@ -138,6 +155,7 @@ class NativeRenderer {
         throw new Error('Initialize: a row-band renderer cannot follow a canvas resize');
       }
       if (!(this.Canvas.width > 0 && this.Canvas.height > 0)) throw new RangeError('Initialize: empty canvas');
+      this.dropPresent();
       if (this.Handle) addon.destroy(this.Handle);
       this.Handle = null;
       this.Width = this.Canvas.width;
@@ -161,8 +179,84 @@ class NativeRenderer {
     addon.setFrame(this.Handle, this.Uniform);
   }
 
-  /** Renderer_TEST.Render (:208-261): all passes + accumulation, asynchronous on the GPU. */
-  Render() { addon.render(this.Handle); }
+  /**
+   * Renderer_TEST.Render (:208-261): all passes + accumulation, asynchronous on the GPU, then the
+   * render pass into the canvas (:233-258) when it has a 2D context -- enqueued behind the frame,
+   * painted when its bytes land (the event loop is never blocked).
+   */
+  Render() {
+    addon.render(this.Handle);
+    this.RenderSerial++;
+    if (this.context2D()) {
+      if (this.PresentInFlight) this.PresentWanted = true;
+      else this.startPresent();
+    }
+  }
+
+  /** The canvas's 2D context (looked up once; null when the canvas has none, e.g. in a worker). */
+  context2D() {
+    if (this.Context2D === undefined) {
+      const c = this.Canvas;
+      this.Context2D = (c && typeof c.getContext === 'function' && c.getContext('2d')) || null;
+    }
+    return this.Context2D;
+  }
+
+  startPresent() {
+    const ctx = this.context2D();
+    const w = this.Canvas.width, h = this.Canvas.height;
+    const image = ctx.createImageData(w, h);
+    addon.presentAsync(this.Handle, w, h, false);
+    this.PresentInFlight = { serial: this.RenderSerial, image, handle: this.Handle };
+    this.PresentWanted = false;
+    soon(() => this.pollPresent(0));
+  }
+
+  pollPresent(tries) {
+    const f = this.PresentInFlight;
+    if (!f || f.handle !== this.Handle) return;  // dropped (Destroy, a resize)
+    let done;
+    try {
+      done = addon.presentPoll(this.Handle, f.image.data);
+    } catch (e) {
+      if (/in flight on this handle/.test(String(e && e.message))) {  // a RenderAsync owns the handle
+        setTimeout(() => this.pollPresent(tries + 1), 1);
+        return;
+      }
+      this.PresentInFlight = null;
+      this.PresentError = e;
+      this.settlePresent();
+      return;
+    }
+    if (!done) {  // the first few polls on the next turns, then every millisecond
+      if (tries < 8) soon(() => this.pollPresent(tries + 1));
+      else setTimeout(() => this.pollPresent(tries + 1), 1);
+      return;
+    }
+    this.PresentInFlight = null;
+    this.PresentedSerial = f.serial;
+    this.context2D().putImageData(f.image, 0, 0);
+    if (this.PresentWanted) this.startPresent();
+    else this.settlePresent();
+  }
+
+  settlePresent() {
+    const ws = this.PresentWaiters;
+    this.PresentWaiters = [];
+    for (const r of ws) r();
+  }
+
+  /** Resolves once no present is in flight (the canvas shows the newest rendered frame). */
+  PresentIdle() {
+    if (!this.PresentInFlight) return Promise.resolve(this.PresentedSerial);
+    return new Promise((resolve) => this.PresentWaiters.push(() => resolve(this.PresentedSerial)));
+  }
+
+  dropPresent() {
+    this.PresentInFlight = null;
+    this.PresentWanted = false;
+    this.settlePresent();
+  }
 
   /** Render off the event loop; resolves once the frame (and the optional copy) is done. */
   RenderAsync(out) { return addon.renderAsync(this.Handle, out || null); }
@@ -192,6 +286,7 @@ class NativeRenderer {
 
   /** DestroyGPUResources (:462-476). */
   Destroy() {
+    this.dropPresent();
     if (this.Handle) addon.destroy(this.Handle);
     this.Handle = null;
   }

@@ -665,6 +665,60 @@ static napi_value js_present(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
+/* presentAsync(handle, canvasW, canvasH, bgra): enqueue the render pass for the frame last rendered
+ * without waiting (ptx_present_async); presentPoll fetches the bytes */
+static napi_value js_present_async(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    if (argc < 4) {
+        napi_throw_type_error(env, NULL, "presentAsync(handle, canvasW, canvasH, bgra)");
+        return NULL;
+    }
+    uint32_t cw = 0, ch = 0;
+    bool bgra = false;
+    CHECK_NAPI(env, napi_get_value_uint32(env, argv[1], &cw));
+    CHECK_NAPI(env, napi_get_value_uint32(env, argv[2], &ch));
+    CHECK_NAPI(env, napi_get_value_bool(env, argv[3], &bgra));
+    int rc = ptx_present_async(H->h, cw, ch, bgra ? 1 : 0);
+    if (rc != PTX_OK) return throw_ptx(env, H, rc, "ptx_present_async");
+    return NULL;
+}
+
+/* presentPoll(handle, out: Uint8Array | Uint8ClampedArray) -> true once the bytes are in `out`,
+ * false while the present is in flight (ptx_present_poll: never waits) */
+static napi_value js_present_poll(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    Handle *H = argc >= 1 ? get_handle(env, argv[0]) : NULL;
+    if (!H) return NULL;
+    void *p;
+    size_t n, es;
+    napi_typedarray_type t;
+    if (argc < 2 || typed_view(env, argv[1], &p, &n, &es, &t) || (t != napi_uint8_array && t != napi_uint8_clamped_array)) {
+        napi_throw_type_error(env, NULL, "presentPoll(handle, out: Uint8Array | Uint8ClampedArray)");
+        return NULL;
+    }
+    int rc = ptx_present_poll(H->h, (uint8_t *)p, n);
+    if (rc != PTX_OK && rc != PTX_E_PENDING) return throw_ptx(env, H, rc, "ptx_present_poll");
+    napi_value r;
+    CHECK_NAPI(env, napi_get_boolean(env, rc == PTX_OK, &r));
+    return r;
+}
+
+/* buildInfo() -> the JSON string of ptx_build_info (which libptx.so build is loaded) */
+static napi_value js_build_info(napi_env env, napi_callback_info info) {
+    (void)info;
+    char buf[2048];
+    ptx_build_info(buf, sizeof buf);
+    napi_value s;
+    CHECK_NAPI(env, napi_create_string_utf8(env, buf, NAPI_AUTO_LENGTH, &s));
+    return s;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     static const struct {
         const char *name;
@@ -681,7 +735,8 @@ static napi_value init(napi_env env, napi_value exports) {
         {"renderBands", js_render_bands},   {"renderBandsAsync", js_render_bands_async},
         {"commUniqueId", js_comm_unique_id}, {"commInit", js_comm_init},
         {"commInitAll", js_comm_init_all},  {"rowCensus", js_row_census},
-        {"present", js_present},
+        {"present", js_present},            {"presentAsync", js_present_async},
+        {"presentPoll", js_present_poll},   {"buildInfo", js_build_info},
     };
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; ++i) {
         napi_value f;

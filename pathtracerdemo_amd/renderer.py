@@ -226,6 +226,22 @@ class Renderer:
         self._call("ptx_present", self._h, cw, ch, 1 if bgra else 0, out.ctypes.data)
         return out
 
+    def present_async(self, canvas_w: int | None = None, canvas_h: int | None = None, bgra: bool = False) -> None:
+        """Enqueue Present for the frame last rendered without waiting (ptx_present_async);
+        present_poll() returns the bytes once they have landed."""
+        cw, ch = int(canvas_w or self.width), int(canvas_h or self.height)
+        self._call("ptx_present_async", self._h, cw, ch, 1 if bgra else 0)
+        self._present_shape = (ch, cw, 4)
+
+    def present_poll(self) -> np.ndarray | None:
+        """The bytes of the present in flight, or None while it is still running (never waits)."""
+        out = np.zeros(self._present_shape, np.uint8)
+        rc = self._lib.ptx_present_poll(self._h, out.ctypes.data, out.nbytes)
+        if rc == N.PTX_E_PENDING:
+            return None
+        N.check(self._lib, self._h, rc, "ptx_present_poll")
+        return out
+
     def trace(self, rays: np.ndarray, eps_mode: int = 1) -> np.ndarray:
         """Closest hits for an (n, 8) f32 ray array {o.xyz, d.xyz, -, -}; returns (n, 8) f32
         {t, flags|inst|mat bits, prim bits, bary.x, bary.y, pos.xyz} (include/ptx.h)."""

@@ -6,10 +6,17 @@
 // NativeRenderer is constructed the way WebGPUEngine constructs Renderer_TEST (:83):
 // new Renderer(adapter, device, canvas).
 //
+// The canvas is a stand-in for the HTMLCanvasElement: width / height and getContext('2d'), whose
+// context records every putImageData -- what NativeRenderer.Render paints (the engine itself never
+// presents: WebGPUEngine.renderLoop calls only Update() and Render()).  Between ticks the loop
+// yields like requestAnimationFrame does (a 16 ms timer), and after the last tick it waits until
+// no present is in flight.
+//
 // argv: JSON {sceneDir | assetsDir, width, height, pipeline, out, dump: [tick...],
 //   ticks: [{dt, keys: ['w', ...], mouse: [movementX, movementY] | null, resize: [w, h] | null}]}
-// stdout: JSON {ticks: [{uniform, width, height, forward, right, moved}]}; the accumulated image
-// after tick t goes to `${out}.${t}` for every t in `dump`.
+// stdout: JSON {ticks: [{uniform, width, height, forward, right, moved}], puts: [{serial, width,
+// height, x, y}]}; the accumulated image after tick t goes to `${out}.${t}` for every t in `dump`,
+// the bytes of put k to `${out}.put.${k}` (serial: the Render() call it shows, tick serial - 1).
 const fs = require('fs');
 const { NativeRenderer } = require('../../pathtracerdemo_amd/js/NativeRenderer');
 const { vec3 } = require('../../pathtracerdemo_amd/js/wgpu_math');
@@ -70,13 +77,28 @@ class InputController {
   }
 }
 
+// a 2D context that records what is painted into it
+class RecordingContext2D {
+  constructor(canvas) { this.canvas = canvas; this.puts = []; this.renderer = null; }
+  createImageData(w, h) { return { width: w, height: h, data: new Uint8ClampedArray(w * h * 4) }; }
+  putImageData(img, x, y) {
+    this.puts.push({ serial: this.renderer ? this.renderer.PresentedSerial : -1, width: img.width,
+      height: img.height, x, y, canvas: [this.canvas.width, this.canvas.height], data: Buffer.from(img.data) });
+  }
+}
+
+const nextFrame = () => new Promise((resolve) => setTimeout(resolve, 16));  // requestAnimationFrame
+
 async function main() {
   const req = JSON.parse(process.argv[2]);
   const canvas = { width: req.width, height: req.height };     // the HTMLCanvasElement's size
+  const ctx2d = new RecordingContext2D(canvas);
+  canvas.getContext = (kind) => (kind === '2d' ? ctx2d : null);
   const world = loadWorld(req);
   const input = new InputController();
   // WebGPUEngine.initialize (:56-91): canvas size, renderer, Initialize(world), setCamera
   const renderer = new NativeRenderer(null, null, canvas, { pipeline: req.pipeline, device: 0 });
+  ctx2d.renderer = renderer;
   input.onCameraMove = () => renderer.ResetFrameCount();       // constructor, :43-47
   await renderer.Initialize(world);
   input.setCamera(renderer.GetCamera());
@@ -111,8 +133,15 @@ async function main() {
       const img = renderer.ReadImage();
       fs.writeFileSync(`${req.out}.${t}`, Buffer.from(img.buffer, img.byteOffset, img.byteLength));
     }
+    await nextFrame();
   }
+  await renderer.PresentIdle();
+  if (renderer.PresentError) throw renderer.PresentError;
+  const puts = ctx2d.puts.map((p, k) => {
+    fs.writeFileSync(`${req.out}.put.${k}`, p.data);
+    return { serial: p.serial, width: p.width, height: p.height, x: p.x, y: p.y, canvas: p.canvas };
+  });
   renderer.Destroy();
-  process.stdout.write(JSON.stringify({ ticks }));
+  process.stdout.write(JSON.stringify({ ticks, puts, renderSerial: renderer.RenderSerial }));
 }
 main().catch((e) => { console.error(e.stack || String(e)); process.exit(1); });

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), f"libptx.so does not export {name}"
     assert sorted(_native.EXPORTED) == declared
-    assert lib.ptx_abi_version() == _native.PTX_ABI_VERSION == 4
+    assert lib.ptx_abi_version() == _native.PTX_ABI_VERSION == 5
 
 
 def test_header_constants_match_the_python_binding():
@@ -240,3 +240,23 @@ def test_recalibrated_costs_rebalance_measured_bands():
     ms2 = [float(truth[b0:b1].sum()) for b0, b1 in re]
     re2 = balanced_bands(recalibrated_costs(c, re, ms2), world, min_rows=30)
     assert band_balance(truth, re2) < 1.05  # ... and a second round closer
+
+
+def test_build_info_labels_the_library_and_ignored_switches():
+    """ptx_build_info: the shipped libptx.so says it is the product build and lists the PTX_AB keys
+    it does not honour (A/B switches of the measurement build), and warns about them on stderr."""
+    import json
+    import subprocess
+    import sys
+    code = ("from pathtracerdemo_amd import _native as N; import json; "
+            "lib = N.load(); print(json.dumps(N.build_info(lib))); lib.ptx_create(None, None)")
+    env = dict(os.environ, PTX_AB="TRACE_DYN=1,DEBUG_FILL=-1,COMM_TIMEOUT_S=30", PTX_STANDALONE_RUNTIME="1")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr
+    info = json.loads(p.stdout.strip().splitlines()[-1])
+    assert info["abi"] == 5 and info["arch"] == "gfx950"
+    if os.path.basename(info["path"]) == "libptx.so":
+        assert info["build"] == "product"
+        assert info["ptx_ab_ignored"] == ["TRACE_DYN"]
+        assert "PTX_AB key TRACE_DYN is not honoured" in p.stderr
+    assert info["ptx_ab"] == "TRACE_DYN=1,DEBUG_FILL=-1,COMM_TIMEOUT_S=30"

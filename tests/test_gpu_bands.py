@@ -5,6 +5,8 @@ communicators).  The bar: the bands reproduce the single-handle frame BIT FOR BI
 single handle is itself pinned to the oracle (test_gpu_reuse.py); small splits are checked
 against the oracle directly.  Plus the work census the cost-balanced split is cut from.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -170,6 +172,41 @@ def test_halo_skip_band_interior_rows(scene3):
     assert band.stats()["frames"] == 3
     one.close()
     band.close()
+
+
+def test_halo_proxy_band_timed_alone_in_the_shipped_library(tmp_path):
+    """PTX_AB=HALO_PROXY_US=n (the exchange's one-GPU stand-in for a band timed alone: its edge
+    rows copied into its own halo rows, then an n-microsecond wait on the exchange stream) is
+    honoured by the shipped library -- no "not honoured" warning -- and changes no interior row."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import sys, time, numpy as np
+sys.path.insert(0, {root!r}); sys.path.insert(0, {os.path.join(root, 'tests')!r})
+from pathtracerdemo_amd.scene.world import compile_scene
+from pathtracerdemo_amd import _native as N
+from test_gpu_bands import make
+cs = compile_scene('c3_interior_32')
+W, H, R, b0, b1, F = 96, 200, 12, 50, 170, 3
+one = make(cs, W, H, radius=R)
+band = make(cs, W, H, radius=R, row_begin=b0, row_end=b1, halo_skip=True)
+t0 = time.perf_counter()
+for _ in range(F):
+    for r in (one, band):
+        r.Update(); r.Render()
+band.synchronize(); one.synchronize()
+dt = time.perf_counter() - t0
+lo, hi = F * R, (b1 - b0) - F * R
+assert np.array_equal(band.read_history()[lo:hi].view(np.uint32), one.read_history()[b0 + lo:b0 + hi].view(np.uint32))
+assert dt >= F * 0.02, dt
+print('ok', N.build_info()['ptx_ab_ignored'])
+"""
+    env = dict(os.environ, PTX_AB="HALO_PROXY_US=20000")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.stdout.strip().splitlines()[-1] == "ok []"
+    assert "not honoured" not in p.stderr
 
 
 def test_pipelined_band_frames_with_host_reads(scene3):

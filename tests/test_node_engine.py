@@ -14,7 +14,11 @@ uniform the JS host writes equals the Python restatement of the same loop, and t
 image after several ticks is bit-identical to the oracle rendering the same uniforms -- the
 reuse pipeline on C3 (its temporal pass reprojecting the history under the motion), ReSTIR GI
 on C3 (the same for its GI history) and the reference pipeline on C1; after the resize the
-frames come out at the new size.
+frames come out at the new size.  The canvas: the engine calls only Update() + Render(), as
+WebGPUEngine.renderLoop does (:199-200), and the canvas's 2D context records every putImageData
+NativeRenderer.Render paints (Renderer_TEST.Render draws into its canvas, Renderer_TEST.ts:233-258):
+each painted frame is byte-identical to oracle.present of the oracle's frame of that tick on that
+canvas size, and the canvas ends on the last tick's frame.
 """
 import json
 import os
@@ -154,6 +158,7 @@ def test_engine_loop_bit_exact(request, oracle_mod, tmp_path, which, pipeline, W
     ref = EngineRef(cs, W, H)
     fr = None
     moved_frames = 0
+    shown = {}  # tick -> oracle.present of the oracle's frame after it, on that tick's canvas
     for t, (ev, got) in enumerate(zip(PATH, ticks)):
         u, moved = ref.tick(ev)
         assert got["moved"] == moved, f"tick {t}"
@@ -171,11 +176,26 @@ def test_engine_loop_bit_exact(request, oracle_mod, tmp_path, which, pipeline, W
             fr.run_gi_frame(threads=16)
         else:
             fr.run(oracle_mod.PASS_RESTIR, threads=16)
+        shown[t] = oracle_mod.present(fr.accum.reshape(ref.H, ref.W, 4), ref.W, ref.H)
         if t in DUMP:
             h, w = ref.H, ref.W
             assert (got["width"], got["height"]) == (w, h)
             img = np.fromfile(f"{out}.{t}", dtype=np.float32).reshape(h, w, 4)
             np.testing.assert_array_equal(img.view(np.uint32), fr.accum.view(np.uint32), f"radiance, tick {t}")
     assert [t["uniform"][23] for t in ticks] == [1, 1, 1, 1, 1, 1, 2, 3, 1, 1, 2]
+    # what reached the canvas: every putImageData, byte for byte, against the oracle's frame
+    res = json.loads(p.stdout)
+    puts = res["puts"]
+    assert res["renderSerial"] == len(PATH)
+    assert len(puts) >= 3, puts
+    serials = [q["serial"] for q in puts]
+    assert serials == sorted(set(serials)) and serials[0] >= 1
+    assert serials[-1] == len(PATH), "the canvas must end on the newest frame"
+    for k, q in enumerate(puts):
+        t = q["serial"] - 1
+        want = shown[t]
+        assert (q["x"], q["y"]) == (0, 0) and (q["height"], q["width"]) == want.shape[:2] == tuple(q["canvas"][::-1])
+        got_px = np.fromfile(f"{out}.put.{k}", dtype=np.uint8).reshape(want.shape)
+        np.testing.assert_array_equal(got_px, want, f"canvas bytes of tick {t}")
     if pipeline in ("reuse", "gi"):
         assert moved_frames >= 4  # the temporal pass reprojected its history on the moved frames
