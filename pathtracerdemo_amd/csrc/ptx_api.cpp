@@ -524,7 +524,8 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t state_b = (size_t)kWaveStateSlots * npix * 16u, act_b = slots * seg_px * jpp * 4u;
     // counts per round and slot, then the dynamic-batch counters of trace_queue: one per
     // (tile set, launch sequence, round) -- kDynCounters words
-    const size_t ctr_b = (2u * kWaveMaxRounds * slots + kDynCounters) * 4u;
+    // (then trace_queue_w1's per (round, slot) batch counters, WaveBufs::take)
+    const size_t ctr_b = (2u * kWaveMaxRounds * slots + kDynCounters + kWaveMaxRounds * slots) * 4u;
     const bool resize = (h->d_wstate.p && h->d_wstate.bytes != state_b) || (h->d_wact0.p && h->d_wact0.bytes != act_b) ||
                         (h->d_wact1.p && h->d_wact1.bytes != act_b) || (h->d_wctr.p && h->d_wctr.bytes != ctr_b) ||
                         (h->wave_ray_cap && cap > h->wave_ray_cap);
@@ -595,6 +596,10 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     w.seg_phys = 0;
     w.cnt_stride = (uint32_t)slots;
     w.dyn = nullptr;  // set per launch sequence (launch_wave_parts)
+    // one-wave trace workgroups per segment on static slots (PTX_AB=TRACE_W1=k: A/B; 0 = off)
+    static const int w1 = ab_knob("TRACE_W1", 0);
+    w.wave_wgs = w1 >= 1 && w1 <= 8 ? (uint32_t)w1 : 0u;
+    w.take = (uint32_t *)h->d_wctr.p + 2u * kWaveMaxRounds * slots + kDynCounters;
     h->wave_slots = (uint32_t)slots;
     return PTX_OK;
 }
@@ -1163,8 +1168,6 @@ int pipe_depth() {
 }
 int quiesce(ptx_handle *h) {
     for (hipStream_t q : {h->stream, h->alt.stream, h->alt2.stream})
-        if (q) HIP_CHECK(h, hipStreamSynchronize(q));
-    for (hipStream_t q : h->hp)
         if (q) HIP_CHECK(h, hipStreamSynchronize(q));
     for (int k = 1; k < ptx_handle::kMaxSplit; ++k) {
         if (h->sub[k]) HIP_CHECK(h, hipStreamSynchronize(h->sub[k]));
@@ -2006,13 +2009,6 @@ int ptx_destroy(ptx_handle *h) {
             if (a.sub[q]) (void)hipStreamDestroy(a.sub[q]);
         }
     }
-    for (hipStream_t &q : h->hp)
-        if (q) {
-            (void)hipStreamSynchronize(q);
-            (void)hipStreamDestroy(q);
-        }
-    if (h->ev_hp_in) (void)hipEventDestroy(h->ev_hp_in);
-    if (h->ev_hp_out) (void)hipEventDestroy(h->ev_hp_out);
     if (h->alt_stream) (void)hipStreamDestroy(h->alt_stream);
     if (h->alt2_stream) (void)hipStreamDestroy(h->alt2_stream);
     if (h->ev_prev) (void)hipEventDestroy(h->ev_prev);

@@ -454,46 +454,6 @@ int check_neighbours(ptx_handle *h) {
 
 }  // namespace
 
-// The back chain of a band frame -- temporal combine, exchange, summaries, spatial pass, PT_4 --
-// is the frame's critical path: the next frame's front (G-buffer + PT_1) runs beside it with slack
-// (a configs[3] band: front 1.96 ms against a 2.45 ms back chain, profiles/r5/bands/kernel_trace.csv).
-// PTX_AB=BAND_PRIO=1 (A/B) enqueues that chain on high-priority streams so the front fills what it
-// leaves; prio_leave joins it back into the frame context's stream (ev_prev and the frame's stop event
-// come after it there).
-static bool band_prio() {
-    static const bool on = ab_knob("BAND_PRIO", 0) != 0;
-    return on;
-}
-int prio_enter(ptx_handle *h) {
-    if (!band_prio() || h->hp_active) return PTX_OK;
-    int lo = 0, hi = 0;
-    HIP_CHECK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    for (int q = 0; q < ptx_handle::kMaxSplit; ++q)
-        if (!h->hp[q]) HIP_CHECK(h, hipStreamCreateWithPriority(&h->hp[q], hipStreamNonBlocking, hi));
-    if (!h->ev_hp_in) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_hp_in, hipEventDisableTiming));
-    if (!h->ev_hp_out) HIP_CHECK(h, hipEventCreateWithFlags(&h->ev_hp_out, hipEventDisableTiming));
-    HIP_CHECK(h, hipEventRecord(h->ev_hp_in, h->stream));
-    HIP_CHECK(h, hipStreamWaitEvent(h->hp[0], h->ev_hp_in, 0));
-    h->hp_saved_stream = h->stream;
-    h->stream = h->hp[0];
-    for (int q = 1; q < ptx_handle::kMaxSplit; ++q) {
-        h->hp_saved_sub[q] = h->sub[q];
-        h->sub[q] = h->hp[q];
-    }
-    h->hp_active = true;
-    return PTX_OK;
-}
-int prio_leave(ptx_handle *h) {
-    if (!h->hp_active) return PTX_OK;
-    h->hp_active = false;
-    for (int q = 1; q < ptx_handle::kMaxSplit; ++q) h->sub[q] = h->hp_saved_sub[q];
-    hipStream_t hp0 = h->stream;
-    h->stream = h->hp_saved_stream;
-    HIP_CHECK(h, hipEventRecord(h->ev_hp_out, hp0));
-    HIP_CHECK(h, hipStreamWaitEvent(h->stream, h->ev_hp_out, 0));
-    return PTX_OK;
-}
-
 // ptx_render of a band handle that owns a communicator: one whole frame, exchange included.
 int render_band_nccl(ptx_handle *h) {
     if (int rc = comm_health(h)) return rc;
@@ -504,7 +464,6 @@ int render_band_nccl(ptx_handle *h) {
     if (int rc = band_prepare(h, sc, w, pipe, moved)) return rc;
     TimedLaunch *ft = nullptr;
     if (int rc = band_front(h, sc, w, ft, pipe, moved)) return rc;
-    if (int rc = prio_enter(h)) return rc;
     if (xchg) {
         NCCL_CHECK(h, rccl().group_start());
         const int rc = nccl_motion_halo(h);
@@ -527,8 +486,7 @@ int render_band_nccl(ptx_handle *h) {
     if (h->halo_top) h->halo_bytes_sent += send_up(h).gb + send_up(h).rb;
     if (h->halo_bot) h->halo_bytes_sent += send_down(h).gb + send_down(h).rb;
     if (int r2 = halo_landed(h, xs)) return r2;
-    if (int r2 = band_back(h, sc, w, ft)) return r2;
-    return prio_leave(h);
+    return band_back(h, sc, w, ft);
 }
 
 // The exchange's proxy on one GPU (PTX_AB=HALO_PROXY_US=n, with PTX_FLAG_HALO_SKIP: timing
@@ -568,7 +526,6 @@ int render_band_solo(ptx_handle *h) {
     if (int rc = band_prepare(h, sc, w, pipe, moved)) return rc;
     TimedLaunch *ft = nullptr;
     if (int rc = band_front(h, sc, w, ft, pipe, moved)) return rc;
-    if (int rc = prio_enter(h)) return rc;
     if (int rc = band_temporal(h, sc, w, pipe, moved)) return rc;  // (a motion halo keeps what it holds)
     hipStream_t xs;
     if (int rc = exchange_stream(h, xs)) return rc;
@@ -577,8 +534,7 @@ int render_band_solo(ptx_handle *h) {
     if (proxy_us > 0 && proxy_us <= 100000)
         if (int rc = halo_proxy(h, xs, (uint32_t)proxy_us)) return rc;
     if (int rc = halo_landed(h, xs)) return rc;
-    if (int rc = band_back(h, sc, w, ft)) return rc;
-    return prio_leave(h);
+    return band_back(h, sc, w, ft);
 }
 
 }  // namespace ptx

@@ -146,13 +146,6 @@ struct ptx_handle {
     // words (uniform 4..22) of the last one
     uint64_t band_frames = 0;
     uint32_t band_camera[19] = {0};
-    // band frames' back chain (temporal combine -> exchange -> spatial -> PT_4) on high-priority
-    // streams (prio_enter / prio_leave, ptx_comm.cpp): h->stream and h->sub are swapped for hp[]
-    // while it is enqueued, then the frame context's stream waits for it
-    hipStream_t hp[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t ev_hp_in = nullptr, ev_hp_out = nullptr;
-    hipStream_t hp_saved_stream = nullptr, hp_saved_sub[kMaxSplit] = {nullptr, nullptr, nullptr, nullptr};
-    bool hp_active = false;
     // ptx_present's canvas on the device; the pinned staging buffer of read_to_host
     DevBuf d_canvas;
     void *host_stage = nullptr;

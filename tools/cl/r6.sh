@@ -10,6 +10,40 @@ first)  # the round's first build: suite, smoke, headline + C1 ReSTIR lines, shi
     $G suite $C && $G smoke $C &&
     $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 &&
     $G profile $C/prof_reuse && $G bands $C bands_r5cut --world 8 --bands "$B5" ;;
+prio)  # band back chain on high-priority streams (PTX_AB=BAND_PRIO=1, measurement build) vs the product
+    $G bands $C base --world 8 --bands "$B5" &&
+    PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so EXTRA_AB=BAND_PRIO=1 $G bands $C prio --world 8 --bands "$B5" &&
+    PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so EXTRA_AB=BAND_PRIO=1 $G bands $C prio_overlap --world 8 --bands "$B5" --overlap &&
+    $G bands $C base2 --world 8 --bands "$B5" ;;
+w1)  # one-wave trace workgroups (PTX_AB=TRACE_W1=k, measurement build) and the spill-free shipped trace
+     # kernel (dynamic / split-segment branches compiled out): GPU suites, then interleaved benches
+    AB=$PWD/pathtracerdemo_amd/libptx_ab.so
+    $G suite $C &&
+    PTX_LIB_PATH=$AB PTX_AB=TRACE_W1=2 $G suite $C/w2 -k "parity or reuse or gi or bands or golden" &&
+    for v in prod w0 w2 w4 prod w2 w1 w0; do
+        if [ $v = prod ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1
+        else PTX_LIB_PATH=$AB PTX_AB=TRACE_W1=${v#w} $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; fi
+    done &&
+    for v in prod w0 w2 w4; do
+        if [ $v = prod ]; then $G bench $C restir_$v --workload restir --no-cpu-baseline || exit 1
+        else PTX_LIB_PATH=$AB PTX_AB=TRACE_W1=${v#w} $G bench $C restir_$v --workload restir --no-cpu-baseline || exit 1; fi
+    done &&
+    $G bands $C bands_prod --world 8 --bands "$B5" &&
+    PTX_LIB_PATH=$AB EXTRA_AB=TRACE_W1=2 $G bands $C bands_w2 --world 8 --bands "$B5" &&
+    PTX_LIB_PATH=$AB EXTRA_AB=TRACE_W1=4 $G bands $C bands_w4 --world 8 --bands "$B5" ;;
+evid)  # round-6 evidence at the current build: GPU suite + smoke, then per workload the shipped-library
+       # profile (tools/gpu.sh profile) and its bench line (CPU baselines, parity window, 4K one-GPU frame)
+    $G suite $C && $G smoke $C &&
+    for wl in reuse gi restir mcpt; do
+        $G profile $C/prof_$wl --workload $wl && $G bench $C $wl --workload $wl || exit 1
+    done ;;
+evid2)  # lane use per traversal region (measurement build), the moving camera, the DYN coverage run
+        # (ADVICE r5), and configs[3]'s bands at this build (the r5 cut, then one measured re-cut)
+    PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so $G simd $C reuse &&
+    PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so $G simd $C restir &&
+    $G bench $C camera --camera-path --no-configs3 &&
+    PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so PTX_AB=TRACE_DYN=1 $G suite $C/dyn -k "parity or reuse" &&
+    $G bands $C bands --world 8 --bands "$B5" --recut 1 ;;
 *)
     echo "unknown case $1"; exit 2 ;;
 esac
