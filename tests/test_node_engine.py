@@ -199,3 +199,22 @@ def test_engine_loop_bit_exact(request, oracle_mod, tmp_path, which, pipeline, W
         np.testing.assert_array_equal(got_px, want, f"canvas bytes of tick {t}")
     if pipeline in ("reuse", "gi"):
         assert moved_frames >= 4  # the temporal pass reprojected its history on the moved frames
+
+
+def test_render_paints_the_newest_frame_without_waiting():
+    """NativeRenderer.Render's canvas painting over a simulated addon (tests/node/paint_fake_addon.js:
+    presents land 0-3 event-loop turns after they were enqueued): Render() never waits, each put
+    shows the frame of the Render() call it names, puts come in order, after a resize the canvas
+    size follows, and the canvas ends on the newest frame."""
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "paint_fake_addon.js")], capture_output=True,
+                       text=True, cwd=ROOT, timeout=60)
+    assert p.returncode == 0, p.stderr
+    r = json.loads(p.stdout)
+    puts, frame_of = r["puts"], {int(k): v for k, v in r["frameOf"].items()}
+    assert len(puts) >= 8
+    serials = [q["serial"] for q in puts]
+    assert serials == sorted(set(serials))
+    assert serials[-1] == r["last"], "the canvas ends on the newest frame"
+    for q in puts:
+        assert q["uniform"] and q["v"] == frame_of[q["serial"]] & 255
+        assert (q["w"], q["h"]) == ((5, 4) if q["serial"] > r["resizedAt"] else (8, 6))
