@@ -524,8 +524,7 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     const size_t state_b = (size_t)kWaveStateSlots * npix * 16u, act_b = slots * seg_px * jpp * 4u;
     // counts per round and slot, then the dynamic-batch counters of trace_queue: one per
     // (tile set, launch sequence, round) -- kDynCounters words
-    // (then trace_queue_w1's per (round, slot) batch counters, WaveBufs::take)
-    const size_t ctr_b = (2u * kWaveMaxRounds * slots + kDynCounters + kWaveMaxRounds * slots) * 4u;
+    const size_t ctr_b = (2u * kWaveMaxRounds * slots + kDynCounters) * 4u;
     const bool resize = (h->d_wstate.p && h->d_wstate.bytes != state_b) || (h->d_wact0.p && h->d_wact0.bytes != act_b) ||
                         (h->d_wact1.p && h->d_wact1.bytes != act_b) || (h->d_wctr.p && h->d_wctr.bytes != ctr_b) ||
                         (h->wave_ray_cap && cap > h->wave_ray_cap);
@@ -596,10 +595,6 @@ int wave_buffers(ptx_handle *h, WaveBufs &w) {
     w.seg_phys = 0;
     w.cnt_stride = (uint32_t)slots;
     w.dyn = nullptr;  // set per launch sequence (launch_wave_parts)
-    // one-wave trace workgroups per segment on static slots (PTX_AB=TRACE_W1=k: A/B; 0 = off)
-    static const int w1 = ab_knob("TRACE_W1", 0);
-    w.wave_wgs = w1 >= 1 && w1 <= 8 ? (uint32_t)w1 : 0u;
-    w.take = (uint32_t *)h->d_wctr.p + 2u * kWaveMaxRounds * slots + kDynCounters;
     h->wave_slots = (uint32_t)slots;
     return PTX_OK;
 }

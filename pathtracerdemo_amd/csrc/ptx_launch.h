@@ -92,11 +92,6 @@ struct WaveBufs {
     // kDynHeads dequeue heads (round r at dyn + r * kDynRoundWords; the logic round that emits
     // trace round r zeroes them in seg_begin); nullptr = one slot per trace workgroup.
     uint32_t *dyn;
-    // One-wave trace workgroups (trace_queue_w1): per (round, queue slot) the count of the slot's
-    // 64-query batches already taken (take[round * cnt_stride + slot]), zeroed by the logic round
-    // that emits the trace round (seg_end); nullptr = not used
-    uint32_t *take;
-    uint32_t wave_wgs;  // trace_queue_w1: one-wave workgroups per segment (0 = the 4-wave trace_queue)
     // DI reuse pipeline: primary-hit surface records (2 uint4 per pixel, first band row; halo
     // rows at negative / >= npix indices), written by winit_start; nullptr otherwise
     uint4 *surf;

@@ -148,14 +148,12 @@ __device__ __forceinline__ void trace_batch(const Scene &sc, const SubRoot *subs
 #ifndef PTX_TRACE_STREAM
 #define PTX_TRACE_STREAM 1
 #endif
-// SB: the workgroup's thread count (the LDS stack's stride); GCTR: `l_next` is the segment's
-// batch counter in global memory, shared by the segment's one-wave workgroups (trace_queue_w1)
-template <bool PROF, bool OCC, bool DYN, uint32_t SB = WB, bool GCTR = false>
+template <bool PROF, bool OCC, bool DYN>
 __device__ __forceinline__ void trace_stream(const Scene &sc, const SubRoot *subs, const Inst *insts, PassEps eps,
                                              uint32_t *stack, CoopLds coop, const WaveBufs &w, uint32_t round,
                                              const uint32_t *pref, uint32_t *heads, float4 *res_all,
                                              uint32_t *l_next = nullptr, uint32_t sj = 0u, uint32_t sn = 0u) {
-    constexpr uint32_t stride = SB;
+    constexpr uint32_t stride = WB;
     const uint32_t lane = __lane_id();
     // ---- the batch stream (wave-uniform)
     const uint32_t total = DYN ? pref[w.seg_count] : 0u;
@@ -248,9 +246,7 @@ __device__ __forceinline__ void trace_stream(const Scene &sc, const SubRoot *sub
             while (want != 0ull && !src_done) {  // wave-uniform
                 if (!DYN && qleft == 0u) {  // the workgroup's next batch of its segment
                     uint32_t b = 0u;
-                    if (lane == 0u)
-                        b = GCTR ? __hip_atomic_fetch_add(l_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : __hip_atomic_fetch_add(l_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (lane == 0u) b = __hip_atomic_fetch_add(l_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
                     if (b * 64u >= sn) {
                         src_done = true;
@@ -488,11 +484,14 @@ __device__ __forceinline__ void dyn_prefix(const WaveBufs &w, uint32_t round, ui
 // modes of the measurement build since late round 5 (every production frame traces static slots,
 // one workgroup per segment: use_dyn_batches): the shipped kernel is compiled without those
 // branches (their batch walks spilled 28 B per lane into the streamed static path).
+#ifndef PTX_TRACE_AB_PATHS
 #ifdef PTX_AB_BUILD
-constexpr bool kAbBuild = true;
+#define PTX_TRACE_AB_PATHS 1
 #else
-constexpr bool kAbBuild = false;
+#define PTX_TRACE_AB_PATHS 0
 #endif
+#endif
+constexpr bool kAbBuild = PTX_TRACE_AB_PATHS != 0;
 template <bool COUNT, int WAVES, bool PROF = false, bool LDS_TABLES = true, bool OCC = false, bool FLAT = false>
 __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
@@ -602,31 +601,6 @@ void trace_queue(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
         trace_batch<COUNT, PROF, OCC, LDS_TABLES, FLAT>(sc, subs, insts, eps, stack, coop, res_buf(w, round), w.rays,
                                                          j * w.ray_stride, i, i < n);
     }
-}
-
-// One-wave workgroups for the streamed walk on static slots: segment j's 64-query batches are
-// taken by its w.wave_wgs one-wave workgroups through a batch counter in global memory
-// (WaveBufs::take, zeroed by the logic round that emitted the rays), instead of by the four
-// waves of one workgroup through an LDS counter.  A wave whose segment is drained leaves at
-// once and its slot (LDS: tables + a 64-lane stack) takes any other workgroup, where a 4-wave
-// workgroup holds its LDS until its slowest wave ends and a new one needs four free slots on one
-// CU.  Same per-query walk (trace_stream), so every result is bit-identical.
-template <int WAVES, bool OCC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
-void trace_queue_w1(Scene sc, WaveBufs w, uint32_t round, PassEps eps) {
-    PTX_WAVE_TIMER(sc, KID_TRACE | (w.seg_base ? 0x80u : 0u));
-    extern __shared__ __attribute__((aligned(16))) uint32_t wstack[];
-    const uint32_t local = blockIdx.x / w.wave_wgs;
-    const uint32_t j = w.seg_phys + w.seg_base + local;  // physical queue slot
-    const uint32_t n = w.cnt[(2u * round + 1u) * w.cnt_stride + j];
-    if ((blockIdx.x % w.wave_wgs) * 64u >= n) return;  // (wave-uniform) more waves than batches
-    __shared__ unsigned long long c_key[64];
-    __shared__ uint32_t c_mark[64];
-    const CoopLds coop{c_key, c_mark};
-    const LdsTables T = stage_tables(sc, wstack);
-    uint32_t *stack = wstack + tables_lds_bytes(sc) / 4u + threadIdx.x;
-    trace_stream<false, OCC, false, 64u, true>(sc, T.subs, T.insts, eps, stack, coop, w, round, nullptr, nullptr,
-                                               res_buf(w, round), w.take + round * w.cnt_stride + j, j, n);
 }
 
 // Lane-refill form of the same queries.  The whole traversal -- instance loop, sub-root
@@ -1632,17 +1606,11 @@ hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_
         const int occ = env_occ ? env_occ : (w.trace_waves == 4u && !flat) ? 4 : 5;
         static const bool no_lds = ab_knob("TRACE_NOLDS", 0) != 0;
         const bool tables_fit = tables_fit_lds(sc) && !no_lds;
-        if (PTX_TRACE_STREAM && w.wave_wgs && w.take && !w.dyn && flat && tables_fit && occ == 5) {
-            // one-wave workgroups over the static slots (trace_queue_w1)
-            const size_t lds1 = tables_lds_bytes(sc) + (size_t)depth * 64u * sizeof(uint32_t);
-            hipLaunchKernelGGL((trace_queue_w1<5, false>), dim3(w.seg_count * w.wave_wgs), dim3(64), lds1, s, sc, w,
-                               (uint32_t)round, eps);
-            return hipGetLastError();
-        }
         auto k = !tables_fit ? trace_queue<false, 5, false, false>
 #ifdef PTX_AB_BUILD
-                 : occ >= 8  ? trace_queue<false, 8> : occ == 7 ? trace_queue<false, 7>
-                 : occ == 6  ? trace_queue<false, 6>
+                 : occ >= 8  ? trace_queue<false, 8>
+                 : occ == 7  ? (flat ? trace_queue<false, 7, false, true, false, true> : trace_queue<false, 7>)
+                 : occ == 6  ? (flat ? trace_queue<false, 6, false, true, false, true> : trace_queue<false, 6>)
 #endif
                  : occ == 5  ? (flat ? trace_queue<false, 5, false, true, false, true> : trace_queue<false, 5>)
                              : (flat ? trace_queue<false, 4, false, true, false, true> : trace_queue<false, 4>);

@@ -73,7 +73,6 @@ __device__ __forceinline__ void seg_end(const WaveBufs &w, const Seg &g) {
     if (threadIdx.x == 0) {
         w.cnt[(2u * g.round) * w.cnt_stride + g.pj] = *g.l_act;
         w.cnt[(2u * g.round + 1u) * w.cnt_stride + g.pj] = *g.l_ray;
-        if (w.take) w.take[g.round * w.cnt_stride + g.pj] = 0u;  // (trace_queue_w1's batch counter)
     }
 }
 // Padded pixel handled by this thread at offset k of segment j.  A segment is seg_px/64
@@ -121,7 +120,6 @@ __device__ __forceinline__ void job_seg_end(const WaveBufs &w, const Seg &g, con
     if (threadIdx.x == 0) {
         w.cnt[(2u * g.round) * w.cnt_stride + g.pj] = *g.l_act | (*L.l_light << 16);
         w.cnt[(2u * g.round + 1u) * w.cnt_stride + g.pj] = *g.l_ray;
-        if (w.take) w.take[g.round * w.cnt_stride + g.pj] = 0u;
     }
 }
 

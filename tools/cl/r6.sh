@@ -31,14 +31,36 @@ w1)  # one-wave trace workgroups (PTX_AB=TRACE_W1=k, measurement build) and the 
     $G bands $C bands_prod --world 8 --bands "$B5" &&
     PTX_LIB_PATH=$AB EXTRA_AB=TRACE_W1=2 $G bands $C bands_w2 --world 8 --bands "$B5" &&
     PTX_LIB_PATH=$AB EXTRA_AB=TRACE_W1=4 $G bands $C bands_w4 --world 8 --bands "$B5" ;;
+occ)  # the streamed trace kernel at 6 / 7 waves per SIMD now that the A/B batch paths are compiled out
+      # (80 VGPRs + 20 B/lane spilled at 6, 72 + 60 B at 7; round 5: 6 waves spilled 136 B and lost 12 %):
+      # variant build libptx_o6.so (measurement switches on, trace A/B paths off), PTX_AB=TRACE_OCC=n
+    O6=$PWD/pathtracerdemo_amd/libptx_o6.so
+    PTX_LIB_PATH=$O6 PTX_AB=TRACE_OCC=6 $G suite $C/o6 -k "parity or reuse or gi or golden" &&
+    for v in 6 5 7 6 5; do PTX_LIB_PATH=$O6 PTX_AB=TRACE_OCC=$v $G bench $C reuse_o$v --no-cpu-baseline --no-configs3 || exit 1; done &&
+    $G bench $C reuse_prod --no-cpu-baseline --no-configs3 &&
+    for v in 6 5; do PTX_LIB_PATH=$O6 PTX_AB=TRACE_OCC=$v $G bench $C restir_o$v --workload restir --no-cpu-baseline || exit 1; done &&
+    for v in 6 5; do PTX_LIB_PATH=$O6 PTX_AB=TRACE_OCC=$v $G bench $C gi_o$v --workload gi --no-cpu-baseline || exit 1; done &&
+    for v in 6 5; do PTX_LIB_PATH=$O6 PTX_AB=TRACE_OCC=$v $G bench $C mcpt_o$v --workload mcpt --no-cpu-baseline || exit 1; done &&
+    for v in 6 5; do PTX_LIB_PATH=$O6 PTX_AB=TRACE_OCC=$v $G bench $C k4_o$v --frame 3840x2160 --no-cpu-baseline || exit 1; done &&
+    PTX_LIB_PATH=$O6 EXTRA_AB=TRACE_OCC=6 $G bands $C bands_o6 --world 8 --bands "$B5" ;;
 evid)  # round-6 evidence at the current build: GPU suite + smoke, then per workload the shipped-library
-       # profile (tools/gpu.sh profile) and its bench line (CPU baselines, parity window, 4K one-GPU frame)
+       # profile (tools/gpu.sh profile) and its bench line (CPU baselines, parity window, 4K one-GPU frame);
+       # then the one-wave trace workgroups against the same-box product (measurement build, TRACE_W1=2)
+    AB=$PWD/pathtracerdemo_amd/libptx_ab.so
     $G suite $C && $G smoke $C &&
-    for wl in reuse gi restir mcpt; do
+    for wl in reuse restir; do
         $G profile $C/prof_$wl --workload $wl && $G bench $C $wl --workload $wl || exit 1
-    done ;;
-evid2)  # lane use per traversal region (measurement build), the moving camera, the DYN coverage run
-        # (ADVICE r5), and configs[3]'s bands at this build (the r5 cut, then one measured re-cut)
+    done &&
+    PTX_LIB_PATH=$AB PTX_AB=TRACE_W1=2 $G bench $C reuse_w2 --no-cpu-baseline --no-configs3 &&
+    PTX_LIB_PATH=$AB PTX_AB=TRACE_W1=0 $G bench $C reuse_w0 --no-cpu-baseline --no-configs3 &&
+    $G bench $C reuse_prod --no-cpu-baseline --no-configs3 &&
+    PTX_LIB_PATH=$AB PTX_AB=TRACE_W1=2 $G bench $C restir_w2 --workload restir --no-cpu-baseline &&
+    $G bench $C restir_prod --workload restir --no-cpu-baseline ;;
+evid2)  # the other two workloads' evidence, lane use per traversal region (measurement build), the moving
+        # camera, the DYN coverage run, and configs[3]'s bands (the r5 cut, one measured re-cut)
+    for wl in gi mcpt; do
+        $G profile $C/prof_$wl --workload $wl && $G bench $C $wl --workload $wl || exit 1
+    done &&
     PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so $G simd $C reuse &&
     PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so $G simd $C restir &&
     $G bench $C camera --camera-path --no-configs3 &&
