@@ -29,6 +29,14 @@ rows = [
      lambda d, w: f"{d['roofline']['avg_launch_ms']:.3f} / {stats[w][1]:.3f} ms" if w in stats else "–"),
     ("algorithmic bytes per launch", lambda d, w: f"{d['roofline']['alg_bytes_per_launch'] / 1e9:.2f} GB"),
     ("roofline frac (`trace_queue`)", lambda d, w: f"**{d['roofline']['frac']:.3f}**"),
+    ("the same bytes over the rocprof average",
+     lambda d, w: f"{d['roofline']['alg_bytes_per_launch'] / (stats[w][1] * 1e-3) / 8e12:.3f}" if w in stats else "–"),
+    ("L2 request bytes per launch (frac of ≈34.5 TB/s; hit rate)",
+     lambda d, w: (f"{lim['l2_bytes_per_launch'] / 1e6:.0f} MB ({lim['l2_frac']:.3f}; {lim['l2_hit_rate']:.2f})"
+                   if (lim := d['roofline'].get('limiters') or {}).get('l2_bytes_per_launch') else "–")),
+    ("node-loop lane use (SIMD-utilisation build)",
+     lambda d, w: f"{(d['roofline'].get('limiters') or {}).get('node_loop_lane_util'):.3f}"
+     if (d['roofline'].get('limiters') or {}).get('node_loop_lane_util') is not None else "–"),
     ("frame-level frac (§8d)", lambda d, w: f"{d['roofline']['frame']['frac']:.3f}"),
     ("HBM traffic per trace launch (PMC)",
      lambda d, w: f"{d['roofline']['traffic'] / 1e6:.0f} MB" if d['roofline'].get('traffic') else "–"),
