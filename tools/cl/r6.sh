@@ -3,6 +3,7 @@
 set -o pipefail
 G="bash tools/gpu.sh"
 C=r6/$1
+mkdir -p gpurun_out/$C
 # configs[3]'s 8 bands at the round-5 last build's measured cut (profiles/r5/bands/last_build_recut.jsonl)
 B5='[[0, 572], [572, 750], [750, 895], [895, 1059], [1059, 1281], [1281, 1534], [1534, 1778], [1778, 2160]]'
 case "$1" in
@@ -43,6 +44,13 @@ occ)  # the streamed trace kernel at 6 / 7 waves per SIMD now that the A/B batch
     for v in 6 5; do PTX_LIB_PATH=$O6 PTX_AB=TRACE_OCC=$v $G bench $C mcpt_o$v --workload mcpt --no-cpu-baseline || exit 1; done &&
     for v in 6 5; do PTX_LIB_PATH=$O6 PTX_AB=TRACE_OCC=$v $G bench $C k4_o$v --frame 3840x2160 --no-cpu-baseline || exit 1; done &&
     PTX_LIB_PATH=$O6 EXTRA_AB=TRACE_OCC=6 $G bands $C bands_o6 --world 8 --bands "$B5" ;;
+tail)  # per-wave timing of the launch-timed region (diagnostic build libptx_wgt.so): how full each trace
+       # launch keeps the chip, 1080p reuse / C1 ReSTIR and the 4K frame
+    W=$PWD/pathtracerdemo_amd/libptx_wgt.so
+    PTX_AB=WGT PTX_LIB_PATH=$W timeout -k 10 300 python -u tools/wave_timeline.py --single-stream > gpurun_out/$C/reuse.txt 2>&1 &&
+    PTX_AB=WGT PTX_LIB_PATH=$W timeout -k 10 300 python -u tools/wave_timeline.py --single-stream --pipeline restir --scene dummy_scene_1 > gpurun_out/$C/restir.txt 2>&1 &&
+    PTX_AB=WGT PTX_LIB_PATH=$W timeout -k 10 300 python -u tools/wave_timeline.py --single-stream --width 3840 --height 2160 > gpurun_out/$C/reuse4k.txt 2>&1 &&
+    grep -A12 "trace launches" gpurun_out/$C/*.txt ;;
 evid)  # round-6 evidence at the current build: GPU suite + smoke, then per workload the shipped-library
        # profile (tools/gpu.sh profile) and its bench line (CPU baselines, parity window, 4K one-GPU frame);
        # then the one-wave trace workgroups against the same-box product (measurement build, TRACE_W1=2)

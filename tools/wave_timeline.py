@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--bin-us", type=float, default=20.0)
     ap.add_argument("--frames", type=int, default=1, help="frames in the measured window (pipelined frames overlap)")
+    ap.add_argument("--single-stream", action="store_true",
+                    help="one launch sequence, one frame in flight (PTX_FLAG_SINGLE_STREAM): the launch-timed "
+                         "region of bench.py; prints each trace launch's fill (wave-us over span x 5120 slots)")
     a = ap.parse_args()
     assert "WGT" in os.environ.get("PTX_AB", "") and "wgt" in os.environ.get("PTX_LIB_PATH", ""), \
         "run with PTX_AB=WGT PTX_LIB_PATH=<libptx_wgt.so>"
@@ -38,7 +41,7 @@ def main():
     lib = N.load()
     lib.ptx_diag_wave_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     lib.ptx_diag_wave_times.restype = ctypes.c_int
-    r = Renderer(a.width, a.height, device=0, pipeline=a.pipeline)
+    r = Renderer(a.width, a.height, device=0, pipeline=a.pipeline, single_stream=a.single_stream)
     r.Initialize(compile_scene(a.scene))
     for _ in range(3):
         r.Update()
@@ -95,6 +98,29 @@ def main():
         if d is not None and len(d):
             msg += f"  waves {len(d):7d}  dur p50 {np.percentile(d,50):7.1f} p90 {np.percentile(d,90):7.1f} p99 {np.percentile(d,99):7.1f} max {d.max():7.1f} us"
         print(msg)
+    if a.single_stream:  # trace launches one after another: split them at gaps in the waves' starts
+        tk = [k for k, v in KIDS.items() if v == "trace"][0]
+        m = kid == tk
+        order = np.argsort(s[m])
+        ts, te = s[m][order], e[m][order]
+        cap = 256 * 4 * 5  # CUs x SIMDs x the streamed trace kernel's waves per SIMD
+        launches, lo, end = [], 0, te[0]
+        for i in range(1, len(ts) + 1):
+            if i == len(ts) or ts[i] > end:
+                launches.append((lo, i))
+                if i < len(ts):
+                    lo, end = i, te[i]
+            else:
+                end = max(end, te[i])
+        print("trace launches (single stream): span, waves, fill = wave-us / (span x %d), time after the "
+              "first wave end until the last (tail)" % cap)
+        for lo, hi in launches:
+            s0, e1 = ts[lo:hi].min(), te[lo:hi].max()
+            d = te[lo:hi] - ts[lo:hi]
+            first_end = te[lo:hi].min()
+            p90_end = np.percentile(te[lo:hi], 90)
+            print(f"  start {s0:8.1f} span {e1 - s0:7.1f} us  waves {hi - lo:6d}  fill {d.sum() / ((e1 - s0) * cap):.3f}  "
+                  f"90% of waves done at {p90_end - s0:7.1f} us, last at {e1 - s0:7.1f}")
     print("timeline (resident waves per 20 us bin; T = trace, L = logic):")
     tr = occ.get("trace", np.zeros(nb))
     lg = total - tr
