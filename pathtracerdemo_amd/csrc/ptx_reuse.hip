@@ -316,10 +316,10 @@ __device__ __forceinline__ void job_finish(const Seg &g, const JobLists &JL, con
 // -3.2 %, TEST_MCPT -10 % (tools/cl/lw5_ab.sh)
 #define JOB_STEP_WAVES 4
 #endif
-__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(JOB_STEP_WAVES, 8)))
-void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
-    PTX_WAVE_TIMER(sc, KID_JOB_STEP | (w.seg_base ? 0x80u : 0u));
-    __shared__ uint32_t lds[3];
+// One job step of this workgroup's segment (wjob_step, and the fused spatial rounds below);
+// `lds` = 3 words of LDS.  Returns the segment's ray count for the next trace round.
+__device__ __forceinline__ uint32_t job_step_segment(const Scene &sc, const WaveBufs &w, uint32_t round,
+                                                     const ReuseArgs &A, uint32_t *lds) {
     const JobLists JL = job_lists(w, lds);
     const Seg g = seg_begin(w, round, lds);
     uint32_t nh;
@@ -381,6 +381,13 @@ void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
         job_finish(g, JL, A, live, s, jid);
     }
     job_seg_end(w, g, JL);
+    return *g.l_ray;  // (stable after job_seg_end's barrier)
+}
+__global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(JOB_STEP_WAVES, 8)))
+void wjob_step(Scene sc, WaveBufs w, uint32_t round, ReuseArgs A) {
+    PTX_WAVE_TIMER(sc, KID_JOB_STEP | (w.seg_base ? 0x80u : 0u));
+    __shared__ uint32_t lds[3];
+    (void)job_step_segment(sc, w, round, A, lds);
 }
 
 __device__ __forceinline__ uint32_t reuse_seed(const Scene &sc, uint32_t x, uint32_t y, uint32_t salt) {

@@ -51,6 +51,17 @@ tail)  # per-wave timing of the launch-timed region (diagnostic build libptx_wgt
     PTX_AB=WGT PTX_LIB_PATH=$W timeout -k 10 300 python -u tools/wave_timeline.py --single-stream --pipeline restir --scene dummy_scene_1 > gpurun_out/$C/restir.txt 2>&1 &&
     PTX_AB=WGT PTX_LIB_PATH=$W timeout -k 10 300 python -u tools/wave_timeline.py --single-stream --width 3840 --height 2160 > gpurun_out/$C/reuse4k.txt 2>&1 &&
     grep -A12 "trace launches" gpurun_out/$C/*.txt ;;
+fused)  # the spatial pass's {trace, step} rounds as ONE launch (wspatial_rounds; PTX_AB=SPATIAL_FUSED=1, band
+        # handles only with =2): variant build libptx_fu.so (switches on, trace A/B paths off) -- the reuse /
+        # band / loopback GPU tests under it, then the headline and configs[3]'s bands against fused = 0
+    FU=$PWD/pathtracerdemo_amd/libptx_fu.so
+    PTX_LIB_PATH=$FU PTX_AB=SPATIAL_FUSED=1 $G suite $C/f1 -k "reuse or bands or loopback or golden or parity" &&
+    for v in 1 0 1 0; do PTX_LIB_PATH=$FU PTX_AB=SPATIAL_FUSED=$v $G bench $C reuse_f$v --no-cpu-baseline --no-configs3 || exit 1; done &&
+    for v in 1 0; do PTX_LIB_PATH=$FU PTX_AB=SPATIAL_FUSED=$v $G bench $C k4_f$v --frame 3840x2160 --no-cpu-baseline || exit 1; done &&
+    PTX_LIB_PATH=$FU EXTRA_AB=SPATIAL_FUSED=2 $G bands $C bands_f2 --world 8 --bands "$B5" &&
+    PTX_LIB_PATH=$FU EXTRA_AB=SPATIAL_FUSED=0 $G bands $C bands_f0 --world 8 --bands "$B5" ;;
+verify)  # the build after the A/Bs were removed: GPU suite + smoke + the default bench line, then the tail case
+    $G suite $C && $G smoke $C && $G bench $C reuse && bash tools/cl/r6.sh tail ;;
 evid)  # round-6 evidence at the current build: GPU suite + smoke, then per workload the shipped-library
        # profile (tools/gpu.sh profile) and its bench line (CPU baselines, parity window, 4K one-GPU frame);
        # then the one-wave trace workgroups against the same-box product (measurement build, TRACE_W1=2)
