@@ -1211,7 +1211,10 @@ __global__ __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(LOGIC_WAVES,
 // trace_queue's grid: trace_split workgroups per segment
 static inline bool trace_dyn(const WaveBufs &w) { return kAbBuild && w.dyn != nullptr && w.seg_count <= kDynMaxSlots; }
 static inline uint32_t trace_grid(const WaveBufs &w) {
-    return trace_dyn(w) ? std::min(w.seg_count, kDynMaxGroups) : w.seg_count * w.trace_split;
+    // (PTX_AB=DYN_GROUPS=n: A/B -- the cap dates from the 4-wave trace; at 5 waves per SIMD the chip
+    // holds 1280 trace workgroups)
+    static const uint32_t groups = (uint32_t)ab_knob("DYN_GROUPS", (int)kDynMaxGroups);
+    return trace_dyn(w) ? std::min(w.seg_count, groups) : w.seg_count * w.trace_split;
 }
 
 hipError_t wave_trace(const Scene &sc, const WaveBufs &w_in, int round, int eps_mode, uint32_t depth, hipStream_t s,

@@ -60,6 +60,14 @@ fused)  # the spatial pass's {trace, step} rounds as ONE launch (wspatial_rounds
     for v in 1 0; do PTX_LIB_PATH=$FU PTX_AB=SPATIAL_FUSED=$v $G bench $C k4_f$v --frame 3840x2160 --no-cpu-baseline || exit 1; done &&
     PTX_LIB_PATH=$FU EXTRA_AB=SPATIAL_FUSED=2 $G bands $C bands_f2 --world 8 --bands "$B5" &&
     PTX_LIB_PATH=$FU EXTRA_AB=SPATIAL_FUSED=0 $G bands $C bands_f0 --world 8 --bands "$B5" ;;
+dyn)  # dynamic trace batches with the workgroup cap of the 5-wave trace (PTX_AB=TRACE_DYN=1,DYN_GROUPS=1280;
+      # round 5 measured them at the 4-wave cap of 1024 workgroups) against static slots, measurement build
+    AB=$PWD/pathtracerdemo_amd/libptx_ab.so
+    for v in "TRACE_DYN=1,DYN_GROUPS=1280" "TRACE_DYN=0" "TRACE_DYN=1,DYN_GROUPS=1024" "TRACE_DYN=1,DYN_GROUPS=1280" "TRACE_DYN=0"; do
+        PTX_LIB_PATH=$AB PTX_AB=$v $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; done &&
+    for v in "TRACE_DYN=1,DYN_GROUPS=1280" "TRACE_DYN=0"; do
+        PTX_LIB_PATH=$AB PTX_AB=$v $G bench $C restir_$v --workload restir --no-cpu-baseline || exit 1; done &&
+    PTX_LIB_PATH=$AB EXTRA_AB=TRACE_DYN=1,DYN_GROUPS=1280 $G bands $C bands_dyn1280 --world 8 --bands "$B5" ;;
 verify)  # the build after the A/Bs were removed: GPU suite + smoke + the default bench line, then the tail case
     $G suite $C && $G smoke $C && $G bench $C reuse && bash tools/cl/r6.sh tail ;;
 evid)  # round-6 evidence at the current build: GPU suite + smoke, then per workload the shipped-library
