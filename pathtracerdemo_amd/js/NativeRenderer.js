@@ -205,10 +205,17 @@ class NativeRenderer {
   startPresent() {
     const ctx = this.context2D();
     const w = this.Canvas.width, h = this.Canvas.height;
-    const image = ctx.createImageData(w, h);
-    addon.presentAsync(this.Handle, w, h, false);
-    this.PresentInFlight = { serial: this.RenderSerial, image, handle: this.Handle };
     this.PresentWanted = false;
+    if (!(w > 0 && h > 0)) return;  // (nothing to paint on an empty canvas)
+    let image;
+    try {
+      image = ctx.createImageData(w, h);
+      addon.presentAsync(this.Handle, w, h, false);
+    } catch (e) {  // painting never breaks the render loop: the error is kept for the host to read
+      this.PresentError = e;
+      return;
+    }
+    this.PresentInFlight = { serial: this.RenderSerial, image, handle: this.Handle };
     soon(() => this.pollPresent(0));
   }
 

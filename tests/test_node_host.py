@@ -24,7 +24,7 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
 EXPORTS = ["abiVersion", "create", "uploadScene", "setFrame", "render", "renderAsync", "runPass", "runPasses",
            "resetAccumulation", "synchronize", "getStats", "resetStats", "readBuffer", "writeBuffer",
            "trace", "destroy", "lastError", "renderBands", "renderBandsAsync", "commUniqueId", "commInit",
-           "commInitAll", "rowCensus", "present"]
+           "commInitAll", "rowCensus", "present", "presentAsync", "presentPoll", "buildInfo"]
 
 
 @pytest.fixture(scope="module")
@@ -48,7 +48,7 @@ def test_addon_exports_the_abi():
     assert out.returncode == 0, out.stderr
     keys, abi = json.loads(out.stdout)
     assert sorted(keys) == sorted(EXPORTS)
-    assert abi == 4
+    assert abi == 5
 
 
 def test_js_uniform_matches_python_host(scene1, scene_dir):
