@@ -68,6 +68,9 @@ dyn)  # dynamic trace batches with the workgroup cap of the 5-wave trace (PTX_AB
     for v in "TRACE_DYN=1,DYN_GROUPS=1280" "TRACE_DYN=0"; do
         PTX_LIB_PATH=$AB PTX_AB=$v $G bench $C restir_$v --workload restir --no-cpu-baseline || exit 1; done &&
     PTX_LIB_PATH=$AB EXTRA_AB=TRACE_DYN=1,DYN_GROUPS=1280 $G bands $C bands_dyn1280 --world 8 --bands "$B5" ;;
+rehearse)  # bench.py --gpus 2 on a one-GPU box (gloo + host halo, both ranks on GPU 0): the N > 1 path runs
+    PTX_DIST_BACKEND=gloo PTX_FORCE_DEVICE=0 $G bench $C gpus2 --gpus 2 --halo torch --steps 3 --warmup 1 &&
+    PTX_DIST_BACKEND=gloo PTX_FORCE_DEVICE=0 $G bench $C gpus2_weak --gpus 2 --halo torch --weak --steps 3 --warmup 1 ;;
 verify)  # the build after the A/Bs were removed: GPU suite + smoke + the default bench line, then the tail case
     $G suite $C && $G smoke $C && $G bench $C reuse && bash tools/cl/r6.sh tail ;;
 evid)  # round-6 evidence at the current build: GPU suite + smoke, then per workload the shipped-library
