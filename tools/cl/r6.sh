@@ -96,6 +96,16 @@ evid2)  # the other two workloads' evidence, lane use per traversal region (meas
     $G bench $C camera --camera-path --no-configs3 &&
     PTX_LIB_PATH=$PWD/pathtracerdemo_amd/libptx_ab.so PTX_AB=TRACE_DYN=1 $G suite $C/dyn -k "parity or reuse" &&
     $G bands $C bands --world 8 --bands "$B5" --recut 1 ;;
+edge)  # band frames with the edge rows' temporal combine first, the exchange leaving beside the interior
+       # rows' combine (PTX_AB=EDGE_FIRST=1, measurement build): band / loopback GPU tests, then bands
+       # (lost, removed: DESIGN.md §9 item 1)
+    AB=$PWD/pathtracerdemo_amd/libptx_ab.so
+    PTX_LIB_PATH=$AB PTX_AB=EDGE_FIRST=1 $G suite $C/e1 -k "bands or loopback or golden" &&
+    $G bands $C base --world 8 --bands "$B5" &&
+    PTX_LIB_PATH=$AB EXTRA_AB=EDGE_FIRST=1 $G bands $C edge1 --world 8 --bands "$B5" &&
+    PTX_LIB_PATH=$AB EXTRA_AB=EDGE_FIRST=0 $G bands $C edge0 --world 8 --bands "$B5" &&
+    PTX_LIB_PATH=$AB EXTRA_AB=EDGE_FIRST=1 $G bands $C edge1b --world 8 --bands "$B5" &&
+    $G bands $C base2 --world 8 --bands "$B5" ;;
 *)
     echo "unknown case $1"; exit 2 ;;
 esac
