@@ -106,6 +106,23 @@ edge)  # band frames with the edge rows' temporal combine first, the exchange le
     PTX_LIB_PATH=$AB EXTRA_AB=EDGE_FIRST=0 $G bands $C edge0 --world 8 --bands "$B5" &&
     PTX_LIB_PATH=$AB EXTRA_AB=EDGE_FIRST=1 $G bands $C edge1b --world 8 --bands "$B5" &&
     $G bands $C base2 --world 8 --bands "$B5" ;;
+seeds)  # the spatial start reading a neighbour's seeds from the summaries' 8-byte seed plane instead of
+        # its reservoir line: GPU suite, then the headline / 4K / bands against the previous build
+        # (libptx_prev.so = the library before the change; no gain, removed: DESIGN.md §9 item 5)
+    P=$PWD/pathtracerdemo_amd/libptx_prev.so
+    $G suite $C &&
+    for v in new prev new prev; do
+        if [ $v = new ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1
+        else PTX_LIB_PATH=$P $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; fi
+    done &&
+    $G bench $C k4_new --frame 3840x2160 --no-cpu-baseline && PTX_LIB_PATH=$P $G bench $C k4_prev --frame 3840x2160 --no-cpu-baseline &&
+    $G bench $C cam_new --camera-path --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$P $G bench $C cam_prev --camera-path --no-cpu-baseline --no-configs3 &&
+    $G bands $C bands_new --world 8 --bands "$B5" && PTX_LIB_PATH=$P $G bands $C bands_prev --world 8 --bands "$B5" ;;
+sq)  # where the logic kernels' wave cycles go (SQ counters, shipped library, profile region)
+    $G sq $C/reuse && python3 tools/sq_table.py gpurun_out/$C/reuse/pmc_sq/run_counter_collection.csv ;;
+camprof)  # the moving camera's kernels (profile region, shipped library) and their SQ counters
+    $G profile $C/prof_cam --camera-path --no-configs3 && $G sq $C/sq_cam --camera-path --no-configs3 &&
+    python3 tools/sq_table.py gpurun_out/$C/sq_cam/pmc_sq/run_counter_collection.csv ;;
 *)
     echo "unknown case $1"; exit 2 ;;
 esac

@@ -16,6 +16,7 @@
 #                               OUT/NAME.jsonl; PROXY_US (default 110) sets the exchange stand-in,
 #                               EXTRA_AB more PTX_AB switches (with PTX_LIB_PATH=.../libptx_ab.so)
 #   simd    OUT WORKLOAD        lane use per traversal region (tools/simd_util.py; measurement build)
+#   sq      OUT [bench.py args] one --pmc pass of SQ wave-cycle / instruction counters (profile region)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 1
@@ -66,6 +67,16 @@ profile)
     timeout -s KILL 120 rocprofv3 --pmc TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum -d "$P/pmc_calib" -o run --output-format csv -- \
         python3 "$R/tools/l2_calib.py" > "$P/l2_calib.log" 2>&1 || { echo "l2 calib rc=$?"; tail -5 "$P/l2_calib.log"; exit 1; }
     echo "l2 calib ok" ;;
+sq)  # one --pmc pass of 8 SQ counters over the profile region (wave cycles: parked / issue-stalled /
+     # issuing; instruction mix) -> OUT/pmc_sq/; tools/sq_table.py summarises it per kernel
+    cd /tmp && export TMPDIR=/tmp
+    P="$R/$O"
+    unset PTX_AB PTX_LIB_PATH
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR -d "$P/pmc_sq" -o run --output-format csv -- \
+        python3 "$R/bench.py" --profile-region --steps 5 --warmup 1 "$@" > "$P/bench_sq.log" 2>&1 \
+        || { echo "pmc sq rc=$?"; tail -5 "$P/bench_sq.log"; exit 1; }
+    echo "pmc sq ok" ;;
 bands)
     name=$1
     shift
