@@ -118,8 +118,10 @@ seeds)  # the spatial start reading a neighbour's seeds from the summaries' 8-by
     $G bench $C k4_new --frame 3840x2160 --no-cpu-baseline && PTX_LIB_PATH=$P $G bench $C k4_prev --frame 3840x2160 --no-cpu-baseline &&
     $G bench $C cam_new --camera-path --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$P $G bench $C cam_prev --camera-path --no-cpu-baseline --no-configs3 &&
     $G bands $C bands_new --world 8 --bands "$B5" && PTX_LIB_PATH=$P $G bands $C bands_prev --world 8 --bands "$B5" ;;
-sq)  # where the logic kernels' wave cycles go (SQ counters, shipped library, profile region)
-    $G sq $C/reuse && python3 tools/sq_table.py gpurun_out/$C/reuse/pmc_sq/run_counter_collection.csv ;;
+sq)  # where the logic kernels' wave cycles go (SQ counters, shipped library, profile region), still and moving
+    $G sq $C/reuse && python3 tools/sq_table.py gpurun_out/$C/reuse/pmc_sq/run_counter_collection.csv &&
+    $G profile $C/prof_cam --camera-path --no-configs3 && $G sq $C/sq_cam --camera-path --no-configs3 &&
+    python3 tools/sq_table.py gpurun_out/$C/sq_cam/pmc_sq/run_counter_collection.csv ;;
 camprof)  # the moving camera's kernels (profile region, shipped library) and their SQ counters
     $G profile $C/prof_cam --camera-path --no-configs3 && $G sq $C/sq_cam --camera-path --no-configs3 &&
     python3 tools/sq_table.py gpurun_out/$C/sq_cam/pmc_sq/run_counter_collection.csv ;;
