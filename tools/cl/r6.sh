@@ -125,6 +125,8 @@ sq)  # where the logic kernels' wave cycles go (SQ counters, shipped library, pr
 camprof)  # the moving camera's kernels (profile region, shipped library) and their SQ counters
     $G profile $C/prof_cam --camera-path --no-configs3 && $G sq $C/sq_cam --camera-path --no-configs3 &&
     python3 tools/sq_table.py gpurun_out/$C/sq_cam/pmc_sq/run_counter_collection.csv ;;
+final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
+    $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)
     echo "unknown case $1"; exit 2 ;;
 esac
