@@ -125,6 +125,16 @@ sq)  # where the logic kernels' wave cycles go (SQ counters, shipped library, pr
 camprof)  # the moving camera's kernels (profile region, shipped library) and their SQ counters
     $G profile $C/prof_cam --camera-path --no-configs3 && $G sq $C/sq_cam --camera-path --no-configs3 &&
     python3 tools/sq_table.py gpurun_out/$C/sq_cam/pmc_sq/run_counter_collection.csv ;;
+motion)  # the motion start slot-major (one job per thread and iteration: 104 B/lane spilled instead of
+         # 164 at 3 waves; libptx_m2.so at 2 waves, 36 B) against the previous build (libptx_prev.so)
+         # (lost 1-2 %, removed: DESIGN.md §9 item 4)
+    P=$PWD/pathtracerdemo_amd/libptx_prev.so; M2=$PWD/pathtracerdemo_amd/libptx_m2.so
+    $G suite $C -k "reuse or motion or camera or bands or loopback or golden or parity" &&
+    for v in new prev m2 new prev m2; do
+        case $v in new) L= ;; prev) L=$P ;; m2) L=$M2 ;; esac
+        PTX_LIB_PATH=$L $G bench $C cam_$v --camera-path --no-cpu-baseline --no-configs3 || exit 1
+    done &&
+    $G bench $C reuse_new --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$P $G bench $C reuse_prev --no-cpu-baseline --no-configs3 ;;
 final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
     $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)
