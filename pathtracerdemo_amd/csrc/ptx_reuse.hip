@@ -100,6 +100,8 @@ __device__ __forceinline__ void job_store(const ReuseArgs &A, uint32_t jid, cons
     st[JS_PREV * n + jid] = make_float4(s.prev.x, s.prev.y, s.prev.z, s.rr_p);
     st[JS_RRF * n + jid] = make_float4(s.rr_f.x, s.rr_f.y, s.rr_f.z, 0.0f);
 }
+// (every field is assigned once, after the layouts' branches: stores of different fields sunk into
+// one store with a selected address kept the job in scratch memory -- 32 B/lane in wjob_step)
 __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, uint32_t jid, Job &s) {
     const size_t n = A.njobs;
     const float4 *st = A.jstate;
@@ -107,30 +109,38 @@ __device__ __forceinline__ void job_load(const Scene &sc, const ReuseArgs &A, ui
     const uint32_t hw = asu(hd.x);
     job_unhw(s, hw);
     s.idx = asu(hd.z); s.ref = (int32_t)asu(hd.w);
-    if (hw & kJobFresh) {  // the fresh layout: gather what it leaves out (same bits)
+    s.prod = fv.w;
+    const bool fresh = (hw & kJobFresh) != 0u;
+    uint32_t seed1 = asu(hd.y), matref = 0u;
+    int32_t dom = s.dom;
+    f3 f = mk(fv.x, fv.y, fv.z), rr_f = mk(0.0f, 0.0f, 0.0f), prev = rr_f;
+    float beta = 0.0f, rr_p = 0.0f;
+    Surface cur{};
+    if (fresh) {  // the fresh layout: gather what it leaves out (same bits)
         const float4 rf = st[JS_RRF * n + jid];
-        s.dom = (int32_t)asu(hd.y);
-        s.seed1 = res_of(A, s.ref)[0].y;
-        s.f = mk(1.0f, 1.0f, 1.0f); s.prod = fv.w;
-        s.rr_f = mk(fv.x, fv.y, fv.z);
-        s.beta = rf.x; s.rr_p = rf.y;
-        (void)surf_load(sc, A.surf, s.dom, s.cur, s.matref);  // (a job exists only where it is valid)
-        const int32_t W = (int32_t)sc.width, q = s.dom >= 0 ? s.dom / W : -((-s.dom + W - 1) / W);
-        s.prev = x0_of(sc, (uint32_t)(s.dom - q * W), (uint32_t)((int32_t)sc.row_begin + q));
-        return;
+        dom = (int32_t)asu(hd.y);
+        seed1 = res_of(A, s.ref)[0].y;
+        f = mk(1.0f, 1.0f, 1.0f);
+        rr_f = mk(fv.x, fv.y, fv.z);
+        beta = rf.x; rr_p = rf.y;
+        (void)surf_load(sc, A.surf, dom, cur, matref);  // (a job exists only where it is valid)
+        const int32_t W = (int32_t)sc.width, q = dom >= 0 ? dom / W : -((-dom + W - 1) / W);
+        prev = x0_of(sc, (uint32_t)(dom - q * W), (uint32_t)((int32_t)sc.row_begin + q));
+    } else if (s.phase != 1u) {  // (a job waiting for its Visibility needs HDR and F only)
+        const float4 cu = st[JS_CUR * n + jid], nr = st[JS_NRM * n + jid];
+        const float4 pv = st[JS_PREV * n + jid], rf = st[JS_RRF * n + jid];
+        matref = asu(cu.w);
+        cur.pos = mk(cu.x, cu.y, cu.z);
+        cur.nrm = mk(nr.x, nr.y, nr.z);
+        cur.mat = material_at(sc, matref);
+        beta = nr.w;
+        prev = mk(pv.x, pv.y, pv.z); rr_p = pv.w;
+        rr_f = mk(rf.x, rf.y, rf.z);
     }
-    s.seed1 = asu(hd.y);
-    s.f = mk(fv.x, fv.y, fv.z); s.prod = fv.w;
-    if (s.phase == 1u) return;
-    const float4 cu = st[JS_CUR * n + jid], nr = st[JS_NRM * n + jid];
-    const float4 pv = st[JS_PREV * n + jid], rf = st[JS_RRF * n + jid];
-    s.matref = asu(cu.w);
-    s.cur.pos = mk(cu.x, cu.y, cu.z);
-    s.cur.nrm = mk(nr.x, nr.y, nr.z);
-    s.cur.mat = material_at(sc, s.matref);
-    s.beta = nr.w;
-    s.prev = mk(pv.x, pv.y, pv.z); s.rr_p = pv.w;
-    s.rr_f = mk(rf.x, rf.y, rf.z);
+    s.seed1 = seed1; s.matref = matref; s.dom = dom;
+    s.f = f; s.rr_f = rr_f; s.prev = prev;
+    s.beta = beta; s.rr_p = rr_p;
+    s.cur = cur;
 }
 
 // PT_1's throughput recursion + Russian roulette at one replayed vertex (oracle rr_step).

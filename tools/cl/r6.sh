@@ -135,6 +135,17 @@ motion)  # the motion start slot-major (one job per thread and iteration: 104 B/
         PTX_LIB_PATH=$L $G bench $C cam_$v --camera-path --no-cpu-baseline --no-configs3 || exit 1
     done &&
     $G bench $C reuse_new --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$P $G bench $C reuse_prev --no-cpu-baseline --no-configs3 ;;
+jobload)  # job_load with one assignment per field (the job no longer kept in scratch: wjob_step 32 -> 12
+          # B/lane, folded spills only) against the previous build (libptx_prev.so)
+    P=$PWD/pathtracerdemo_amd/libptx_prev.so
+    $G suite $C -k "reuse or motion or camera or bands or loopback or golden or parity" &&
+    for v in new prev new prev; do
+        if [ $v = new ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1
+        else PTX_LIB_PATH=$P $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; fi
+    done &&
+    $G bench $C cam_new --camera-path --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$P $G bench $C cam_prev --camera-path --no-cpu-baseline --no-configs3 &&
+    $G bench $C k4_new --frame 3840x2160 --no-cpu-baseline && PTX_LIB_PATH=$P $G bench $C k4_prev --frame 3840x2160 --no-cpu-baseline &&
+    $G bands $C bands_new --world 8 --bands "$B5" && PTX_LIB_PATH=$P $G bands $C bands_prev --world 8 --bands "$B5" ;;
 final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
     $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)
