@@ -146,6 +146,16 @@ jobload)  # job_load with one assignment per field (the job no longer kept in sc
     $G bench $C cam_new --camera-path --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$P $G bench $C cam_prev --camera-path --no-cpu-baseline --no-configs3 &&
     $G bench $C k4_new --frame 3840x2160 --no-cpu-baseline && PTX_LIB_PATH=$P $G bench $C k4_prev --frame 3840x2160 --no-cpu-baseline &&
     $G bands $C bands_new --world 8 --bands "$B5" && PTX_LIB_PATH=$P $G bands $C bands_prev --world 8 --bands "$B5" ;;
+tres)  # tile-coalesced reservoir rows in the temporal combine (tres_load / tres_store) against the
+       # previous build (libptx_prev.so): reuse GPU tests, per-kernel times, headline
+       # (no gain, removed: DESIGN.md §9 item 5)
+    P=$PWD/pathtracerdemo_amd/libptx_prev.so
+    $G suite $C -k "reuse or bands or loopback or golden or parity" &&
+    $G kstats $C/k_new && PTX_LIB_PATH=$P $G kstats $C/k_prev &&
+    for v in new prev new prev; do
+        if [ $v = new ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1
+        else PTX_LIB_PATH=$P $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; fi
+    done ;;
 final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
     $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)

@@ -16,6 +16,7 @@
 #                               OUT/NAME.jsonl; PROXY_US (default 110) sets the exchange stand-in,
 #                               EXTRA_AB more PTX_AB switches (with PTX_LIB_PATH=.../libptx_ab.so)
 #   simd    OUT WORKLOAD        lane use per traversal region (tools/simd_util.py; measurement build)
+#   kstats  OUT [bench.py args] kernel trace + stats of the profile region (PTX_LIB_PATH honoured)
 #   sq      OUT [bench.py args] one --pmc pass of SQ wave-cycle / instruction counters (profile region)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -67,6 +68,14 @@ profile)
     timeout -s KILL 120 rocprofv3 --pmc TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum -d "$P/pmc_calib" -o run --output-format csv -- \
         python3 "$R/tools/l2_calib.py" > "$P/l2_calib.log" 2>&1 || { echo "l2 calib rc=$?"; tail -5 "$P/l2_calib.log"; exit 1; }
     echo "l2 calib ok" ;;
+kstats)  # rocprofv3 --kernel-trace --stats of the profile region only, on the library PTX_LIB_PATH names
+         # (default: the shipped one) -> OUT/trace/; tools/kstats.py prints per-kernel averages
+    cd /tmp && export TMPDIR=/tmp
+    P="$R/$O"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$P/trace" -o run --output-format csv -- \
+        python3 "$R/bench.py" --profile-region --steps 20 --warmup 3 "$@" > "$P/bench_trace.log" 2>&1 \
+        || { echo "kstats rc=$?"; tail -5 "$P/bench_trace.log"; exit 1; }
+    python3 "$R/tools/kstats.py" "$P/trace/run_kernel_stats.csv" ;;
 sq)  # one --pmc pass of 8 SQ counters over the profile region (wave cycles: parked / issue-stalled /
      # issuing; instruction mix) -> OUT/pmc_sq/; tools/sq_table.py summarises it per kernel
     cd /tmp && export TMPDIR=/tmp
