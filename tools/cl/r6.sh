@@ -156,6 +156,22 @@ tres)  # tile-coalesced reservoir rows in the temporal combine (tres_load / tres
         if [ $v = new ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1
         else PTX_LIB_PATH=$P $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; fi
     done ;;
+evid3a)  # the round's last build (job_load fix): GPU suite + smoke, the headline's and C1 ReSTIR's
+         # shipped-library profiles and bench lines, the headline's SQ counters
+    $G suite $C && $G smoke $C &&
+    for wl in reuse restir; do
+        $G profile $C/prof_$wl --workload $wl && $G bench $C $wl --workload $wl || exit 1
+    done &&
+    $G sq $C/sq_reuse && python3 tools/sq_table.py gpurun_out/$C/sq_reuse/pmc_sq/run_counter_collection.csv ;;
+evid3b)  # the same build: GI and TEST_MCPT profiles + lines, lane use (measurement build), the moving
+         # camera, configs[3]'s bands
+    AB=$PWD/pathtracerdemo_amd/libptx_ab.so
+    for wl in gi mcpt; do
+        $G profile $C/prof_$wl --workload $wl && $G bench $C $wl --workload $wl || exit 1
+    done &&
+    PTX_LIB_PATH=$AB $G simd $C reuse && PTX_LIB_PATH=$AB $G simd $C restir &&
+    $G bench $C camera --camera-path --no-configs3 &&
+    $G bands $C bands --world 8 --bands "$B5" ;;
 final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
     $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)
