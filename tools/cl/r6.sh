@@ -172,6 +172,19 @@ evid3b)  # the same build: GI and TEST_MCPT profiles + lines, lane use (measurem
     PTX_LIB_PATH=$AB $G simd $C reuse && PTX_LIB_PATH=$AB $G simd $C restir &&
     $G bench $C camera --camera-path --no-configs3 &&
     $G bands $C bands --world 8 --bands "$B5" ;;
+idc)  # the streamed walk keeping an identity instance's ray transform for the next identity instance
+      # (no repeated transforms / IEEE divisions) against the previous build (libptx_prev.so)
+      # (lost 1-2 %, removed: DESIGN.md §9 item 2)
+    P=$PWD/pathtracerdemo_amd/libptx_prev.so
+    $G suite $C &&
+    $G kstats $C/k_new && PTX_LIB_PATH=$P $G kstats $C/k_prev &&
+    for v in new prev new prev; do
+        if [ $v = new ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1
+        else PTX_LIB_PATH=$P $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; fi
+    done &&
+    for wl in restir gi mcpt; do
+        $G bench $C ${wl}_new --workload $wl --no-cpu-baseline && PTX_LIB_PATH=$P $G bench $C ${wl}_prev --workload $wl --no-cpu-baseline || exit 1
+    done ;;
 final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
     $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)
