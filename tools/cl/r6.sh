@@ -185,6 +185,27 @@ idc)  # the streamed walk keeping an identity instance's ray transform for the n
     for wl in restir gi mcpt; do
         $G bench $C ${wl}_new --workload $wl --no-cpu-baseline && PTX_LIB_PATH=$P $G bench $C ${wl}_prev --workload $wl --no-cpu-baseline || exit 1
     done ;;
+rcfree)  # diagnostic upper bound (wrong results, timing only): the reconnection vertex's surface
+         # reconstruction made free of memory (libptx_rcfree.so, -DPTX_DIAG_RC_FREE) against the product
+    F=$PWD/pathtracerdemo_amd/libptx_rcfree.so
+    $G kstats $C/k_prod && PTX_LIB_PATH=$F $G kstats $C/k_free &&
+    for v in prod free prod free; do
+        if [ $v = prod ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1
+        else PTX_LIB_PATH=$F $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; fi
+    done ;;
+rcrec)  # reconnection-vertex records (ReuseArgs::rc: x_k's surface written beside each summary, read
+        # by the spatial pass's hybrid-shift jobs) against the previous build (libptx_prev.so)
+        # (no gain, removed: DESIGN.md §9, after item 7)
+    P=$PWD/pathtracerdemo_amd/libptx_prev.so
+    $G suite $C &&
+    $G kstats $C/k_new && PTX_LIB_PATH=$P $G kstats $C/k_prev &&
+    for v in new prev new prev; do
+        if [ $v = new ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1
+        else PTX_LIB_PATH=$P $G bench $C reuse_$v --no-cpu-baseline --no-configs3 || exit 1; fi
+    done &&
+    $G bench $C cam_new --camera-path --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$P $G bench $C cam_prev --camera-path --no-cpu-baseline --no-configs3 &&
+    $G bench $C k4_new --frame 3840x2160 --no-cpu-baseline && PTX_LIB_PATH=$P $G bench $C k4_prev --frame 3840x2160 --no-cpu-baseline &&
+    $G bands $C bands_new --world 8 --bands "$B5" && PTX_LIB_PATH=$P $G bands $C bands_prev --world 8 --bands "$B5" ;;
 final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
     $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)
