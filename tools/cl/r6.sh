@@ -206,6 +206,15 @@ rcrec)  # reconnection-vertex records (ReuseArgs::rc: x_k's surface written besi
     $G bench $C cam_new --camera-path --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$P $G bench $C cam_prev --camera-path --no-cpu-baseline --no-configs3 &&
     $G bench $C k4_new --frame 3840x2160 --no-cpu-baseline && PTX_LIB_PATH=$P $G bench $C k4_prev --frame 3840x2160 --no-cpu-baseline &&
     $G bands $C bands_new --world 8 --bands "$B5" && PTX_LIB_PATH=$P $G bands $C bands_prev --world 8 --bands "$B5" ;;
+is5)  # the PT_1 step kernel alone at 5 waves per SIMD (libptx_is5.so, -DINIT_STEP_WAVES=5: 95 VGPRs +
+      # 36 B/lane spilled, against 102 VGPRs at 4) against the product: PT_1 parity, headline, C1 ReSTIR
+    V=$PWD/pathtracerdemo_amd/libptx_is5.so
+    PTX_LIB_PATH=$V $G suite $C/is5 -k "parity or restir or reuse_frames" &&
+    $G kstats $C/k_prod && PTX_LIB_PATH=$V $G kstats $C/k_is5 &&
+    for v in prod is5 prod is5; do
+        if [ $v = prod ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 && $G bench $C restir_$v --workload restir --no-cpu-baseline || exit 1
+        else PTX_LIB_PATH=$V $G bench $C reuse_$v --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$V $G bench $C restir_$v --workload restir --no-cpu-baseline || exit 1; fi
+    done ;;
 final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
     $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)
