@@ -208,6 +208,7 @@ rcrec)  # reconnection-vertex records (ReuseArgs::rc: x_k's surface written besi
     $G bands $C bands_new --world 8 --bands "$B5" && PTX_LIB_PATH=$P $G bands $C bands_prev --world 8 --bands "$B5" ;;
 is5)  # the PT_1 step kernel alone at 5 waves per SIMD (libptx_is5.so, -DINIT_STEP_WAVES=5: 95 VGPRs +
       # 36 B/lane spilled, against 102 VGPRs at 4) against the product: PT_1 parity, headline, C1 ReSTIR
+      # (noise either way, not kept: DESIGN.md §9)
     V=$PWD/pathtracerdemo_amd/libptx_is5.so
     PTX_LIB_PATH=$V $G suite $C/is5 -k "parity or restir or reuse_frames" &&
     $G kstats $C/k_prod && PTX_LIB_PATH=$V $G kstats $C/k_is5 &&
