@@ -133,6 +133,9 @@ def parse():
                          "temporal pass reprojects its history (the interactive case behind the UI)")
     ap.add_argument("--variant", choices=["wave", "simple"], default="wave",
                     help="kernel variant (A/B): wavefront queues, or 1 thread/pixel")
+    ap.add_argument("--no-pmc-traffic", action="store_true",
+                    help="skip the in-run PMC passes that measure roofline.traffic (one GPU): take the traffic "
+                         "of profiles/hbm_traffic.json instead")
     ap.add_argument("--profile-region", action="store_true",
                     help="run ONLY the launch-timed region (one launch sequence, one frame in flight) on the "
                          "shipped library: what rocprofv3 profiles, so its per-kernel averages are the line's "
@@ -199,6 +202,54 @@ def calibrate_band(cs, W, H, pipeline, device, row_begin, row_end, passes, frame
     ms = (time.perf_counter() - t0) / frames * 1e3
     r.close()
     return ms
+
+
+# the timed traversal symbol (every workload since round 5: the flattened walk at 5 waves per SIMD;
+# GI's closest-hit instance, not its any-hit one)
+TIMED_SYMBOL = "trace_queue<false, 5, false, true, false, true"
+
+
+def pmc_traffic(args, W, H):
+    """roofline.traffic measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE:
+    one pass cannot hold both) over the launch-timed region of the same workload, each a child process
+    of this one (`bench.py --profile-region`), per launch of TIMED_SYMBOL: 2 * FETCH_SIZE + WRITE_SIZE
+    bytes (the gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md §HBM; tools/hbm_traffic.py).
+    Returns (bytes per launch, dispatches) or (None, why not)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 is not on PATH"
+    child = [sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--scene", args.scene,
+             "--frame", f"{W}x{H}", "--variant", args.variant, "--profile-region", "--steps", "5", "--warmup", "1",
+             "--no-pmc-traffic"] + (["--camera-path"] if args.camera_path else [])
+    tmp = tempfile.mkdtemp(prefix="ptx_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            print(f"bench.py: in-run PMC pass {ctr}", file=sys.stderr, flush=True)
+            out = os.path.join(tmp, ctr)
+            cmd = ["timeout", "-s", "KILL", "180", exe, "--pmc", ctr, "-d", out, "-o", "run", "--output-format", "csv",
+                   "--"] + child
+            rc = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL).returncode
+            if rc != 0:
+                return None, f"rocprofv3 --pmc {ctr} exited {rc}"
+            xs = []
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for r in csv.DictReader(fh):
+                        if TIMED_SYMBOL in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+                            xs.append(float(r["Counter_Value"]) * 1024.0)
+            if not xs:
+                return None, f"no {ctr} samples of {TIMED_SYMBOL}"
+            vals[ctr] = (sum(xs) / len(xs), len(xs))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return 2.0 * vals["FETCH_SIZE"][0] + vals["WRITE_SIZE"][0], vals["FETCH_SIZE"][1]
 
 
 def band_work(tile_census: np.ndarray, row_begin: int, row_end: int) -> dict:
@@ -495,12 +546,29 @@ def main():
     # excludes only the per-round profile directories)
     key = f"{pipeline}:{args.scene}:{dom}:{W}x{Hb}"
     prof = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    traffic_source = None
     if os.path.exists(prof):
         try:
             entry = json.load(open(prof)).get(key)
             traffic = entry["bytes_per_launch"] if isinstance(entry, dict) else entry
+            if traffic:
+                traffic_source = ("profiles/hbm_traffic.json (" + (entry.get("source", "?") if isinstance(entry, dict)
+                                                                   else "?") + "): an earlier run's PMC passes")
         except Exception:
             traffic = None
+    # measured in this run where the box allows it (one GPU, the timed traversal symbol)
+    if (world == 1 and n_trace and args.variant == "wave" and not args.profile_region
+            and not args.no_pmc_traffic):
+        measured, info = pmc_traffic(args, W, Hb)
+        if measured is not None:
+            traffic = int(round(measured))
+            traffic_source = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (child "
+                              f"processes, launch-timed region, {info} dispatches), 2*FETCH_SIZE + WRITE_SIZE per "
+                              f"launch of {TIMED_SYMBOL}>")
+        elif traffic_source:
+            traffic_source += f"; in-run PMC unavailable: {info}"
+        else:
+            traffic_source = f"in-run PMC unavailable: {info}"
     lim = os.path.join(ROOT, "profiles", "limiters.json")
     if os.path.exists(lim) and n_trace:
         try:
@@ -558,6 +626,7 @@ def main():
         "nonfinite_px": nonfinite,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_source,
                      "avg_launch_ms": round(dom_ms, 4), "alg_bytes_per_launch": int(dom_bytes),
                      "work_per_frame": work, **extra, "limiters": limiters,
                      "frame": {"alg_bytes": int(frame_bytes), "alg_bytes_per_sample": round(frame_bytes / px, 1),

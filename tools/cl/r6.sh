@@ -216,6 +216,9 @@ is5)  # the PT_1 step kernel alone at 5 waves per SIMD (libptx_is5.so, -DINIT_ST
         if [ $v = prod ]; then $G bench $C reuse_$v --no-cpu-baseline --no-configs3 && $G bench $C restir_$v --workload restir --no-cpu-baseline || exit 1
         else PTX_LIB_PATH=$V $G bench $C reuse_$v --no-cpu-baseline --no-configs3 && PTX_LIB_PATH=$V $G bench $C restir_$v --workload restir --no-cpu-baseline || exit 1; fi
     done ;;
+pmcline)  # the default bench line with roofline.traffic measured in the run (child PMC passes)
+    $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 --no-cpu-baseline &&
+    python3 -c "import json; [print(w, json.load(open(f'gpurun_out/$C/{w}.json'))['roofline']['traffic'], json.load(open(f'gpurun_out/$C/{w}.json'))['roofline']['traffic_source']) for w in ('reuse', 'restir')]" ;;
 final)  # the round's last build: GPU suite + smoke + the default bench line + C1 ReSTIR
     $G suite $C && $G smoke $C && $G bench $C reuse && $G bench $C restir --workload restir --no-configs3 ;;
 *)
